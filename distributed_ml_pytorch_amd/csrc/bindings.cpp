@@ -1,0 +1,321 @@
+// Python bindings for the gfx950 kernels. Every op checks device, dtype,
+// contiguity and alignment on the host before launching (a mis-shaped launch
+// of a hand-written kernel must fail loudly here, never fault on the GPU), and
+// launches on the caller's current HIP stream so ops compose with torch
+// streams, events and hipGraph capture.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "launchers.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous() || t.is_contiguous(at::MemoryFormat::ChannelsLast), name,
+              " must be dense (contiguous or channels_last)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name,
+              " must be 16-byte aligned");
+}
+
+void check_flat(const Tensor& t, at::ScalarType dt, int64_t n, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.numel() == n, name, " has ", t.numel(), " elements, expected ", n);
+}
+
+template <typename T>
+T* ptr_or_null(const optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// ----------------------------------------------------------------- optimizer
+void asgd_fused_step(Tensor g, Tensor p, optional<Tensor> acc, optional<Tensor> mom,
+                     optional<Tensor> w16, double lr, double wd, double momentum,
+                     double dampening, bool nesterov) {
+  const int64_t n = p.numel();
+  TORCH_CHECK(n % 4 == 0, "flat arena length must be a multiple of 4");
+  check_flat(p, at::kFloat, n, "p");
+  check_flat(g, at::kFloat, n, "g");
+  if (acc) check_flat(*acc, at::kFloat, n, "acc");
+  if (mom) check_flat(*mom, at::kFloat, n, "mom");
+  if (w16) check_flat(*w16, at::kBFloat16, n, "w16");
+  dmp::launch_asgd_fused_step(g.data_ptr<float>(), p.data_ptr<float>(), ptr_or_null<float>(acc),
+                              ptr_or_null<float>(mom), ptr_or_null<uint16_t>(w16), n, (float)lr,
+                              (float)wd, (float)momentum, (float)dampening, nesterov,
+                              cur_stream());
+}
+
+void ps_apply(Tensor shard, Tensor delta, optional<Tensor> mirror, double scale) {
+  const int64_t n = shard.numel();
+  TORCH_CHECK(n % 4 == 0, "shard length must be a multiple of 4");
+  check_flat(shard, at::kFloat, n, "shard");
+  if (mirror) check_flat(*mirror, at::kBFloat16, n, "mirror");
+  if (delta.scalar_type() == at::kFloat) {
+    check_flat(delta, at::kFloat, n, "delta");
+    dmp::launch_ps_apply_f32(shard.data_ptr<float>(), delta.data_ptr<float>(),
+                             ptr_or_null<uint16_t>(mirror), n, (float)scale, cur_stream());
+  } else {
+    check_flat(delta, at::kBFloat16, n, "delta");
+    dmp::launch_ps_apply_bf16(shard.data_ptr<float>(),
+                              reinterpret_cast<uint16_t*>(delta.data_ptr()),
+                              ptr_or_null<uint16_t>(mirror), n, (float)scale, cur_stream());
+  }
+}
+
+void pull_land(Tensor p, Tensor src, optional<Tensor> acc, optional<Tensor> w16) {
+  const int64_t n = p.numel();
+  TORCH_CHECK(n % 4 == 0, "arena length must be a multiple of 4");
+  check_flat(p, at::kFloat, n, "p");
+  if (acc) check_flat(*acc, at::kFloat, n, "acc");
+  if (w16) check_flat(*w16, at::kBFloat16, n, "w16");
+  if (src.scalar_type() == at::kFloat) {
+    check_flat(src, at::kFloat, n, "src");
+    dmp::launch_pull_land_f32(p.data_ptr<float>(), src.data_ptr<float>(), ptr_or_null<float>(acc),
+                              ptr_or_null<uint16_t>(w16), n, cur_stream());
+  } else {
+    check_flat(src, at::kBFloat16, n, "src");
+    dmp::launch_pull_land_bf16(p.data_ptr<float>(), reinterpret_cast<uint16_t*>(src.data_ptr()),
+                               ptr_or_null<float>(acc), ptr_or_null<uint16_t>(w16), n,
+                               cur_stream());
+  }
+}
+
+void push_handoff(Tensor acc, optional<Tensor> out32, optional<Tensor> out16) {
+  const int64_t n = acc.numel();
+  TORCH_CHECK(n % 4 == 0, "arena length must be a multiple of 4");
+  check_flat(acc, at::kFloat, n, "acc");
+  if (out32) check_flat(*out32, at::kFloat, n, "out32");
+  if (out16) check_flat(*out16, at::kBFloat16, n, "out16");
+  dmp::launch_push_handoff(acc.data_ptr<float>(), ptr_or_null<float>(out32),
+                           ptr_or_null<uint16_t>(out16), n, cur_stream());
+}
+
+void cast_f32_bf16(Tensor src, Tensor dst) {
+  const int64_t n = src.numel();
+  TORCH_CHECK(n % 4 == 0, "length must be a multiple of 4");
+  check_flat(src, at::kFloat, n, "src");
+  check_flat(dst, at::kBFloat16, n, "dst");
+  dmp::launch_cast_f32_bf16(src.data_ptr<float>(), reinterpret_cast<uint16_t*>(dst.data_ptr()), n,
+                            cur_stream());
+}
+
+Tensor sumsq(Tensor x) {
+  const int64_t n = x.numel();
+  TORCH_CHECK(n % 4 == 0, "length must be a multiple of 4");
+  check_flat(x, at::kFloat, n, "x");
+  auto part = at::empty({1024}, x.options());
+  const int g = dmp::launch_sumsq_partial(x.data_ptr<float>(), part.data_ptr<float>(), n,
+                                          cur_stream());
+  return part.narrow(0, 0, g).sum();
+}
+
+// ------------------------------------------------------------ cross-entropy
+std::vector<Tensor> softmax_xent(Tensor logits, Tensor labels, bool want_grad, double smoothing,
+                                 int64_t ignore_index) {
+  check_gpu(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits must be contiguous [B, C]");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous(),
+              "labels must be a contiguous int64 GPU tensor");
+  const int B = (int)logits.size(0), C = (int)logits.size(1);
+  TORCH_CHECK(labels.numel() == B, "labels length mismatch");
+  auto fopt = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({}, fopt);
+  auto hits = at::empty({}, logits.options().dtype(at::kInt));
+  auto row_loss = at::empty({B}, fopt);
+  auto row_hit = at::empty({B}, logits.options().dtype(at::kInt));
+  Tensor dlogits;
+  if (want_grad) dlogits = at::empty_like(logits);
+  const float grad_scale = 1.f / (float)std::max(B, 1);
+  if (logits.scalar_type() == at::kBFloat16) {
+    dmp::launch_softmax_xent_bf16(
+        reinterpret_cast<const uint16_t*>(logits.data_ptr()), labels.data_ptr<int64_t>(),
+        want_grad ? reinterpret_cast<uint16_t*>(dlogits.data_ptr()) : nullptr,
+        row_loss.data_ptr<float>(), row_hit.data_ptr<int>(), loss.data_ptr<float>(),
+        hits.data_ptr<int>(), B, C, grad_scale, (float)smoothing, (int)ignore_index, cur_stream());
+  } else {
+    TORCH_CHECK(logits.scalar_type() == at::kFloat, "logits must be bf16 or f32");
+    dmp::launch_softmax_xent_f32(
+        logits.data_ptr<float>(), labels.data_ptr<int64_t>(),
+        want_grad ? dlogits.data_ptr<float>() : nullptr, row_loss.data_ptr<float>(),
+        row_hit.data_ptr<int>(), loss.data_ptr<float>(), hits.data_ptr<int>(), B, C, grad_scale,
+        (float)smoothing, (int)ignore_index, cur_stream());
+  }
+  return {loss, hits, want_grad ? dlogits : Tensor()};
+}
+
+// ---------------------------------------------------------------- batchnorm
+// x is a channels-last activation (N,C,H,W logical) or a [M, C] matrix.
+int64_t channels_of(const Tensor& x) { return x.dim() == 2 ? x.size(1) : x.size(1); }
+
+void check_nhwc_bf16(const Tensor& x, const char* name) {
+  check_gpu(x, name);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, name, " must be bf16");
+  if (x.dim() == 4) {
+    TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), name, " must be channels_last");
+  } else {
+    TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), name, " must be [M, C] contiguous");
+  }
+}
+
+std::vector<Tensor> bn_fwd(Tensor x, optional<Tensor> res, optional<Tensor> gamma,
+                           optional<Tensor> beta, optional<Tensor> running_mean,
+                           optional<Tensor> running_var, double momentum, double eps,
+                           bool training, bool relu) {
+  check_nhwc_bf16(x, "x");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: C must be a multiple of 8 and <= 2048, got ", C);
+  if (res) {
+    check_nhwc_bf16(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "res shape mismatch");
+  }
+  for (auto* t : {&gamma, &beta, &running_mean, &running_var}) {
+    if (t->has_value()) {
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == C &&
+                      (*t)->is_contiguous(),
+                  "bn affine/running tensors must be contiguous fp32 [C] on the GPU");
+    }
+  }
+  TORCH_CHECK(training || (running_mean && running_var), "eval-mode bn needs running stats");
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto stats = at::empty({4, C}, fopt);
+  const int G = dmp::bn_num_partials(M, (int)C);
+  auto part = at::empty({2 * G * C}, fopt);
+  dmp::launch_bn_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                     res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr,
+                     reinterpret_cast<uint16_t*>(y.data_ptr()), ptr_or_null<float>(gamma),
+                     ptr_or_null<float>(beta), ptr_or_null<float>(running_mean),
+                     ptr_or_null<float>(running_var), stats.data_ptr<float>(),
+                     part.data_ptr<float>(), M, (int)C, (float)momentum, (float)eps, training,
+                     relu, cur_stream());
+  return {y, stats};
+}
+
+std::vector<Tensor> bn_bwd(Tensor x, Tensor dy, optional<Tensor> y, optional<Tensor> gamma,
+                           Tensor stats, optional<Tensor> dgamma, optional<Tensor> dbeta,
+                           bool relu, bool want_dres) {
+  check_nhwc_bf16(x, "x");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: bad C");
+  if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.dim() == 4)
+    dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc_bf16(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "dy shape mismatch");
+  if (relu) {
+    TORCH_CHECK(y.has_value(), "relu backward needs the forward output");
+    check_nhwc_bf16(*y, "y");
+  }
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * C, "bad stats");
+  for (auto* t : {&gamma, &dgamma, &dbeta}) {
+    if (t->has_value()) {
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == C &&
+                      (*t)->is_contiguous(),
+                  "bn gamma/dgamma/dbeta must be contiguous fp32 [C]");
+    }
+  }
+  auto dx = at::empty_like(x);
+  Tensor dres;
+  if (want_dres) dres = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  const int G = dmp::bn_num_partials(M, (int)C);
+  auto part = at::empty({2 * G * C}, fopt);
+  auto coef = at::empty({3, C}, fopt);
+  dmp::launch_bn_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                     reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                     relu ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr,
+                     ptr_or_null<float>(gamma), stats.data_ptr<float>(),
+                     ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta), coef.data_ptr<float>(),
+                     part.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                     want_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr, M,
+                     (int)C, relu, cur_stream());
+  return {dx, want_dres ? dres : Tensor()};
+}
+
+// ------------------------------------------------------------------ pooling
+Tensor gap_fwd(Tensor x) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4, "gap expects NCHW (channels_last) input");
+  const int N = (int)x.size(0), C = (int)x.size(1), HW = (int)(x.size(2) * x.size(3));
+  TORCH_CHECK(C % 8 == 0, "gap: C must be a multiple of 8");
+  auto y = at::empty({N, C}, x.options().memory_format(at::MemoryFormat::Contiguous));
+  dmp::launch_gap_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                      reinterpret_cast<uint16_t*>(y.data_ptr()), N, HW, C, cur_stream());
+  return y;
+}
+
+Tensor gap_bwd(Tensor dy, int64_t H, int64_t W) {
+  dy = dy.contiguous();
+  check_gpu(dy, "dy");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 2, "gap_bwd expects bf16 [N, C]");
+  const int N = (int)dy.size(0), C = (int)dy.size(1);
+  TORCH_CHECK(C % 8 == 0, "gap: C must be a multiple of 8");
+  auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dmp::launch_gap_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                      reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)(H * W), C,
+                      cur_stream());
+  return dx;
+}
+
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4, "maxpool expects 4-D input");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(C % 8 == 0 && K >= 1 && K <= 15, "maxpool: C % 8 == 0 and 1 <= K <= 15");
+  const int Ho = H / (int)K, Wo = W / (int)K;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "maxpool: window larger than input");
+  auto mf = at::MemoryFormat::ChannelsLast;
+  auto y = at::empty({N, C, Ho, Wo}, x.options().memory_format(mf));
+  auto idx = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(mf));
+  dmp::launch_maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                          reinterpret_cast<uint16_t*>(y.data_ptr()), idx.data_ptr<uint8_t>(), N, H,
+                          W, C, (int)K, cur_stream());
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t K) {
+  auto mf = at::MemoryFormat::ChannelsLast;
+  dy = dy.contiguous(mf);
+  check_nhwc_bf16(dy, "dy");
+  TORCH_CHECK(idx.sizes() == dy.sizes() && idx.is_contiguous(mf), "maxpool idx mismatch");
+  const int N = (int)dy.size(0), C = (int)dy.size(1);
+  TORCH_CHECK(dy.size(2) == H / K && dy.size(3) == W / K, "maxpool_bwd: shape mismatch");
+  Tensor dx = (H % K == 0 && W % K == 0)
+                  ? at::empty({N, C, H, W}, dy.options().memory_format(mf))
+                  : at::zeros({N, C, H, W}, dy.options().memory_format(mf));
+  dmp::launch_maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
+                          reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)H, (int)W, C, (int)K,
+                          cur_stream());
+  return dx;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "gfx950 (MI355X) HIP kernels for distributed_ml_pytorch_amd";
+  m.def("asgd_fused_step", &asgd_fused_step, "fused flat ASGD/SGD update");
+  m.def("ps_apply", &ps_apply, "parameter-server delta apply");
+  m.def("pull_land", &pull_land, "land a parameter pull into the worker arena");
+  m.def("push_handoff", &push_handoff, "snapshot+zero the push accumulator");
+  m.def("cast_f32_bf16", &cast_f32_bf16, "flat fp32 -> bf16");
+  m.def("sumsq", &sumsq, "sum of squares of a flat fp32 buffer");
+  m.def("softmax_xent", &softmax_xent, "fused softmax cross entropy fwd+bwd");
+  m.def("bn_fwd", &bn_fwd, "NHWC batchnorm(+residual)(+relu) forward");
+  m.def("bn_bwd", &bn_bwd, "NHWC batchnorm(+residual)(+relu) backward");
+  m.def("gap_fwd", &gap_fwd, "NHWC global average pool forward");
+  m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
+  m.def("maxpool_fwd", &maxpool_fwd, "NHWC KxK/sK max pool forward");
+  m.def("maxpool_bwd", &maxpool_bwd, "NHWC KxK/sK max pool backward");
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,263 @@
+// Channels-last (NHWC) BatchNorm for training, with ReLU and residual-add fused.
+//
+// The reference models have no BatchNorm (/root/reference/example/models.py);
+// it is needed by the BASELINE.json models (ResNet-18/50). Layout is [M, C]
+// bf16 with M = N*H*W, every thread owning 8 consecutive channels (16 B).
+//
+// forward  : stats (partial sums per block) -> finalize (mean/invstd, running
+//            stats, folded scale/shift) -> apply  y = relu(x*scale + shift [+ res])
+// backward : reduce (sum dz, sum dz*xhat with dz = dy*[y>0]) -> finalize
+//            (dgamma/dbeta accumulated straight into the fp32 grad arena, folded
+//            dx coefficients) -> apply  dx = A*dz + Cc*x + Bc  [and dres = dz]
+#include "common.h"
+
+namespace dmp {
+
+__device__ __forceinline__ void load8(const u16* p, float v[8]) {
+  const bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = bf2f(r.v[k]);
+}
+
+__device__ __forceinline__ void store8(u16* p, const float v[8]) {
+  bf16x8 r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r.v[k] = f2bf(v[k]);
+  *reinterpret_cast<bf16x8*>(p) = r;
+}
+
+// -------- per-block channel partial sums --------------------------------
+// MODE 0: s += x, q += x*x                       (forward statistics)
+// MODE 1: s += dz, q += dz*(x-mean)*invstd        (backward reduction)
+template <int MODE, bool RELU>
+__global__ void __launch_bounds__(256) bn_partial_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
+    const float* __restrict__ stats, float* __restrict__ part, long long M, int C) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tpr = C >> 3;
+  const int rpi = 256 / tpr;
+  const int t = threadIdx.x;
+  const int cg = t % tpr, r0 = t / tpr;
+  const long long rows_per_blk = (M + gridDim.x - 1) / gridDim.x;
+  const long long start = (long long)blockIdx.x * rows_per_blk;
+  const long long end = min(M, start + rows_per_blk);
+  float s[8], q[8], mean[8], inv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
+  if (MODE == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { mean[k] = stats[cg * 8 + k]; inv[k] = stats[C + cg * 8 + k]; }
+  }
+  if (r0 < rpi) {
+    for (long long row = start + r0; row < end; row += rpi) {
+      const long long off = row * C + cg * 8;
+      float xv[8];
+      load8(x + off, xv);
+      if (MODE == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s[k] += xv[k]; q[k] += xv[k] * xv[k]; }
+      } else {
+        float g[8];
+        load8(dy + off, g);
+        if (RELU) {
+          float yv[8];
+          load8(y + off, yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] += g[k] * (xv[k] - mean[k]) * inv[k]; }
+      }
+    }
+  }
+  // LDS reduce over the rpi row-lanes that share a channel group.
+  float* ls = smem;            // [rpi][C]
+  float* lq = smem + rpi * C;  // [rpi][C]
+  if (r0 < rpi) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { ls[r0 * C + cg * 8 + k] = s[k]; lq[r0 * C + cg * 8 + k] = q[k]; }
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rpi; ++r) { a += ls[r * C + c]; b += lq[r * C + c]; }
+    part[(long long)blockIdx.x * C + c] = a;
+    part[(long long)(gridDim.x + blockIdx.x) * C + c] = b;
+  }
+}
+
+// -------- forward finalize: stats = [mean | invstd | scale | shift] -------
+__global__ void __launch_bounds__(256) bn_fwd_finalize_kernel(
+    const float* __restrict__ part, int G, long long M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ running_mean,
+    float* __restrict__ running_var, float momentum, float eps, float* __restrict__ stats,
+    int use_running) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float mean, var;
+  if (use_running) {
+    mean = running_mean[c];
+    var = running_var[c];
+  } else {
+    double S = 0.0, Q = 0.0;
+    for (int g = 0; g < G; ++g) { S += part[(long long)g * C + c]; Q += part[(long long)(G + g) * C + c]; }
+    const double dm = S / (double)M;
+    double dv = Q / (double)M - dm * dm;
+    if (dv < 0.0) dv = 0.0;
+    mean = (float)dm;
+    var = (float)dv;
+    if (running_mean) {
+      const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+    }
+  }
+  const float inv = rsqrtf(var + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  const float sc = g * inv;
+  stats[c] = mean;
+  stats[C + c] = inv;
+  stats[2 * C + c] = sc;
+  stats[3 * C + c] = b - mean * sc;
+}
+
+// -------- forward apply --------------------------------------------------
+template <bool RELU, bool RES>
+__global__ void __launch_bounds__(256) bn_apply_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ res, const float* __restrict__ stats,
+    u16* __restrict__ y, long long nvec, int C) {
+  const int tpr = C >> 3;
+  const float* scale = stats + 2 * C;
+  const float* shift = stats + 3 * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int c0 = (int)(v % tpr) * 8;
+    float xv[8];
+    load8(x + v * 8, xv);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = xv[k] * scale[c0 + k] + shift[c0 + k];
+    if (RES) {
+      float rv[8];
+      load8(res + v * 8, rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] += rv[k];
+    }
+    if (RELU) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = fmaxf(o[k], 0.f);
+    }
+    store8(y + v * 8, o);
+  }
+}
+
+// -------- backward finalize: coef = [A | Bc | Cc] -----------------------------
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
+    const float* __restrict__ part, int G, long long M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ stats, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double S = 0.0, Q = 0.0;
+  for (int g = 0; g < G; ++g) { S += part[(long long)g * C + c]; Q += part[(long long)(G + g) * C + c]; }
+  const float db = (float)S;   // sum dz
+  const float dg = (float)Q;   // sum dz * xhat
+  if (dgamma) dgamma[c] += dg;
+  if (dbeta) dbeta[c] += db;
+  const float mean = stats[c], inv = stats[C + c];
+  const float k1 = (gamma ? gamma[c] : 1.f) * inv;
+  const float invM = 1.f / (float)M;
+  // dx = k1*(dz - db/M - xhat*dg/M), xhat = (x-mean)*inv
+  const float Cc = -k1 * inv * dg * invM;
+  const float Bc = -k1 * db * invM - Cc * mean;
+  coef[c] = k1;
+  coef[C + c] = Bc;
+  coef[2 * C + c] = Cc;
+}
+
+template <bool RELU, bool WRITE_DRES>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
+    const float* __restrict__ coef, u16* __restrict__ dx, u16* __restrict__ dres, long long nvec,
+    int C) {
+  const int tpr = C >> 3;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const int c0 = (int)(v % tpr) * 8;
+    float xv[8], g[8];
+    load8(x + v * 8, xv);
+    load8(dy + v * 8, g);
+    if (RELU) {
+      float yv[8];
+      load8(y + v * 8, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    if (WRITE_DRES) store8(dres + v * 8, g);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = coef[c0 + k] * g[k] + coef[2 * C + c0 + k] * xv[k] + coef[C + c0 + k];
+    store8(dx + v * 8, o);
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+int bn_num_partials(long long M, int C) {
+  long long vecs = M * (C / 8);
+  long long g = vecs / (256 * 8);
+  if (g < 1) g = 1;
+  if (g > 1024) g = 1024;
+  if (g > M) g = M;
+  return (int)g;
+}
+
+void launch_bn_fwd(const u16* x, const u16* res, u16* y, const float* gamma, const float* beta,
+                   float* running_mean, float* running_var, float* stats, float* part,
+                   long long M, int C, float momentum, float eps, bool training, bool relu,
+                   hipStream_t s) {
+  const int G = bn_num_partials(M, C);
+  const int rpi = 256 / (C / 8);
+  const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
+  if (training) {
+    hipLaunchKernelGGL((bn_partial_kernel<0, false>), dim3(G), dim3(256), lds, s, x, nullptr,
+                       nullptr, nullptr, part, M, C);
+  }
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, M,
+                     C, gamma, beta, running_mean, running_var, momentum, eps, stats,
+                     training ? 0 : 1);
+  const long long nvec = M * C / 8;
+  const dim3 grid(stream_grid(nvec, 256));
+  if (relu) {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<true, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
+  } else {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<false, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
+  }
+}
+
+void launch_bn_bwd(const u16* x, const u16* dy, const u16* y, const float* gamma,
+                   const float* stats, float* dgamma, float* dbeta, float* coef, float* part,
+                   u16* dx, u16* dres, long long M, int C, bool relu, hipStream_t s) {
+  const int G = bn_num_partials(M, C);
+  const int rpi = 256 / (C / 8);
+  const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
+  if (relu)
+    hipLaunchKernelGGL((bn_partial_kernel<1, true>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, M, C);
+  else
+    hipLaunchKernelGGL((bn_partial_kernel<1, false>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, M, C);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, M,
+                     C, gamma, stats, dgamma, dbeta, coef);
+  const long long nvec = M * C / 8;
+  const dim3 grid(stream_grid(nvec, 256));
+  if (relu) {
+    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), grid, dim3(256), 0, s, x, dy, y, coef, dx, dres, nvec, C);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), grid, dim3(256), 0, s, x, dy, y, coef, dx, dres, nvec, C);
+  } else {
+    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), grid, dim3(256), 0, s, x, dy, y, coef, dx, dres, nvec, C);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), grid, dim3(256), 0, s, x, dy, y, coef, dx, dres, nvec, C);
+  }
+}
+
+}  // namespace dmp

@@ -1,0 +1,72 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of this package.
+//
+// Conventions used by every kernel file:
+//   * wave = 64 lanes (hard-coded, never warpSize tricks from 32-lane hardware);
+//   * bf16 is carried as raw `uint16_t` bits; f32 <-> bf16 via bit arithmetic
+//     (round-to-nearest-even) so memory-bound kernels stay vectorised (16 B/lane);
+//   * every launcher takes an explicit hipStream_t (graph-capturable: no malloc,
+//     no sync inside launch functions).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmp {
+
+constexpr int kWave = 64;
+
+using u16 = uint16_t;
+using u32 = uint32_t;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+struct alignas(16) bf16x8 { u16 v[8]; };
+struct alignas(8) bf16x4 { u16 v[4]; };
+
+__device__ __forceinline__ float bf2f(u16 h) {
+  return __uint_as_float(((u32)h) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16 (NaN kept as a quiet NaN).
+__device__ __forceinline__ u16 f2bf(float f) {
+  u32 u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u16)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (u16)(u >> 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Grid size for a grid-stride memory-bound kernel: enough blocks to fill
+// 256 CUs several times over, capped (Guideline 11).
+inline int stream_grid(long long work_items, int block) {
+  long long g = (work_items + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  return (int)g;
+}
+
+}  // namespace dmp
+
+#define DMP_HIP_CHECK(expr)                                                   \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) {                                                   \
+      throw std::runtime_error(std::string("HIP error: ") +                   \
+                               hipGetErrorString(_e) + " at " __FILE__ ":" + \
+                               std::to_string(__LINE__));                     \
+    }                                                                         \
+  } while (0)

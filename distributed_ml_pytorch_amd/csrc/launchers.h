@@ -1,0 +1,52 @@
+// Host-side launch entry points of the gfx950 kernels (raw pointers + stream).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace dmp {
+
+// optim.hip
+void launch_asgd_fused_step(const float* g, float* p, float* acc, float* mom, uint16_t* w16,
+                            long long n, float lr, float wd, float momentum, float dampening,
+                            bool nesterov, hipStream_t s);
+void launch_ps_apply_f32(float* shard, const float* delta, uint16_t* mirror, long long n,
+                         float scale, hipStream_t s);
+void launch_ps_apply_bf16(float* shard, const uint16_t* delta, uint16_t* mirror, long long n,
+                          float scale, hipStream_t s);
+void launch_pull_land_f32(float* p, const float* src, const float* acc, uint16_t* w16,
+                          long long n, hipStream_t s);
+void launch_pull_land_bf16(float* p, const uint16_t* src, const float* acc, uint16_t* w16,
+                           long long n, hipStream_t s);
+void launch_push_handoff(float* acc, float* out32, uint16_t* out16, long long n, hipStream_t s);
+void launch_cast_f32_bf16(const float* src, uint16_t* dst, long long n, hipStream_t s);
+int launch_sumsq_partial(const float* x, float* partial, long long n, hipStream_t s);
+
+// xent.hip
+void launch_softmax_xent_bf16(const uint16_t* logits, const int64_t* labels, uint16_t* dlogits,
+                              float* row_loss, int* row_hit, float* loss_out, int* hits_out,
+                              int B, int C, float grad_scale, float smoothing, int ignore_index,
+                              hipStream_t s);
+void launch_softmax_xent_f32(const float* logits, const int64_t* labels, float* dlogits,
+                             float* row_loss, int* row_hit, float* loss_out, int* hits_out, int B,
+                             int C, float grad_scale, float smoothing, int ignore_index,
+                             hipStream_t s);
+
+// bn.hip
+int bn_num_partials(long long M, int C);
+void launch_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma,
+                   const float* beta, float* running_mean, float* running_var, float* stats,
+                   float* part, long long M, int C, float momentum, float eps, bool training,
+                   bool relu, hipStream_t s);
+void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const float* gamma,
+                   const float* stats, float* dgamma, float* dbeta, float* coef, float* part,
+                   uint16_t* dx, uint16_t* dres, long long M, int C, bool relu, hipStream_t s);
+
+// pool.hip
+void launch_gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s);
+void launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s);
+void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C,
+                        int K, hipStream_t s);
+void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W,
+                        int C, int K, hipStream_t s);
+
+}  // namespace dmp

@@ -1,0 +1,150 @@
+// NHWC pooling kernels (bf16, 8 channels = 16 B per thread).
+//
+//  * global average pool  [N,H,W,C] -> [N,C]   (ResNet head, avg_pool2d(4) on CIFAR)
+//  * max pool k x k / stride k (non-overlapping windows), with uint8 argmax
+//    indices for the backward scatter.  The reference uses 2x2/s2 max pooling
+//    in both its models (/root/reference/example/models.py:16-17,29,32,41).
+#include "common.h"
+
+namespace dmp {
+
+__global__ void __launch_bounds__(256) gap_fwd_kernel(const u16* __restrict__ x,
+                                                      u16* __restrict__ y, int N, int HW, int C) {
+  const int tpr = C >> 3;
+  const long long total = (long long)N * tpr;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float inv = 1.f / (float)HW;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const long long n = t / tpr;
+    const int cg = (int)(t % tpr);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const u16* base = x + n * HW * C + cg * 8;
+    for (int p = 0; p < HW; ++p) {
+      const bf16x8 r = *reinterpret_cast<const bf16x8*>(base + (long long)p * C);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += bf2f(r.v[k]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(acc[k] * inv);
+    *reinterpret_cast<bf16x8*>(y + n * C + cg * 8) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) gap_bwd_kernel(const u16* __restrict__ dy,
+                                                      u16* __restrict__ dx, int N, int HW, int C) {
+  const int tpr = C >> 3;
+  const long long total = (long long)N * HW * tpr;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float inv = 1.f / (float)HW;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int cg = (int)(t % tpr);
+    const long long n = t / ((long long)HW * tpr);
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>(dy + n * C + cg * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(bf2f(r.v[k]) * inv);
+    *reinterpret_cast<bf16x8*>(dx + t * 8) = o;
+  }
+}
+
+// Max pool, window K x K, stride K, no padding, floor mode.
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const u16* __restrict__ x,
+                                                          u16* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, int N, int H,
+                                                          int W, int C, int K, int Ho, int Wo) {
+  const int tpr = C >> 3;
+  const long long total = (long long)N * Ho * Wo * tpr;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int cg = (int)(t % tpr);
+    long long r = t / tpr;
+    const int wo = (int)(r % Wo); r /= Wo;
+    const int ho = (int)(r % Ho);
+    const long long n = r / Ho;
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+    for (int i = 0; i < K; ++i) {
+      for (int j = 0; j < K; ++j) {
+        const int h = ho * K + i, w = wo * K + j;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((n * H + h) * W + w) * C + cg * 8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float f = bf2f(v.v[k]);
+          if (f > best[k] || (f != f)) { best[k] = f; bi[k] = (uint8_t)(i * K + j); }
+        }
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(best[k]);
+    *reinterpret_cast<bf16x8*>(y + t * 8) = o;
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((u32)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((u32)bi[7] << 24);
+    *reinterpret_cast<uint2*>(idx + t * 8) = packed;
+  }
+}
+
+// dx must be zero-initialised by the caller only when H or W is not a multiple
+// of K (floor mode leaves un-pooled border rows/cols untouched).
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(const u16* __restrict__ dy,
+                                                          const uint8_t* __restrict__ idx,
+                                                          u16* __restrict__ dx, int N, int H,
+                                                          int W, int C, int K, int Ho, int Wo) {
+  const int tpr = C >> 3;
+  const long long total = (long long)N * Ho * Wo * tpr;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int cg = (int)(t % tpr);
+    long long r = t / tpr;
+    const int wo = (int)(r % Wo); r /= Wo;
+    const int ho = (int)(r % Ho);
+    const long long n = r / Ho;
+    const bf16x8 g = *reinterpret_cast<const bf16x8*>(dy + t * 8);
+    const uint2 packed = *reinterpret_cast<const uint2*>(idx + t * 8);
+    uint8_t bi[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { bi[k] = (packed.x >> (8 * k)) & 0xff; bi[4 + k] = (packed.y >> (8 * k)) & 0xff; }
+    for (int i = 0; i < K; ++i) {
+      for (int j = 0; j < K; ++j) {
+        const uint8_t me = (uint8_t)(i * K + j);
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.v[k] = (bi[k] == me) ? g.v[k] : (u16)0;
+        const int h = ho * K + i, w = wo * K + j;
+        *reinterpret_cast<bf16x8*>(dx + ((n * H + h) * W + w) * C + cg * 8) = o;
+      }
+    }
+  }
+}
+
+void launch_gap_fwd(const u16* x, u16* y, int N, int HW, int C, hipStream_t s) {
+  const long long total = (long long)N * (C / 8);
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, x, y, N, HW, C);
+}
+
+void launch_gap_bwd(const u16* dy, u16* dx, int N, int HW, int C, hipStream_t s) {
+  const long long total = (long long)N * HW * (C / 8);
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy, dx, N, HW, C);
+}
+
+void launch_maxpool_fwd(const u16* x, u16* y, uint8_t* idx, int N, int H, int W, int C, int K,
+                        hipStream_t s) {
+  const int Ho = H / K, Wo = W / K;
+  const long long total = (long long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, x, y, idx,
+                     N, H, W, C, K, Ho, Wo);
+}
+
+void launch_maxpool_bwd(const u16* dy, const uint8_t* idx, u16* dx, int N, int H, int W, int C,
+                        int K, hipStream_t s) {
+  const int Ho = H / K, Wo = W / K;
+  const long long total = (long long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy, idx,
+                     dx, N, H, W, C, K, Ho, Wo);
+}
+
+}  // namespace dmp

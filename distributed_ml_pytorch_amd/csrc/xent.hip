@@ -1,0 +1,172 @@
+// Fused softmax-cross-entropy: forward loss + backward dlogits + top-1 hits in
+// ONE pass over the logits (one wave per row, 64-lane shuffle reductions).
+//
+// Replaces the ATen chain _log_softmax -> nll_loss_forward -> nll_loss_backward
+// -> _log_softmax_backward_data -> max that the reference runs per iteration
+// (/root/reference/example/main.py:71-75; op trace in SURVEY.md §2.3).
+//
+// dlogits = (softmax(x) - onehot(y)) * grad_scale  where grad_scale = 1/B for a
+// mean-reduced loss; the autograd wrapper rescales by the incoming grad_output.
+#include "common.h"
+
+namespace dmp {
+
+template <typename T>
+__device__ __forceinline__ float ld(const T* p, long long i);
+template <>
+__device__ __forceinline__ float ld<float>(const float* p, long long i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ld<u16>(const u16* p, long long i) { return bf2f(p[i]); }
+
+template <typename T>
+__device__ __forceinline__ void st(T* p, long long i, float v);
+template <>
+__device__ __forceinline__ void st<float>(float* p, long long i, float v) { p[i] = v; }
+template <>
+__device__ __forceinline__ void st<u16>(u16* p, long long i, float v) { p[i] = f2bf(v); }
+
+// Phase 1: rows [blockIdx.x*rows_per_block, ...). Each wave owns one row at a time.
+// If `fused_finalize` (grid == 1) the same block reduces the row results.
+template <typename T>
+__global__ void __launch_bounds__(1024) softmax_xent_kernel(
+    const T* __restrict__ logits, const int64_t* __restrict__ labels, T* __restrict__ dlogits,
+    float* __restrict__ row_loss, int* __restrict__ row_hit, float* __restrict__ loss_out,
+    int* __restrict__ hits_out, int B, int C, float grad_scale, float label_smoothing,
+    int ignore_index, int rows_per_block, int fused_finalize) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  const int r_begin = blockIdx.x * rows_per_block;
+  const int r_end = min(B, r_begin + rows_per_block);
+  float my_loss = 0.f;
+  int my_hit = 0, my_valid = 0;
+  for (int r = r_begin + wid; r < r_end; r += nw) {
+    const T* x = logits + (long long)r * C;
+    const long long y = labels[r];
+    const bool valid = (y != ignore_index);
+    // pass 1: max + argmax
+    float m = -INFINITY;
+    int am = 0x7fffffff;
+    for (int j = lane; j < C; j += 64) {
+      const float v = ld(x, j);
+      if (v > m || (v == m && j < am)) { m = v; am = j; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(m, o, 64);
+      const int oa = __shfl_xor(am, o, 64);
+      if (om > m || (om == m && oa < am)) { m = om; am = oa; }
+    }
+    // pass 2: sum exp and sum of logits (for label smoothing)
+    float s = 0.f, sx = 0.f;
+    for (int j = lane; j < C; j += 64) {
+      const float v = ld(x, j);
+      s += __expf(v - m);
+      sx += v;
+    }
+    s = wave_sum(s);
+    sx = wave_sum(sx);
+    const float lse = m + __logf(s);
+    const float xy = valid ? ld(x, y) : 0.f;
+    // loss = (1-eps) * (lse - x_y) + eps * (lse - mean(x))
+    const float eps = label_smoothing;
+    const float loss = valid ? ((1.f - eps) * (lse - xy) + eps * (lse - sx / (float)C)) : 0.f;
+    // pass 3: gradient
+    if (dlogits) {
+      T* d = dlogits + (long long)r * C;
+      const float inv_s = 1.f / s;
+      const float smooth = eps / (float)C;
+      for (int j = lane; j < C; j += 64) {
+        float g = 0.f;
+        if (valid) {
+          const float p = __expf(ld(x, j) - m) * inv_s;
+          g = (p - smooth - (j == y ? (1.f - eps) : 0.f)) * grad_scale;
+        }
+        st(d, j, g);
+      }
+    }
+    if (lane == 0) {
+      if (row_loss) row_loss[r] = loss;
+      if (row_hit) row_hit[r] = (valid && am == y) ? 1 : 0;
+      my_loss += loss;
+      my_hit += (valid && am == y) ? 1 : 0;
+      my_valid += valid ? 1 : 0;
+    }
+  }
+  if (!fused_finalize) return;
+  __shared__ float sl[16];
+  __shared__ int sh[16];
+  __shared__ int sv[16];
+  if (lane == 0) { sl[wid] = my_loss; sh[wid] = my_hit; sv[wid] = my_valid; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tl = 0.f; int th = 0, tv = 0;
+    for (int w = 0; w < nw; ++w) { tl += sl[w]; th += sh[w]; tv += sv[w]; }
+    loss_out[0] = tl / (float)max(tv, 1);
+    hits_out[0] = th;
+  }
+}
+
+// Phase 2 for the multi-block path: one block reduces the per-row results.
+__global__ void __launch_bounds__(1024) xent_finalize_kernel(
+    const float* __restrict__ row_loss, const int* __restrict__ row_hit,
+    const int64_t* __restrict__ labels, float* __restrict__ loss_out, int* __restrict__ hits_out,
+    int B, int ignore_index) {
+  __shared__ float sl[16];
+  __shared__ int sh[16], sv[16];
+  float l = 0.f; int h = 0, v = 0;
+  for (int r = threadIdx.x; r < B; r += blockDim.x) {
+    l += row_loss[r]; h += row_hit[r]; v += (labels[r] != ignore_index) ? 1 : 0;
+  }
+  l = wave_sum(l);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { h += __shfl_xor(h, o, 64); v += __shfl_xor(v, o, 64); }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sl[wid] = l; sh[wid] = h; sv[wid] = v; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tl = 0.f; int th = 0, tv = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { tl += sl[w]; th += sh[w]; tv += sv[w]; }
+    loss_out[0] = tl / (float)max(tv, 1);
+    hits_out[0] = th;
+  }
+}
+
+template <typename T>
+void launch_xent_t(const T* logits, const int64_t* labels, T* dlogits, float* row_loss,
+                   int* row_hit, float* loss_out, int* hits_out, int B, int C, float grad_scale,
+                   float smoothing, int ignore_index, hipStream_t s) {
+  // Small problems (every CIFAR/MNIST config): one block, fused finalize.
+  const long long work = (long long)B * C;
+  if (work <= (1 << 20) || B <= 64) {
+    hipLaunchKernelGGL(softmax_xent_kernel<T>, dim3(1), dim3(1024), 0, s, logits, labels, dlogits,
+                       row_loss, row_hit, loss_out, hits_out, B, C, grad_scale, smoothing,
+                       ignore_index, B, 1);
+    return;
+  }
+  const int rows_per_block = 64;
+  const int grid = (B + rows_per_block - 1) / rows_per_block;
+  hipLaunchKernelGGL(softmax_xent_kernel<T>, dim3(grid), dim3(1024), 0, s, logits, labels,
+                     dlogits, row_loss, row_hit, loss_out, hits_out, B, C, grad_scale, smoothing,
+                     ignore_index, rows_per_block, 0);
+  hipLaunchKernelGGL(xent_finalize_kernel, dim3(1), dim3(1024), 0, s, row_loss, row_hit, labels,
+                     loss_out, hits_out, B, ignore_index);
+}
+
+void launch_softmax_xent_bf16(const u16* logits, const int64_t* labels, u16* dlogits,
+                              float* row_loss, int* row_hit, float* loss_out, int* hits_out,
+                              int B, int C, float grad_scale, float smoothing, int ignore_index,
+                              hipStream_t s) {
+  launch_xent_t<u16>(logits, labels, dlogits, row_loss, row_hit, loss_out, hits_out, B, C,
+                     grad_scale, smoothing, ignore_index, s);
+}
+
+void launch_softmax_xent_f32(const float* logits, const int64_t* labels, float* dlogits,
+                             float* row_loss, int* row_hit, float* loss_out, int* hits_out, int B,
+                             int C, float grad_scale, float smoothing, int ignore_index,
+                             hipStream_t s) {
+  launch_xent_t<float>(logits, labels, dlogits, row_loss, row_hit, loss_out, hits_out, B, C,
+                       grad_scale, smoothing, ignore_index, s);
+}
+
+}  // namespace dmp

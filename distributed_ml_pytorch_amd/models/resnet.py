@@ -1,0 +1,123 @@
+"""ResNet family for BASELINE.json configs #2-#4 (ResNet-18 ASGD, ResNet-50 sync DP).
+
+Not present in the reference (its models are LeNet/AlexNet only);
+the north-star metric is ResNet-18 samples/s.  Two stems:
+
+* ``cifar``    : conv3x3(64) stride 1, no max-pool (32x32 inputs). ResNet-18 ->
+  11,173,962 parameters, the count SURVEY §5.8 prices the messages with.
+* ``imagenet`` : conv7x7/s2 + maxpool3/s2 (224x224 inputs). ResNet-50 ->
+  25,557,032 parameters.
+
+Every conv is followed by a fused BN(+residual)(+ReLU) kernel pair; the
+block output ``relu(bn2(conv2(h)) + shortcut)`` is ONE kernel on GPU.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops import layers as L
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin: int, planes: int, stride: int = 1):
+        super().__init__()
+        self.conv1 = L.Conv2d(cin, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn1 = L.BatchNorm2d(planes, relu=True)
+        self.conv2 = L.Conv2d(planes, planes, 3, stride=1, padding=1, bias=False)
+        self.bn2 = L.BatchNorm2d(planes, relu=True)
+        self.shortcut = None
+        if stride != 1 or cin != planes:
+            self.shortcut = nn.Sequential(
+                L.Conv2d(cin, planes, 1, stride=stride, bias=False), L.BatchNorm2d(planes))
+
+    def forward(self, x):
+        h = self.bn1(self.conv1(x))
+        sc = x if self.shortcut is None else self.shortcut(x)
+        return self.bn2(self.conv2(h), residual=sc)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, planes: int, stride: int = 1):
+        super().__init__()
+        out = planes * self.expansion
+        self.conv1 = L.Conv2d(cin, planes, 1, bias=False)
+        self.bn1 = L.BatchNorm2d(planes, relu=True)
+        self.conv2 = L.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = L.BatchNorm2d(planes, relu=True)
+        self.conv3 = L.Conv2d(planes, out, 1, bias=False)
+        self.bn3 = L.BatchNorm2d(out, relu=True)
+        self.shortcut = None
+        if stride != 1 or cin != out:
+            self.shortcut = nn.Sequential(
+                L.Conv2d(cin, out, 1, stride=stride, bias=False), L.BatchNorm2d(out))
+
+    def forward(self, x):
+        h = self.bn1(self.conv1(x))
+        h = self.bn2(self.conv2(h))
+        sc = x if self.shortcut is None else self.shortcut(x)
+        return self.bn3(self.conv3(h), residual=sc)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block, layers, num_classes: int = 10, stem: str = "cifar",
+                 zero_init_residual: bool = False):
+        super().__init__()
+        self.stem_kind = stem
+        if stem == "cifar":
+            self.conv1 = L.Conv2d(3, 64, 3, stride=1, padding=1, bias=False)
+            self.pool = None
+        elif stem == "imagenet":
+            self.conv1 = L.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+            self.pool = nn.MaxPool2d(3, stride=2, padding=1)
+        else:
+            raise ValueError(f"unknown stem {stem!r}")
+        self.bn1 = L.BatchNorm2d(64, relu=True)
+        cin = 64
+        stages = []
+        for i, (planes, n) in enumerate(zip((64, 128, 256, 512), layers)):
+            blocks = []
+            for j in range(n):
+                stride = 2 if (i > 0 and j == 0) else 1
+                blocks.append(block(cin, planes, stride))
+                cin = planes * block.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.avgpool = L.GlobalAvgPool()
+        self.linear = L.Linear(cin, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+                elif isinstance(m, BasicBlock):
+                    nn.init.zeros_(m.bn2.weight)
+
+    def forward(self, x):
+        h = self.bn1(self.conv1(x))
+        if self.pool is not None:
+            h = self.pool(h)
+        h = self.layer4(self.layer3(self.layer2(self.layer1(h))))
+        return self.linear(self.avgpool(h))
+
+
+def resnet18(num_classes: int = 10, stem: str = "cifar", **kw) -> ResNet:
+    return ResNet(BasicBlock, (2, 2, 2, 2), num_classes, stem, **kw)
+
+
+def resnet34(num_classes: int = 10, stem: str = "cifar", **kw) -> ResNet:
+    return ResNet(BasicBlock, (3, 4, 6, 3), num_classes, stem, **kw)
+
+
+def resnet50(num_classes: int = 1000, stem: str = "imagenet", **kw) -> ResNet:
+    return ResNet(Bottleneck, (3, 4, 6, 3), num_classes, stem, **kw)
+
+
+def resnet101(num_classes: int = 1000, stem: str = "imagenet", **kw) -> ResNet:
+    return ResNet(Bottleneck, (3, 4, 23, 3), num_classes, stem, **kw)

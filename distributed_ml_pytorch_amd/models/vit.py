@@ -1,0 +1,100 @@
+"""Vision Transformer (BASELINE.json config #5: ViT-Base/16 ASGD bf16).
+
+Not in the reference (no sequence models there).  ViT-B/16 at
+224x224 = 197 tokens, D=768, 12 heads, MLP 3072, 86,567,656 parameters with a
+1000-class head.  Patch embedding is a stride-16 conv (an implicit GEMM);
+attention uses PyTorch-ROCm's fused SDPA kernel; the projection GEMMs run on
+hipBLASLt through ``F.linear`` (plain library GEMMs).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import layers as L
+from ..ops.functional import compute_weight
+
+
+class LayerNorm(nn.LayerNorm):
+    def forward(self, x):
+        return F.layer_norm(x, self.normalized_shape, compute_weight(self.weight, x.dtype),
+                            compute_weight(self.bias, x.dtype), self.eps)
+
+
+class Attention(nn.Module):
+    def __init__(self, dim: int, heads: int):
+        super().__init__()
+        self.heads = heads
+        self.qkv = L.Linear(dim, 3 * dim)
+        self.proj = L.Linear(dim, dim)
+
+    def forward(self, x):
+        B, N, D = x.shape
+        qkv = self.qkv(x).view(B, N, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
+        q, k, v = qkv[0], qkv[1], qkv[2]
+        o = F.scaled_dot_product_attention(q, k, v)
+        return self.proj(o.transpose(1, 2).reshape(B, N, D))
+
+
+class Block(nn.Module):
+    def __init__(self, dim: int, heads: int, mlp_ratio: float = 4.0):
+        super().__init__()
+        self.norm1 = LayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, heads)
+        self.norm2 = LayerNorm(dim, eps=1e-6)
+        hidden = int(dim * mlp_ratio)
+        self.fc1 = L.Linear(dim, hidden)
+        self.fc2 = L.Linear(hidden, dim)
+
+    def forward(self, x):
+        x = x + self.attn(self.norm1(x))
+        return x + self.fc2(F.gelu(self.fc1(self.norm2(x)), approximate="tanh"))
+
+
+class VisionTransformer(nn.Module):
+    def __init__(self, image_size: int = 224, patch: int = 16, dim: int = 768, depth: int = 12,
+                 heads: int = 12, mlp_ratio: float = 4.0, num_classes: int = 1000,
+                 in_chans: int = 3):
+        super().__init__()
+        assert image_size % patch == 0
+        self.patch = patch
+        self.num_patches = (image_size // patch) ** 2
+        self.patch_embed = L.Conv2d(in_chans, dim, kernel_size=patch, stride=patch)
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, self.num_patches + 1, dim))
+        self.blocks = nn.ModuleList(Block(dim, heads, mlp_ratio) for _ in range(depth))
+        self.norm = LayerNorm(dim, eps=1e-6)
+        self.head = L.Linear(dim, num_classes)
+        nn.init.trunc_normal_(self.pos_embed, std=0.02)
+        nn.init.trunc_normal_(self.cls_token, std=0.02)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+        w = self.patch_embed.weight
+        nn.init.uniform_(w, -1 / math.sqrt(w[0].numel()), 1 / math.sqrt(w[0].numel()))
+
+    def forward(self, x):
+        h = self.patch_embed(x)                       # [B, D, H/p, W/p]
+        h = h.flatten(2).transpose(1, 2)              # [B, N, D]
+        cls = compute_weight(self.cls_token, h.dtype).expand(h.shape[0], -1, -1)
+        h = torch.cat([cls, h], dim=1) + compute_weight(self.pos_embed, h.dtype)
+        for blk in self.blocks:
+            h = blk(h)
+        h = self.norm(h)
+        return self.head(h[:, 0].contiguous())
+
+
+def vit_b16(num_classes: int = 1000, image_size: int = 224) -> VisionTransformer:
+    return VisionTransformer(image_size=image_size, patch=16, dim=768, depth=12, heads=12,
+                             num_classes=num_classes)
+
+
+def vit_tiny(num_classes: int = 10, image_size: int = 32, patch: int = 4) -> VisionTransformer:
+    """Small ViT for CPU tests and CIFAR-shaped smoke runs."""
+    return VisionTransformer(image_size=image_size, patch=patch, dim=64, depth=2, heads=4,
+                             num_classes=num_classes)

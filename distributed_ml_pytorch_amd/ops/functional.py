@@ -1,0 +1,208 @@
+"""Autograd-level ops over the gfx950 kernels.
+
+GPU tensors run the hand-written HIP kernels (``_native``); CPU tensors run
+the PyTorch formulation of the same math, which doubles as the test oracle.
+
+Gradient plumbing for parameters that live in a :class:`FlatArena`
+(``p._dmp_arena`` set): the native backward writes/accumulates the fp32
+parameter gradient straight into ``p.grad`` (a view of the arena's flat grad
+buffer) and returns ``None`` for that input, so autograd never materialises a
+per-parameter grad tensor nor runs an AccumulateGrad copy.  The arena is told
+the gradient is ready through ``p._dmp_grad_ready`` (drives bucketed
+all-reduce overlap in sync-DP mode).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from ._ext import native
+
+CL = torch.channels_last
+
+
+def _arena_grad(p):
+    """fp32 grad view for an arena-managed parameter, else None."""
+    if p is None or not getattr(p, "_dmp_arena", False):
+        return None
+    return p.grad
+
+
+def _notify(*ps):
+    for p in ps:
+        cb = getattr(p, "_dmp_grad_ready", None) if p is not None else None
+        if cb is not None:
+            cb(p)
+
+
+# --------------------------------------------------------------- shadow weight
+class _ShadowWeight(Function):
+    """Use the arena's bf16 shadow of an fp32 master parameter in compute.
+
+    Forward returns the pre-cast bf16 shadow (refreshed by the fused optimizer
+    kernel each step, so no per-step cast).  Backward folds the bf16 weight
+    gradient into the fp32 master grad in place.
+    """
+
+    @staticmethod
+    def forward(ctx, p, w16):
+        ctx.p = p
+        return w16.view_as(w16)
+
+    @staticmethod
+    def backward(ctx, g):
+        p = ctx.p
+        if p.grad is None:
+            return g.to(p.dtype), None
+        p.grad.add_(g)
+        _notify(p)
+        return None, None
+
+
+def compute_weight(p: torch.Tensor | None, dtype: torch.dtype):
+    if p is None:
+        return None
+    if p.dtype == dtype:
+        return p
+    w16 = getattr(p, "_dmp_w16", None)
+    if w16 is not None and dtype == w16.dtype and p.requires_grad and torch.is_grad_enabled():
+        return _ShadowWeight.apply(p, w16)
+    if w16 is not None and dtype == w16.dtype:
+        return w16
+    return p.to(dtype)
+
+
+# --------------------------------------------------------------- cross entropy
+class _SoftmaxXent(Function):
+    @staticmethod
+    def forward(ctx, logits, labels, smoothing, ignore_index):
+        loss, hits, dlogits = native().softmax_xent(logits.contiguous(), labels.contiguous(), True,
+                                                    float(smoothing), int(ignore_index))
+        ctx.save_for_backward(dlogits)
+        ctx.mark_non_differentiable(hits)
+        return loss, hits
+
+    @staticmethod
+    def backward(ctx, gloss, ghits):
+        (dlogits,) = ctx.saved_tensors
+        return dlogits * gloss.to(dlogits.dtype), None, None, None
+
+
+def softmax_cross_entropy(logits, labels, label_smoothing: float = 0.0, ignore_index: int = -100):
+    """Mean cross-entropy; returns ``(loss, hits)`` with hits = #top-1 correct.
+
+    Reference: ``F.cross_entropy`` + ``torch.max`` at /root/reference/example/main.py:71,75.
+    """
+    if logits.is_cuda:
+        return _SoftmaxXent.apply(logits, labels, label_smoothing, ignore_index)
+    loss = F.cross_entropy(logits.float(), labels, label_smoothing=label_smoothing,
+                           ignore_index=ignore_index)
+    with torch.no_grad():
+        valid = labels != ignore_index
+        hits = ((logits.argmax(1) == labels) & valid).sum().to(torch.int32)
+    return loss, hits
+
+
+# ------------------------------------------------------------------ batchnorm
+class _BNAct(Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
+                relu):
+        if x.dim() == 4:
+            x = x.contiguous(memory_format=CL)
+            if residual is not None:
+                residual = residual.contiguous(memory_format=CL)
+        y, stats = native().bn_fwd(x, residual, gamma, beta, running_mean, running_var,
+                                   float(momentum), float(eps), bool(training), bool(relu))
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.gamma, ctx.beta = gamma, beta
+        ctx.save_for_backward(x, y if relu else None, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, stats = ctx.saved_tensors
+        gamma, beta = ctx.gamma, ctx.beta
+        dg_arena, db_arena = _arena_grad(gamma), _arena_grad(beta)
+        need_g = gamma is not None and ctx.needs_input_grad[1]
+        need_b = beta is not None and ctx.needs_input_grad[2]
+        dg = dg_arena if dg_arena is not None else (
+            torch.zeros_like(gamma) if need_g else None)
+        db = db_arena if db_arena is not None else (
+            torch.zeros_like(beta) if need_b else None)
+        if x.dim() == 4:
+            dy = dy.contiguous(memory_format=CL)
+        else:
+            dy = dy.contiguous()
+        dx, dres = native().bn_bwd(x, dy, y, gamma, stats, dg, db, ctx.relu, ctx.has_res)
+        if dg_arena is not None or db_arena is not None:
+            _notify(gamma, beta)
+        ret_g = None if (dg_arena is not None or not need_g) else dg
+        ret_b = None if (db_arena is not None or not need_b) else db
+        return dx, ret_g, ret_b, (dres if ctx.has_res else None), None, None, None, None, None, None
+
+
+def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float,
+                   eps: float, relu: bool = False, residual=None):
+    """``relu?(batch_norm(x) [+ residual])`` in one fused kernel pair (NHWC bf16 on GPU)."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0 and x.shape[1] <= 2048:
+        if not training and (running_mean is None or running_var is None):
+            training = True
+        return _BNAct.apply(x, weight, bias, residual, running_mean, running_var, training,
+                            momentum, eps, relu)
+    if x.is_cuda:
+        raise RuntimeError(
+            f"batch_norm_act: unsupported GPU input (dtype={x.dtype}, C={x.shape[1]}); "
+            "the native kernel needs bf16 with C % 8 == 0 and C <= 2048")
+    w = weight.to(x.dtype) if weight is not None else None
+    b = bias.to(x.dtype) if bias is not None else None
+    y = F.batch_norm(x, running_mean, running_var, w, b, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+# -------------------------------------------------------------------- pooling
+class _GAP(Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous(memory_format=CL)
+        ctx.hw = (x.shape[2], x.shape[3])
+        return native().gap_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return native().gap_bwd(dy.contiguous(), ctx.hw[0], ctx.hw[1])
+
+
+def global_avg_pool(x):
+    """[N,C,H,W] -> [N,C] mean over H,W."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+        return _GAP.apply(x)
+    return x.mean(dim=(2, 3))
+
+
+class _MaxPool(Function):
+    @staticmethod
+    def forward(ctx, x, k):
+        x = x.contiguous(memory_format=CL)
+        y, idx = native().maxpool_fwd(x, k)
+        ctx.save_for_backward(idx)
+        ctx.meta = (x.shape[2], x.shape[3], k)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        H, W, k = ctx.meta
+        return native().maxpool_bwd(dy, idx, H, W, k), None
+
+
+def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0):
+    stride = kernel_size if stride is None else stride
+    if (x.is_cuda and x.dtype == torch.bfloat16 and stride == kernel_size and padding == 0
+            and x.shape[1] % 8 == 0 and x.shape[2] >= kernel_size and x.shape[3] >= kernel_size):
+        return _MaxPool.apply(x, int(kernel_size))
+    return F.max_pool2d(x, kernel_size, stride, padding)

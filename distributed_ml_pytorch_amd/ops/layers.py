@@ -1,0 +1,81 @@
+"""nn.Module layers that route to the gfx950 kernels on GPU.
+
+They subclass the stock torch modules so state_dicts, initialisation and
+parameter order (the ravel order of the reference's serialization, see
+``utils/serialization.py``) are unchanged.  Compute dtype follows the input:
+fp32 masters are cast through the arena's bf16 shadow (``compute_weight``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import functional as DF
+from .conv import conv2d as _conv2d
+
+
+class Conv2d(nn.Conv2d):
+    def forward(self, x):
+        w = DF.compute_weight(self.weight, x.dtype)
+        b = DF.compute_weight(self.bias, x.dtype)
+        return _conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups,
+                       master=self.weight)
+
+
+class Linear(nn.Linear):
+    def forward(self, x):
+        w = DF.compute_weight(self.weight, x.dtype)
+        b = DF.compute_weight(self.bias, x.dtype)
+        return F.linear(x, w, b)
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """BatchNorm with optional fused residual-add and ReLU epilogue."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, relu: bool = False, **kw):
+        super().__init__(num_features, eps=eps, momentum=momentum, **kw)
+        self.relu = relu
+
+    def forward(self, x, residual=None):
+        use_batch = self.training or not self.track_running_stats
+        return DF.batch_norm_act(
+            x, self.weight, self.bias,
+            self.running_mean if self.track_running_stats else None,
+            self.running_var if self.track_running_stats else None,
+            use_batch, 0.1 if self.momentum is None else self.momentum, self.eps,
+            relu=self.relu, residual=residual)
+
+
+class BatchNorm1d(nn.BatchNorm1d):
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, relu: bool = False, **kw):
+        super().__init__(num_features, eps=eps, momentum=momentum, **kw)
+        self.relu = relu
+
+    def forward(self, x, residual=None):
+        use_batch = self.training or not self.track_running_stats
+        return DF.batch_norm_act(
+            x, self.weight, self.bias,
+            self.running_mean if self.track_running_stats else None,
+            self.running_var if self.track_running_stats else None,
+            use_batch, 0.1 if self.momentum is None else self.momentum, self.eps,
+            relu=self.relu, residual=residual)
+
+
+class MaxPool2d(nn.MaxPool2d):
+    def forward(self, x):
+        k = self.kernel_size if isinstance(self.kernel_size, int) else self.kernel_size[0]
+        s = self.stride if isinstance(self.stride, int) else self.stride[0]
+        p = self.padding if isinstance(self.padding, int) else self.padding[0]
+        if self.ceil_mode or self.dilation not in (1, (1, 1)):
+            return super().forward(x)
+        return DF.max_pool2d(x, k, s, p)
+
+
+class GlobalAvgPool(nn.Module):
+    def forward(self, x):
+        return DF.global_avg_pool(x)
+
+
+class ReLU(nn.ReLU):
+    pass

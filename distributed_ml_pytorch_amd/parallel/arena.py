@@ -1,0 +1,173 @@
+"""Flat parameter arena: every parameter and gradient is a view into one buffer.
+
+The reference ravels the model with a ``torch.cat`` over all parameters on
+EVERY optimizer step (``ravel_model_params`` at
+/root/reference/asgd/optim/Asynchronous.py:27,34,54) and copies slices back on
+every pull (``unravel_model_params`` :18).  Here the flat buffer IS the
+storage, so ravel/unravel are zero-copy and the ASGD update, the push, the
+pull landing and the sync-DP all-reduce each touch one contiguous buffer.
+
+Layout (fp32 master ``p32``, fp32 ``g32`` grads, optional bf16 ``w16`` compute
+shadow refreshed by the fused optimizer kernel):
+  * parameter order = ``model.parameters()`` order (the reference's ravel order)
+  * each parameter starts on a 64-element (256 B) boundary -> every view is
+    16-B aligned for the vectorised kernels
+  * 4-D weights get channels_last strides (physical [Cout][kh][kw][Cin]), the
+    layout the NHWC conv kernels and MIOpen's NHWC path consume
+  * the total is padded to a multiple of ``pad_multiple`` elements so the buffer
+    splits evenly into world-size shards for reduce-scatter / all-gather.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+ALIGN = 64
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def _strided_view(flat: torch.Tensor, offset: int, like: torch.Tensor, channels_last: bool):
+    shape = tuple(like.shape)
+    if channels_last and len(shape) == 4:
+        n, c, h, w = shape
+        stride = (h * w * c, 1, w * c, c)
+    else:
+        stride = []
+        acc = 1
+        for s in reversed(shape):
+            stride.append(acc)
+            acc *= s
+        stride = tuple(reversed(stride))
+    return torch.as_strided(flat, shape, stride, flat.storage_offset() + offset)
+
+
+@dataclass
+class Slot:
+    index: int
+    offset: int
+    numel: int
+    shape: tuple
+
+
+class FlatArena:
+    def __init__(self, params, device=None, shadow_dtype: torch.dtype | None = torch.bfloat16,
+                 channels_last: bool = True, pad_multiple: int = ALIGN * 840,
+                 with_grads: bool = True):
+        if isinstance(params, torch.nn.Module):
+            params = list(params.parameters())
+        self.params = list(params)
+        if not self.params:
+            raise ValueError("FlatArena needs at least one parameter")
+        dev = torch.device(device) if device is not None else self.params[0].device
+        self.device = dev
+        self.channels_last = channels_last
+        off = 0
+        self.slots: list[Slot] = []
+        for i, p in enumerate(self.params):
+            self.slots.append(Slot(i, off, p.numel(), tuple(p.shape)))
+            off = _round_up(off + p.numel(), ALIGN)
+        self.used = sum(s.numel for s in self.slots)          # reference ravel length
+        self.numel = _round_up(max(off, ALIGN), pad_multiple)  # padded flat length
+        self.p32 = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        self.g32 = torch.zeros(self.numel, dtype=torch.float32, device=dev) if with_grads else None
+        self.shadow_dtype = shadow_dtype
+        self.w16 = (torch.zeros(self.numel, dtype=shadow_dtype, device=dev)
+                    if shadow_dtype is not None else None)
+        self._ready_cb = None
+        with torch.no_grad():
+            for p, s in zip(self.params, self.slots):
+                cl = channels_last and p.dim() == 4
+                view = _strided_view(self.p32, s.offset, p, cl)
+                view.copy_(p.detach().to(torch.float32))
+                p.data = view
+                if self.g32 is not None:
+                    p.grad = _strided_view(self.g32, s.offset, p, cl)
+                p._dmp_arena = True
+                if self.w16 is not None:
+                    p._dmp_w16 = _strided_view(self.w16, s.offset, p, cl)
+        self.refresh_shadow()
+
+    # ------------------------------------------------------------------ views
+    def param_view(self, i: int) -> torch.Tensor:
+        return self.params[i].data
+
+    def flat(self, grads: bool = False) -> torch.Tensor:
+        return self.g32 if grads else self.p32
+
+    # ----------------------------------------------------------------- shadow
+    def refresh_shadow(self):
+        if self.w16 is None:
+            return
+        if self.p32.is_cuda:
+            from ..ops._ext import native
+
+            native().cast_f32_bf16(self.p32, self.w16)
+        else:
+            self.w16.copy_(self.p32)
+
+    # ------------------------------------------------------------------ grads
+    def zero_grad(self):
+        if self.g32 is not None:
+            self.g32.zero_()
+
+    def ensure_grads_attached(self):
+        """Re-attach grad views if user code set ``p.grad = None``."""
+        if self.g32 is None:
+            return
+        for p, s in zip(self.params, self.slots):
+            if p.grad is None or p.grad.data_ptr() != self.g32.data_ptr() + 4 * s.offset:
+                cl = self.channels_last and p.dim() == 4
+                p.grad = _strided_view(self.g32, s.offset, p, cl)
+
+    def set_grad_ready_callback(self, cb):
+        """``cb(param_index)`` is called as each parameter's gradient becomes final."""
+        self._ready_cb = cb
+        for i, p in enumerate(self.params):
+            def _ready(_p, _i=i):
+                if self._ready_cb is not None:
+                    self._ready_cb(_i)
+            p._dmp_grad_ready = _ready
+            if not hasattr(p, "_dmp_hook_handle"):
+                p._dmp_hook_handle = p.register_post_accumulate_grad_hook(
+                    lambda t: t._dmp_grad_ready(t) if getattr(t, "_dmp_grad_ready", None) else None)
+
+    # ----------------------------------------------------- ravel compatibility
+    def ravel(self, grads: bool = False) -> torch.Tensor:
+        """Unpadded concatenation in ``model.parameters()`` order (reference layout)."""
+        src = [p.grad if grads else p.data for p in self.params]
+        return torch.cat([t.reshape(-1) for t in src])
+
+    def unravel(self, flat: torch.Tensor):
+        flat = flat.to(self.device)
+        with torch.no_grad():
+            if flat.numel() == self.numel:
+                self.p32.copy_(flat)
+            elif flat.numel() == self.used:
+                o = 0
+                for p, s in zip(self.params, self.slots):
+                    p.data.copy_(flat[o:o + s.numel].view(s.shape))
+                    o += s.numel
+            else:
+                raise ValueError(f"flat vector has {flat.numel()} elements; expected "
+                                 f"{self.used} (ravel) or {self.numel} (arena)")
+        self.refresh_shadow()
+
+    def state_dict(self):
+        return {"p32": self.p32.detach().cpu(), "used": self.used, "numel": self.numel}
+
+    def load_state_dict(self, sd):
+        self.unravel(sd["p32"])
+
+
+def attach_arena(model: torch.nn.Module, **kw) -> FlatArena:
+    arena = FlatArena(list(model.parameters()), **kw)
+    model._dmp_arena_obj = arena
+    return arena
+
+
+def get_arena(model: torch.nn.Module) -> FlatArena | None:
+    return getattr(model, "_dmp_arena_obj", None)

@@ -1,0 +1,405 @@
+"""Worker-side parameter-server clients for the Downpour/ASGD optimizer.
+
+One interface, four transports:
+
+* :class:`LocalPSClient`   - in-process PS on the worker's own device (1 GPU).
+* :class:`GlooPSClient`    - the reference topology: rank ``ps_rank`` runs
+  :class:`~.server.ParameterServer`, headers+payloads over gloo (CPU tensors).
+* :class:`RcclPSClient`    - same topology on GPUs: header on a CPU gloo control
+  group, payload on a per-(PS, worker) RCCL communicator (xGMI link).
+* :class:`ShardedPSClient` - DistBelief-style sharded PS co-located on every
+  worker: a push is a reduce-scatter of the accumulated deltas into each
+  rank's fp32 master shard (+ apply), a pull is an all-gather of the shards.
+  On 8 GPUs this drives all 7 xGMI links of every GPU instead of funnelling
+  through one PS GPU.
+
+Timing semantics shared by all clients (``staleness = s``):
+  step k:   fused update -> [push if k % n_push == 0] -> [pull request if
+            k % n_pull == 0] -> land every pull requested at step <= k - s.
+On GPU, push/pull communication runs on a side stream / the RCCL stream and a
+pull is landed by making the compute stream wait on its event, so the host
+never blocks and forward/backward of steps k+1..k+s overlap the transfer.
+"""
+from __future__ import annotations
+
+import logging
+from collections import deque
+
+import torch
+import torch.distributed as dist
+
+from . import messaging as M
+
+_LOG = logging.getLogger(__name__)
+
+
+class _Pending:
+    __slots__ = ("step", "buf", "work", "event", "version")
+
+    def __init__(self, step, buf, work=None, event=None, version=0):
+        self.step, self.buf, self.work, self.event, self.version = step, buf, work, event, version
+
+
+class PSClient:
+    """Base class: owns staging buffers and the landing logic."""
+
+    def __init__(self, staleness: int = 1, pull_mode: str = "overwrite",
+                 wire_dtype: torch.dtype = torch.float32):
+        if staleness < 0:
+            raise ValueError("staleness must be >= 0")
+        if pull_mode not in ("overwrite", "rebase"):
+            raise ValueError("pull_mode must be 'overwrite' (reference) or 'rebase'")
+        self.staleness = staleness
+        self.pull_mode = pull_mode
+        self.wire_dtype = wire_dtype
+        self.pending: deque[_Pending] = deque()
+        self.version = 0            # version of the PS params last landed
+        self.pushes = 0
+        self.pulls = 0
+        self.bytes_sent = 0
+        self.bytes_recv = 0
+
+    # -- wiring ------------------------------------------------------------
+    def attach(self, opt):
+        self.opt = opt
+        self.arena = opt.arena
+        self.device = self.arena.device
+        self.cuda = self.device.type == "cuda"
+        if self.cuda:
+            from ..ops._ext import native
+
+            self.nat = native()
+        self._send = [None, None]
+        self._send_work = [None, None]
+        self._send_slot = 0
+
+    def init(self):
+        pass
+
+    # -- push --------------------------------------------------------------
+    def _handoff(self, n: int | None = None) -> torch.Tensor:
+        """Snapshot the accumulator into a send buffer and zero it."""
+        acc = self.opt.acc
+        slot = self._send_slot
+        self._send_slot ^= 1
+        prev = self._send_work[slot]
+        if prev is not None:
+            prev.wait()
+            self._send_work[slot] = None
+        buf = self._send[slot]
+        if buf is None or buf.numel() != acc.numel():
+            buf = torch.empty(acc.numel(), dtype=self.wire_dtype, device=self.device)
+            self._send[slot] = buf
+        if self.cuda:
+            if self.wire_dtype == torch.float32:
+                self.nat.push_handoff(acc, buf, None)
+            else:
+                self.nat.push_handoff(acc, None, buf)
+        else:
+            buf.copy_(acc)
+            acc.zero_()
+        self._cur_slot = slot
+        return buf
+
+    def push(self, step: int):
+        raise NotImplementedError
+
+    def request_pull(self, step: int):
+        raise NotImplementedError
+
+    # -- landing -----------------------------------------------------------
+    def _land(self, pend: _Pending):
+        arena = self.arena
+        acc = self.opt.acc if self.pull_mode == "rebase" else None
+        src = pend.buf
+        if self.cuda:
+            if pend.event is not None:
+                torch.cuda.current_stream().wait_event(pend.event)
+            if pend.work is not None:
+                pend.work.wait()
+            n = arena.numel
+            self.nat.pull_land(arena.p32, src[:n] if src.numel() != n else src,
+                               acc, arena.w16)
+        else:
+            if pend.work is not None:
+                pend.work.wait()
+            with torch.no_grad():
+                n = arena.numel
+                flat = src[:n].to(torch.float32) if src.numel() >= n else None
+                if flat is None:
+                    arena.p32.zero_()
+                    arena.p32[: src.numel()].copy_(src)
+                else:
+                    arena.p32.copy_(flat)
+                if acc is not None:
+                    arena.p32.add_(acc)
+                if arena.w16 is not None:
+                    arena.w16.copy_(arena.p32)
+        self.version = max(self.version, pend.version)
+        self.pulls += 1
+
+    def land_due(self, step: int, force: bool = False):
+        while self.pending and (force or self.pending[0].step <= step - self.staleness):
+            self._land(self.pending.popleft())
+
+    def finish(self):
+        self.land_due(0, force=True)
+        for w in self._send_work:
+            if w is not None:
+                w.wait()
+        M.SENDS.drain()
+
+    def stats(self) -> dict:
+        return {"pushes": self.pushes, "pulls": self.pulls, "bytes_sent": self.bytes_sent,
+                "bytes_recv": self.bytes_recv, "version": self.version}
+
+
+class LocalPSClient(PSClient):
+    """In-process parameter server on the worker's device (single-GPU / tests)."""
+
+    def init(self):
+        self.master = self.arena.p32.detach().clone()
+        self.ps_version = 0
+        self.side = torch.cuda.Stream(self.device) if self.cuda else None
+
+    def push(self, step: int):
+        buf = self._handoff()
+        if self.cuda:
+            self.nat.ps_apply(self.master, buf, None, 1.0)
+        else:
+            self.master.add_(buf.to(torch.float32))
+        self.ps_version += 1
+        self.pushes += 1
+        self.bytes_sent += buf.numel() * buf.element_size()
+
+    def request_pull(self, step: int):
+        snap = self.master.clone() if self.wire_dtype == torch.float32 else \
+            self.master.to(self.wire_dtype)
+        self.pending.append(_Pending(step, snap, version=self.ps_version))
+        self.bytes_recv += snap.numel() * snap.element_size()
+
+
+class GlooPSClient(PSClient):
+    """Reference topology over gloo: ``send_message`` to the PS, reply on TAG_REPLY."""
+
+    def __init__(self, ps_rank: int = 0, group=None, **kw):
+        super().__init__(**kw)
+        self.ps_rank = ps_rank
+        self.group = group
+
+    def _cpu(self, t):
+        return t if t.device.type == "cpu" else t.cpu()
+
+    def init(self):
+        self.used = self.arena.numel
+        M.send_message(M.MessageCode.ParameterUpdate, self._cpu(self.arena.p32), self.ps_rank,
+                       step=0, group=self.group)
+
+    def push(self, step: int):
+        buf = self._handoff()
+        M.send_message(M.MessageCode.GradientUpdate, self._cpu(buf), self.ps_rank, step=step,
+                       version=self.version, group=self.group)
+        self.pushes += 1
+        self.bytes_sent += buf.numel() * buf.element_size()
+
+    def request_pull(self, step: int):
+        M.send_message(M.MessageCode.ParameterRequest, None, self.ps_rank, step=step,
+                       group=self.group)
+        buf = torch.empty(self.arena.numel, dtype=torch.float32)
+        work = dist.irecv(buf, self.ps_rank, group=self.group, tag=M.TAG_REPLY)
+        self.pending.append(_Pending(step, buf, work=work))
+        self.bytes_recv += buf.numel() * 4
+
+    def _land(self, pend):
+        if self.cuda:
+            pend.work.wait()
+            pend.work = None
+            pend.buf = pend.buf.to(self.device, non_blocking=False)
+        super()._land(pend)
+
+    def finish(self):
+        super().finish()
+        M.send_message(M.MessageCode.Shutdown, None, self.ps_rank, group=self.group)
+        M.SENDS.drain()
+
+
+class RcclPSClient(PSClient):
+    """Central PS on GPUs: control header on gloo, payload over a per-pair RCCL comm."""
+
+    def __init__(self, ps_rank: int, control_group, pair_group, **kw):
+        super().__init__(**kw)
+        self.ps_rank = ps_rank
+        self.ctrl = control_group
+        self.pair = pair_group
+        self._pull_bufs: deque = deque()
+
+    def _send_payload(self, buf):
+        # torch's RCCL p2p waits on the current (compute) stream, so the send is
+        # ordered after the hand-off kernel without a host sync.
+        return dist.isend(buf, self.ps_rank, group=self.pair)
+
+    def init(self):
+        n = self.arena.numel
+        header = M.make_header(M.MessageCode.ParameterUpdate, dist.get_rank(), 0, 0, n)
+        M.SENDS.add(dist.isend(header, self.ps_rank, group=self.ctrl, tag=M.TAG_HEADER), header)
+        w = self._send_payload(self.arena.p32)
+        w.wait()
+
+    def push(self, step: int):
+        buf = self._handoff()
+        header = M.make_header(M.MessageCode.GradientUpdate, dist.get_rank(), step, self.version,
+                               buf.numel(), buf.dtype)
+        M.SENDS.add(dist.isend(header, self.ps_rank, group=self.ctrl, tag=M.TAG_HEADER), header)
+        self._send_work[self._cur_slot] = self._send_payload(buf)
+        self.pushes += 1
+        self.bytes_sent += buf.numel() * buf.element_size()
+
+    def request_pull(self, step: int):
+        header = M.make_header(M.MessageCode.ParameterRequest, dist.get_rank(), step, 0, 0)
+        M.SENDS.add(dist.isend(header, self.ps_rank, group=self.ctrl, tag=M.TAG_HEADER), header)
+        buf = self._pull_bufs.popleft() if len(self._pull_bufs) > self.staleness else \
+            torch.empty(self.arena.numel, dtype=torch.float32, device=self.device)
+        work = dist.irecv(buf[: self.arena.numel], self.ps_rank, group=self.pair)
+        self.pending.append(_Pending(step, buf, work=work))
+        self.bytes_recv += buf.numel() * 4
+
+    def _land(self, pend):
+        super()._land(pend)
+        self._pull_bufs.append(pend.buf)
+
+    def finish(self):
+        super().finish()
+        header = M.make_header(M.MessageCode.Shutdown, dist.get_rank(), 0, 0, 0)
+        dist.send(header, self.ps_rank, group=self.ctrl, tag=M.TAG_HEADER)
+        M.SENDS.drain()
+
+
+class ShardedPSClient(PSClient):
+    """Sharded PS co-located on every worker (collective push/pull).
+
+    Each rank owns ``numel / world`` of the fp32 master parameters.  Push =
+    ``reduce_scatter(sum of every worker's accumulated delta)`` + apply into the
+    local master shard (exactly what a central PS does for simultaneous
+    pushes); pull = ``all_gather`` of the master shards.  On GPU both run on a
+    side stream; the pull's event is waited by the compute stream only when
+    the pull is due (``staleness`` steps later).
+    """
+
+    def __init__(self, group=None, **kw):
+        super().__init__(**kw)
+        self.group = group
+
+    def init(self):
+        self.world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(self.group) if dist.is_initialized() else 0
+        n = self.arena.numel
+        if n % self.world:
+            raise ValueError(f"arena length {n} not divisible by world size {self.world}")
+        self.shard_n = n // self.world
+        if self.world > 1:
+            # identical starting point everywhere (the reference let every worker
+            # start from its own random init and converge through pulls)
+            dist.broadcast(self.arena.p32, 0, group=self.group)
+            self.arena.refresh_shadow()
+        lo = self.rank * self.shard_n
+        self.master = self.arena.p32[lo: lo + self.shard_n].detach().clone()
+        self.delta_shard = torch.zeros(self.shard_n, dtype=self.wire_dtype, device=self.device)
+        self.side = torch.cuda.Stream(self.device) if self.cuda else None
+        self._pull_bufs: deque = deque()
+        self._push_event = None
+
+    def _apply_delta(self):
+        if self.cuda:
+            self.nat.ps_apply(self.master, self.delta_shard, None, 1.0)
+        else:
+            self.master.add_(self.delta_shard.to(torch.float32))
+
+    def push(self, step: int):
+        buf = self._handoff()
+        self.pushes += 1
+        self.bytes_sent += buf.numel() * buf.element_size() * (self.world - 1) // max(self.world, 1)
+        if self.world == 1:
+            if self.cuda:
+                self.nat.ps_apply(self.master, buf, None, 1.0)
+            else:
+                self.master.add_(buf.to(torch.float32))
+            return
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(ev)
+                work = dist.reduce_scatter_tensor(self.delta_shard, buf, group=self.group,
+                                                  async_op=True)
+                work.wait()
+                self._apply_delta()
+                done = torch.cuda.Event()
+                done.record()
+            self._send_work[self._cur_slot] = _EventWork(done)
+        else:
+            dist.reduce_scatter_tensor(self.delta_shard, buf, group=self.group) \
+                if dist.get_backend(self.group) != "gloo" else self._gloo_reduce_scatter(buf)
+            self._apply_delta()
+
+    def _gloo_reduce_scatter(self, buf):
+        # gloo has no reduce_scatter_tensor: all_reduce the flat buffer, keep our shard.
+        tmp = buf.clone()
+        dist.all_reduce(tmp, group=self.group)
+        lo = self.rank * self.shard_n
+        self.delta_shard.copy_(tmp[lo: lo + self.shard_n])
+
+    def request_pull(self, step: int):
+        n = self.arena.numel
+        buf, free_ev = self._pull_bufs.popleft() if len(self._pull_bufs) > self.staleness else \
+            (torch.empty(n, dtype=torch.float32, device=self.device), None)
+        self.bytes_recv += n * 4 * (self.world - 1) // max(self.world, 1)
+        if self.world == 1:
+            buf.copy_(self.master)
+            self.pending.append(_Pending(step, buf))
+            return
+        if self.cuda:
+            with torch.cuda.stream(self.side):
+                if free_ev is not None:
+                    self.side.wait_event(free_ev)   # previous land kernel done reading buf
+                work = dist.all_gather_into_tensor(buf, self.master, group=self.group,
+                                                   async_op=True)
+                work.wait()
+                ev = torch.cuda.Event()
+                ev.record()
+            self.pending.append(_Pending(step, buf, event=ev))
+        else:
+            work = dist.all_gather_into_tensor(buf, self.master, group=self.group,
+                                               async_op=True) \
+                if dist.get_backend(self.group) != "gloo" else self._gloo_all_gather(buf)
+            self.pending.append(_Pending(step, buf, work=work))
+
+    def _gloo_all_gather(self, buf):
+        chunks = list(buf.view(self.world, self.shard_n).unbind(0))
+        return dist.all_gather(chunks, self.master.contiguous(), group=self.group, async_op=True)
+
+    def _land(self, pend):
+        super()._land(pend)
+        ev = None
+        if self.cuda:
+            # the buffer may be re-used by the side stream only after the land kernel
+            ev = torch.cuda.Event()
+            ev.record()
+        self._pull_bufs.append((pend.buf, ev))
+
+    def finish(self):
+        super().finish()
+        if self.cuda:
+            self.side.synchronize()
+
+
+class _EventWork:
+    """Adapter so a CUDA event can sit in the send-work slots."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+    def is_completed(self):
+        return self.ev.query()

@@ -1,0 +1,273 @@
+"""Central parameter server (reference C7: ``asgd.server.ParameterServer``).
+
+Contract, reconstructed from /root/reference/example/main.py:135-138 and the
+worker side /root/reference/asgd/optim/Asynchronous.py:34,49,59:
+``ParameterServer(model=...)`` owns a flat fp32 shard; ``.run()`` serves
+
+* ``ParameterUpdate``  -> initialise the shard from a worker's parameters,
+* ``GradientUpdate``   -> ``shard += delta`` (delta already carries ``-lr``),
+* ``ParameterRequest`` -> reply to the SENDER with the current shard,
+
+until every worker has sent ``Shutdown`` (the reference's loop never ended,
+SURVEY D9).  Additions: a version counter (number of applied deltas; pushes
+report the version their base params came from, so the server measures
+staleness), per-worker liveness, periodic checkpoints, and two payload paths:
+
+* ``payload="gloo"`` - headers and payloads on the (CPU) gloo group;
+* ``payload="rccl"`` - headers on a CPU gloo control group, payloads on a
+  per-(PS, worker) RCCL communicator on the PS GPU.  The shard, the apply
+  kernel and the reply snapshots stay on the GPU; one PS stream orders
+  ``recv -> apply`` and ``apply -> snapshot -> send`` without host syncs.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from collections import Counter, defaultdict
+
+import torch
+import torch.distributed as dist
+
+from . import messaging as M
+from .arena import FlatArena
+
+_LOG = logging.getLogger(__name__)
+
+
+def make_ps_groups(ps_rank: int = 0, payload: str = "gloo"):
+    """Create the control group and per-pair payload groups.
+
+    MUST be called by every rank, in the same order (torch ``new_group`` rule).
+    Returns ``(control_group, {worker_rank: pair_group})``.
+    """
+    world = dist.get_world_size()
+    backend = dist.get_backend()
+    if payload == "gloo" and backend == "gloo":
+        return None, {}
+    ctrl = dist.new_group(list(range(world)), backend="gloo")
+    pairs = {}
+    for w in range(world):
+        if w == ps_rank:
+            continue
+        pairs[w] = dist.new_group([min(ps_rank, w), max(ps_rank, w)],
+                                  backend="nccl" if payload == "rccl" else "gloo")
+    return ctrl, pairs
+
+
+class ParameterServer:
+    def __init__(self, model=None, numel: int | None = None, workers=None, control_group=None,
+                 pair_groups=None, payload: str = "auto", device=None, init_policy: str = "first",
+                 checkpoint_path: str | None = None, checkpoint_every: int = 0,
+                 worker_timeout: float | None = None):
+        if not dist.is_initialized():
+            raise RuntimeError("ParameterServer needs torch.distributed to be initialised")
+        self.rank = dist.get_rank()
+        world = dist.get_world_size()
+        self.workers = list(workers) if workers is not None else [
+            r for r in range(world) if r != self.rank]
+        if payload == "auto":
+            payload = "rccl" if dist.get_backend() == "nccl" else "gloo"
+        self.payload = payload
+        self.ctrl = control_group
+        self.pairs = pair_groups or {}
+        if payload == "rccl":
+            if not self.pairs:
+                raise ValueError("payload='rccl' needs pair_groups from make_ps_groups()")
+            self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
+        else:
+            self.device = torch.device(device or "cpu")
+        if model is not None:
+            # the wire layout is the workers' flat arena (64-aligned params,
+            # channels_last 4-D weights, padded total), not the unpadded ravel
+            flat = FlatArena(list(model.parameters()), device="cpu", shadow_dtype=None,
+                             with_grads=False).p32
+        elif numel is not None:
+            flat = torch.zeros(numel, dtype=torch.float32)
+        else:
+            raise ValueError("ParameterServer needs a model or numel")
+        self.numel = flat.numel()
+        pad = (-self.numel) % 4
+        self.shard = torch.zeros(self.numel + pad, dtype=torch.float32, device=self.device)
+        self.shard[: self.numel].copy_(flat)
+        self.version = 0
+        self.initialized = False
+        self.init_policy = init_policy
+        self.counts: Counter = Counter()
+        self.bytes_in = 0
+        self.bytes_out = 0
+        self.staleness: list[int] = []
+        self.last_seen = {w: time.monotonic() for w in self.workers}
+        self.worker_timeout = worker_timeout
+        self.checkpoint_path = checkpoint_path
+        self.checkpoint_every = checkpoint_every
+        self._tracker = M.SendTracker()
+        self._send_bufs: dict[int, torch.Tensor] = {}
+        self._send_work: dict[int, object] = {}
+        self._recv_bufs = defaultdict(dict)
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        if self.device.type == "cuda":
+            from ..ops._ext import native
+
+            self._native = native()
+        else:
+            self._native = None
+
+    # -------------------------------------------------------------- payload io
+    def _recv_payload(self, sender: int, nelem: int, dtype: torch.dtype) -> torch.Tensor:
+        if nelem != self.numel:
+            raise RuntimeError(f"PS: worker {sender} sent {nelem} elements, the shard has "
+                               f"{self.numel} (model/arena layout mismatch)")
+        padded = nelem + ((-nelem) % 4)
+        bufs = self._recv_bufs[sender]
+        buf = bufs.get(dtype)
+        if buf is None or buf.numel() != padded:
+            buf = torch.zeros(padded, dtype=dtype, device=self.device)
+            bufs[dtype] = buf
+        view = buf[:nelem]
+        if self.payload == "rccl":
+            with torch.cuda.stream(self.stream):
+                work = dist.irecv(view, src=sender, group=self.pairs[sender])
+                work.wait()   # PS stream waits on the RCCL stream; host not blocked
+        else:
+            dist.recv(view, src=sender, group=self.ctrl, tag=M.TAG_PAYLOAD)
+        self.bytes_in += nelem * view.element_size()
+        return buf
+
+    def _reply(self, dst: int):
+        if self.payload == "rccl":
+            with torch.cuda.stream(self.stream):
+                prev = self._send_work.pop(dst, None)
+                if prev is not None:
+                    prev.wait()
+                buf = self._send_bufs.get(dst)
+                if buf is None:
+                    buf = torch.empty_like(self.shard)
+                    self._send_bufs[dst] = buf
+                buf.copy_(self.shard)   # snapshot: later applies never tear the reply
+                self._send_work[dst] = dist.isend(buf[: self.numel], dst, group=self.pairs[dst])
+        else:
+            snap = self.shard[: self.numel].clone()
+            w = dist.isend(snap, dst, group=self.ctrl, tag=M.TAG_REPLY)
+            self._tracker.add(w, snap)
+        self.bytes_out += self.numel * 4
+
+    def _apply(self, delta: torch.Tensor):
+        if self._native is not None:
+            with torch.cuda.stream(self.stream):
+                self._native.ps_apply(self.shard, delta, None, 1.0)
+        else:
+            self.shard[: self.numel].add_(delta[: self.numel].to(torch.float32))
+        self.version += 1
+
+    def _set(self, params: torch.Tensor):
+        with torch.cuda.stream(self.stream) if self.stream is not None else _null():
+            self.shard[: self.numel].copy_(params[: self.numel])
+
+    # -------------------------------------------------------------------- loop
+    def handle(self, code, sender: int, step: int, version: int, nelem: int, dtype):
+        self.counts[code.name] += 1
+        self.last_seen[sender] = time.monotonic()
+        if code == M.MessageCode.GradientUpdate:
+            delta = self._recv_payload(sender, nelem, dtype)
+            self.staleness.append(self.version - version)
+            self._apply(delta)
+            if self.checkpoint_every and self.version % self.checkpoint_every == 0:
+                self.save_checkpoint()
+        elif code == M.MessageCode.ParameterUpdate:
+            params = self._recv_payload(sender, nelem, dtype)
+            if not self.initialized or self.init_policy == "last":
+                self._set(params)
+                self.initialized = True
+        elif code == M.MessageCode.ParameterRequest:
+            self._reply(sender)
+        elif code == M.MessageCode.Checkpoint:
+            self.save_checkpoint()
+        elif code == M.MessageCode.Heartbeat:
+            pass
+
+    def run(self):
+        alive = set(self.workers)
+        _LOG.info("PS rank %d serving workers %s (%s payload, %d params)", self.rank,
+                  sorted(alive), self.payload, self.numel)
+        while alive:
+            try:
+                code, sender, step, version, nelem, dtype = M.recv_header(None, self.ctrl)
+            except RuntimeError as e:
+                # A worker died (connection closed / timeout): keep what we have.
+                _LOG.warning("PS: control receive failed (%r); stopping with %d live workers",
+                             e, len(alive))
+                break
+            if code == M.MessageCode.Shutdown:
+                alive.discard(sender)
+                continue
+            self.handle(code, sender, step, version, nelem, dtype)
+            if self.worker_timeout:
+                now = time.monotonic()
+                for w in list(alive):
+                    if now - self.last_seen[w] > self.worker_timeout:
+                        _LOG.warning("PS: worker %d silent for %.1fs, dropping", w,
+                                     now - self.last_seen[w])
+                        alive.discard(w)
+        self.finish()
+        return self.stats()
+
+    def finish(self):
+        for w in list(self._send_work.values()):
+            w.wait()
+        self._send_work.clear()
+        self._tracker.drain()
+        if self.stream is not None:
+            self.stream.synchronize()
+        if self.checkpoint_path:
+            self.save_checkpoint()
+
+    # --------------------------------------------------------------- utilities
+    def parameters(self) -> torch.Tensor:
+        if self.stream is not None:
+            self.stream.synchronize()
+        return self.shard[: self.numel]
+
+    def stats(self) -> dict:
+        st = self.staleness
+        return {
+            "version": self.version,
+            "counts": dict(self.counts),
+            "bytes_in": self.bytes_in,
+            "bytes_out": self.bytes_out,
+            "staleness_mean": (sum(st) / len(st)) if st else 0.0,
+            "staleness_max": max(st) if st else 0,
+        }
+
+    def save_checkpoint(self, path: str | None = None):
+        path = path or self.checkpoint_path
+        if not path:
+            return
+        from ..utils.checkpoint import save_ps_checkpoint
+
+        save_ps_checkpoint(path, self.parameters().detach().cpu(), self.version, self.stats())
+
+    def load_checkpoint(self, path: str):
+        from ..utils.checkpoint import load_ps_checkpoint
+
+        flat, version, _ = load_ps_checkpoint(path)
+        self._set(flat.to(self.device))
+        self.version = version
+        self.initialized = True
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def serve(model=None, **kw):
+    """Convenience: build a server for ``model`` and run it to completion."""
+    return ParameterServer(model=model, **kw).run()
+
+
+if os.environ.get("DMP_PS_DEBUG"):
+    logging.basicConfig(level=logging.INFO)

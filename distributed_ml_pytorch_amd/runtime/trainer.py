@@ -1,0 +1,313 @@
+"""Training driver: the reference's ``example/main.py`` loop as a reusable engine.
+
+Roles and loop follow /root/reference/example/main.py:31-138 (rank 0 = PS in
+the central topology, workers train with ``Asynchronous``; ``--no-distributed``
+= plain SGD), plus the modes BASELINE.json asks for:
+
+* ``mode="asgd"``   Downpour SGD; ``ps`` = ``central`` (reference star,
+  gloo or RCCL payloads), ``sharded`` (PS co-located on every GPU, collective
+  push/pull) or ``local`` (in-process PS, 1 device);
+* ``mode="sync"``   bucketed all-reduce data parallel;
+* ``mode="single"`` plain SGD, no communication.
+
+Per step: zero the flat grad arena (one memset) -> bf16 channels-last forward
+through the native layers -> fused softmax-xent -> backward (native kernels
+write fp32 weight grads straight into the arena) -> [bucket sync] -> fused
+optimizer kernel (+ push/pull).  No host sync per step: the loss is kept on
+device and only read at log points.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import time
+from dataclasses import asdict, dataclass, field
+
+import torch
+import torch.distributed as dist
+
+from ..models import build_model
+from ..ops.functional import softmax_cross_entropy
+from ..parallel.arena import attach_arena
+from ..parallel.asgd import Asynchronous
+from ..parallel.clients import (GlooPSClient, LocalPSClient, RcclPSClient, ShardedPSClient)
+from ..parallel.ddp import BucketedAllReduce, FusedSGD
+from ..parallel.server import ParameterServer, make_ps_groups
+from ..utils import checkpoint as ckpt
+from ..utils.data import get_datasets, make_loaders
+from ..utils.metrics import IterationLog, Throughput
+from .dist import DistInfo
+
+_LOG = logging.getLogger(__name__)
+
+
+@dataclass
+class TrainConfig:
+    model: str = "alexnet"
+    num_classes: int | None = None
+    dataset: str = "synthetic"
+    data_dir: str = "./data"
+    n_train: int = 50000
+    n_test: int = 10000
+    batch_size: int = 64
+    test_batch_size: int = 10000
+    epochs: int = 20
+    max_steps: int | None = None
+    lr: float = 0.008
+    momentum: float = 0.0
+    weight_decay: float = 0.0
+    lr_schedule: str = "constant"     # or "inv_epoch": the reference's LambdaLR(1/(epoch+1))
+    n_push: int = 10
+    n_pull: int = 10
+    staleness: int = 1
+    pull_mode: str = "overwrite"
+    wire_dtype: str = "fp32"
+    mode: str = "asgd"                # asgd | sync | single
+    ps: str = "central"               # central | sharded | local
+    payload: str = "auto"             # central PS payload transport: gloo | rccl | auto
+    dtype: str = "bf16"               # compute dtype on GPU (CPU always fp32)
+    cuda: bool = True
+    log_interval: int = 100
+    evaluate: bool = True
+    seed: int = 0
+    log_dir: str = "log"
+    checkpoint: str | None = None
+    checkpoint_every: int = 0
+    resume: str | None = None
+    bucket_mb: float = 32.0
+    label_smoothing: float = 0.0
+    verbose: bool = True
+    extra: dict = field(default_factory=dict)
+
+
+def _dtype(name: str) -> torch.dtype:
+    return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32,
+            "float32": torch.float32, "fp16": torch.float16}[name]
+
+
+class Worker:
+    """One training process: model + arena + optimizer + step function."""
+
+    def __init__(self, cfg: TrainConfig, info: DistInfo, ps_groups=None):
+        self.cfg = cfg
+        self.info = info
+        torch.manual_seed(cfg.seed + info.rank)
+        self.device = info.device if (cfg.cuda and info.device.type == "cuda") else \
+            torch.device("cpu")
+        self.compute_dtype = _dtype(cfg.dtype) if self.device.type == "cuda" else torch.float32
+        model, shape, nc = build_model(cfg.model, cfg.num_classes)
+        self.input_shape, self.num_classes = shape, nc
+        self.model = model.to(self.device)
+        shadow = self.compute_dtype if self.compute_dtype != torch.float32 else None
+        self.arena = attach_arena(self.model, shadow_dtype=shadow,
+                                  channels_last=True)
+        self.ddp = None
+        params = list(self.model.parameters())
+        if cfg.mode == "asgd":
+            client = self._make_client(ps_groups)
+            self.opt = Asynchronous(params, lr=cfg.lr, n_push=cfg.n_push, n_pull=cfg.n_pull,
+                                    model=self.model, client=client, momentum=cfg.momentum,
+                                    weight_decay=cfg.weight_decay)
+        elif cfg.mode == "sync":
+            world = dist.get_world_size() if info.is_distributed else 1
+            if info.is_distributed:
+                dist.broadcast(self.arena.p32, 0)
+                self.arena.refresh_shadow()
+            self.ddp = BucketedAllReduce(self.arena, bucket_mb=cfg.bucket_mb)
+            self.opt = FusedSGD(params, self.arena, cfg.lr, cfg.momentum,
+                                weight_decay=cfg.weight_decay, grad_scale=1.0 / world)
+        elif cfg.mode == "single":
+            self.opt = FusedSGD(params, self.arena, cfg.lr, cfg.momentum,
+                                weight_decay=cfg.weight_decay)
+        else:
+            raise ValueError(f"unknown mode {cfg.mode!r}")
+        self.step_idx = 0
+        if cfg.resume:
+            self.step_idx = ckpt.load_worker_checkpoint(cfg.resume, self.model, self.opt)
+
+    def _make_client(self, ps_groups):
+        cfg, info = self.cfg, self.info
+        kw = dict(staleness=cfg.staleness, pull_mode=cfg.pull_mode,
+                  wire_dtype=_dtype(cfg.wire_dtype))
+        if cfg.ps == "local" or not info.is_distributed:
+            return LocalPSClient(**kw)
+        if cfg.ps == "sharded":
+            return ShardedPSClient(**kw)
+        if cfg.ps == "central":
+            ctrl, pairs = ps_groups if ps_groups is not None else (None, {})
+            if pairs and self.device.type == "cuda" and _payload(cfg, info) == "rccl":
+                return RcclPSClient(0, ctrl, pairs[info.rank], **kw)
+            return GlooPSClient(ps_rank=0, group=ctrl, **kw)
+        raise ValueError(f"unknown ps kind {cfg.ps!r}")
+
+    # --------------------------------------------------------------- stepping
+    def prepare(self, x, y):
+        x = x.to(self.device, non_blocking=True)
+        if self.device.type == "cuda":
+            x = x.to(self.compute_dtype)
+            if x.dim() == 4:
+                x = x.contiguous(memory_format=torch.channels_last)
+        return x, y.to(self.device, non_blocking=True)
+
+    def train_step(self, x, y):
+        """One fwd+bwd+update. Returns (loss, hits) as device tensors (no sync)."""
+        self.opt.zero_grad()
+        logits = self.model(x)
+        loss, hits = softmax_cross_entropy(logits, y, self.cfg.label_smoothing)
+        loss.backward()
+        if self.ddp is not None:
+            self.ddp.synchronize()
+        self.opt.step()
+        self.step_idx += 1
+        return loss.detach(), hits
+
+    @torch.no_grad()
+    def evaluate(self, loader, max_batches: int | None = None):
+        """Mean loss and accuracy over ALL test batches (reference used the last batch
+        only, main.py:127); restores train mode afterwards (D6)."""
+        was = self.model.training
+        self.model.eval()
+        tot_loss = torch.zeros((), device=self.device)
+        tot_hits = torch.zeros((), device=self.device, dtype=torch.int64)
+        n = 0
+        nb = 0
+        for xb, yb in loader:
+            xb, yb = self.prepare(xb, yb)
+            out = self.model(xb)
+            loss, hits = softmax_cross_entropy(out, yb)
+            tot_loss += loss.float() * yb.numel()
+            tot_hits += hits.to(torch.int64)
+            n += yb.numel()
+            nb += 1
+            if max_batches and nb >= max_batches:
+                break
+        self.model.train(was)
+        if n == 0:
+            return float("nan"), float("nan")
+        return (tot_loss / n).item(), tot_hits.item() / n
+
+    def set_lr(self, lr: float):
+        for g in self.opt.param_groups:
+            g["lr"] = lr
+
+    def finish(self):
+        if isinstance(self.opt, Asynchronous):
+            self.opt.finish()
+
+
+def _payload(cfg: TrainConfig, info: DistInfo) -> str:
+    if cfg.payload != "auto":
+        return cfg.payload
+    return "rccl" if info.backend == "nccl" else "gloo"
+
+
+def run_server(cfg: TrainConfig, info: DistInfo, ps_groups):
+    """Rank 0 in the central topology (reference main.py:135-138)."""
+    ctrl, pairs = ps_groups
+    model, _, _ = build_model(cfg.model, cfg.num_classes)
+    payload = _payload(cfg, info)
+    server = ParameterServer(model=model, control_group=ctrl, pair_groups=pairs,
+                             payload=payload,
+                             device=info.device if payload == "rccl" else "cpu",
+                             checkpoint_path=cfg.checkpoint,
+                             checkpoint_every=cfg.checkpoint_every)
+    if cfg.resume and os.path.exists(cfg.resume):
+        try:
+            server.load_checkpoint(cfg.resume)
+        except ValueError:
+            pass
+    stats = server.run()
+    if cfg.verbose:
+        print(f"[ps] finished: {stats}", flush=True)
+    return stats
+
+
+def run_training(cfg: TrainConfig, info: DistInfo):
+    """Entry point for every rank. Returns a result dict (worker) or PS stats."""
+    ps_groups = None
+    central = cfg.mode == "asgd" and cfg.ps == "central" and info.is_distributed
+    if central:
+        ps_groups = make_ps_groups(0, _payload(cfg, info))
+        if info.rank == 0:
+            return {"role": "ps", **run_server(cfg, info, ps_groups)}
+    w = Worker(cfg, info, ps_groups)
+    tr, te, source = get_datasets(cfg.dataset, cfg.data_dir, w.input_shape, w.num_classes,
+                                  cfg.n_train, cfg.n_test, seed=cfg.seed)
+    # every worker sees the full dataset in its own shuffle order (reference has no
+    # DistributedSampler, main.py:27); sync-DP shards by rank instead.
+    if cfg.mode == "sync" and info.is_distributed:
+        idx = list(range(info.rank, len(tr), info.world_size))
+        tr = torch.utils.data.Subset(tr, idx)
+    train_loader, test_loader = make_loaders(tr, te, cfg.batch_size, cfg.test_batch_size,
+                                             shuffle_seed=cfg.seed + info.rank)
+    log = IterationLog()
+    meter = Throughput(sync_cuda=w.device.type == "cuda")
+    base_lr = cfg.lr
+    done = False
+    t_start = time.perf_counter()
+    for epoch in range(cfg.epochs):
+        if cfg.lr_schedule == "inv_epoch":
+            w.set_lr(base_lr / (epoch + 1))
+        if cfg.verbose and info.rank <= 1:
+            print(f"Training for epoch {epoch}", flush=True)
+        for i, (xb, yb) in enumerate(train_loader):
+            xb, yb = w.prepare(xb, yb)
+            loss, hits = w.train_step(xb, yb)
+            meter.add(yb.numel())
+            row = log.append(epoch, i, loss)
+            if cfg.log_interval and i % cfg.log_interval == 0 and i > 0:
+                row["samples_per_sec"] = meter.rate()
+                if cfg.evaluate:
+                    row["test_loss"], row["test_accuracy"] = w.evaluate(test_loader)
+                log.flush_pending()
+                if cfg.verbose:
+                    print("Timestamp: {timestamp} | Iteration: {iteration:6} | "
+                          "Loss: {training_loss:6.4f} | Test Loss: {tl} | Test Accuracy: {ta} | "
+                          "samples/s: {sps:.1f}".format(
+                              tl=_fmt(row.get("test_loss")), ta=_fmt(row.get("test_accuracy")),
+                              sps=row["samples_per_sec"], **row), flush=True)
+            if cfg.checkpoint and cfg.checkpoint_every and w.step_idx % cfg.checkpoint_every == 0:
+                ckpt.save_worker_checkpoint(_worker_ckpt(cfg, info), w.model, w.opt, w.step_idx)
+            if cfg.max_steps and w.step_idx >= cfg.max_steps:
+                done = True
+                break
+        if cfg.evaluate and not done:
+            vl, va = w.evaluate(test_loader)
+            if cfg.verbose:
+                print(f"epoch {epoch}: lr {w.opt.param_groups[0]['lr']:.5g} "
+                      f"test loss {vl:.4f} test accuracy {va:.4f}", flush=True)
+        if done:
+            break
+    w.finish()
+    elapsed = time.perf_counter() - t_start
+    final = w.evaluate(test_loader) if cfg.evaluate else (float("nan"), float("nan"))
+    if cfg.checkpoint:
+        ckpt.save_worker_checkpoint(_worker_ckpt(cfg, info), w.model, w.opt, w.step_idx)
+    from ..utils.metrics import log_path
+
+    path = log_path(cfg.mode == "single" and not info.is_distributed,
+                    w.device.type == "cuda", info.rank, cfg.log_dir)
+    log.to_csv(path)
+    res = {"role": "worker", "rank": info.rank, "steps": w.step_idx, "elapsed_s": elapsed,
+           "samples_per_sec": meter.rate(), "test_loss": final[0], "test_accuracy": final[1],
+           "data": source, "log": path}
+    if isinstance(w.opt, Asynchronous):
+        res.update(w.opt.stats())
+    if cfg.verbose:
+        print(f"[worker {info.rank}] {res}", flush=True)
+    return res
+
+
+def _worker_ckpt(cfg, info):
+    base = cfg.checkpoint
+    root, ext = os.path.splitext(base)
+    return f"{root}.worker{info.rank}{ext or '.pt'}"
+
+
+def _fmt(v):
+    return "   n/a" if v is None or (isinstance(v, float) and math.isnan(v)) else f"{v:6.4f}"
+
+
+def config_dict(cfg: TrainConfig) -> dict:
+    return asdict(cfg)

@@ -1,0 +1,200 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+
+@pytest.fixture(scope="module")
+def nat():
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    return native()
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------- optimizer
+@pytest.mark.parametrize("momentum,wd,nesterov", [(0.0, 0.0, False), (0.9, 5e-4, False),
+                                                  (0.9, 0.0, True)])
+def test_asgd_fused_step(nat, momentum, wd, nesterov):
+    n = 4096 * 7 + 64
+    g = torch.randn(n, device="cuda")
+    p = torch.randn(n, device="cuda")
+    acc = torch.randn(n, device="cuda")
+    mom = torch.randn(n, device="cuda") if momentum else None
+    w16 = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    lr = 0.1
+    # reference
+    d = g + wd * p
+    rm = None
+    if momentum:
+        rm = momentum * mom + d
+        d = d + momentum * rm if nesterov else rm
+    rp = p - lr * d
+    racc = acc - lr * d
+    nat.asgd_fused_step(g, p, acc, mom, w16, lr, wd, momentum, 0.0, nesterov)
+    torch.testing.assert_close(p, rp, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(acc, racc, rtol=1e-6, atol=1e-6)
+    if momentum:
+        torch.testing.assert_close(mom, rm, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(w16, rp.to(torch.bfloat16), rtol=0, atol=0)
+
+
+def test_ps_apply_and_pull_land(nat):
+    n = 1 << 16
+    shard = torch.randn(n, device="cuda")
+    delta = torch.randn(n, device="cuda")
+    ref = shard + 0.5 * delta
+    mirror = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    nat.ps_apply(shard, delta, mirror, 0.5)
+    torch.testing.assert_close(shard, ref)
+    torch.testing.assert_close(mirror, ref.to(torch.bfloat16), rtol=0, atol=0)
+    d16 = delta.to(torch.bfloat16)
+    ref2 = shard + d16.float()
+    nat.ps_apply(shard, d16, None, 1.0)
+    torch.testing.assert_close(shard, ref2)
+    p = torch.empty(n, device="cuda")
+    acc = torch.randn(n, device="cuda")
+    w16 = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    nat.pull_land(p, shard, acc, w16)
+    torch.testing.assert_close(p, shard + acc)
+    nat.pull_land(p, shard, None, w16)
+    torch.testing.assert_close(p, shard)
+    torch.testing.assert_close(w16, shard.to(torch.bfloat16), rtol=0, atol=0)
+
+
+def test_push_handoff_and_sumsq(nat):
+    n = 1 << 15
+    acc = torch.randn(n, device="cuda")
+    ref = acc.clone()
+    o32 = torch.empty_like(acc)
+    o16 = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    nat.push_handoff(acc, o32, o16)
+    torch.testing.assert_close(o32, ref)
+    torch.testing.assert_close(o16, ref.to(torch.bfloat16), rtol=0, atol=0)
+    assert int((acc != 0).sum()) == 0
+    x = torch.randn(n, device="cuda")
+    torch.testing.assert_close(nat.sumsq(x), (x.double() ** 2).sum().float(), rtol=1e-4, atol=1e-3)
+
+
+def test_native_rejects_bad_shapes(nat):
+    with pytest.raises(RuntimeError):
+        nat.asgd_fused_step(torch.zeros(6, device="cuda"), torch.zeros(6, device="cuda"),
+                            None, None, None, 0.1, 0.0, 0.0, 0.0, False)
+    with pytest.raises(RuntimeError):
+        nat.bn_fwd(torch.zeros(2, 12, 4, 4, device="cuda", dtype=torch.bfloat16)
+                   .contiguous(memory_format=CL), None, None, None, None, None, 0.1, 1e-5,
+                   True, False)
+
+
+# --------------------------------------------------------------- cross entropy
+@pytest.mark.parametrize("B,C,dtype", [(64, 10, torch.bfloat16), (256, 10, torch.float32),
+                                       (1000, 1000, torch.bfloat16), (3, 130, torch.float32)])
+def test_softmax_xent(B, C, dtype):
+    from distributed_ml_pytorch_amd.ops.functional import softmax_cross_entropy
+
+    logits = (torch.randn(B, C, device="cuda") * 3).to(dtype).requires_grad_(True)
+    y = torch.randint(0, C, (B,), device="cuda")
+    loss, hits = softmax_cross_entropy(logits, y)
+    loss.backward()
+    ref_in = logits.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(ref_in, y)
+    ref.backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(loss.float(), ref, rtol=tol, atol=tol)
+    torch.testing.assert_close(logits.grad.float(), ref_in.grad, rtol=tol, atol=tol / 10)
+    assert int(hits) == int((ref_in.argmax(1) == y).sum())
+
+
+# ------------------------------------------------------------------ batchnorm
+@pytest.mark.parametrize("shape,relu,res", [((8, 64, 16, 16), True, False),
+                                            ((4, 128, 8, 8), True, True),
+                                            ((16, 512, 4, 4), False, True),
+                                            ((2, 192, 5, 7), False, False)])
+def test_bn_act_fwd_bwd(shape, relu, res):
+    from distributed_ml_pytorch_amd.ops.functional import batch_norm_act
+
+    C = shape[1]
+    x = torch.randn(shape, device="cuda") * 2 + 0.5
+    r = torch.randn(shape, device="cuda") if res else None
+    gamma = (torch.rand(C, device="cuda") + 0.5).requires_grad_(True)
+    beta = torch.randn(C, device="cuda").requires_grad_(True)
+    rm = torch.zeros(C, device="cuda")
+    rv = torch.ones(C, device="cuda")
+    xb = _bf(x).contiguous(memory_format=CL).requires_grad_(True)
+    rb = _bf(r).contiguous(memory_format=CL).requires_grad_(True) if res else None
+    y = batch_norm_act(xb, gamma, beta, rm, rv, True, 0.1, 1e-5, relu=relu, residual=rb)
+    # fp32 reference on the SAME bf16-rounded inputs
+    xr = xb.detach().float().requires_grad_(True)
+    rr = rb.detach().float().requires_grad_(True) if res else None
+    g2 = gamma.detach().clone().requires_grad_(True)
+    b2 = beta.detach().clone().requires_grad_(True)
+    rm2 = torch.zeros(C, device="cuda")
+    rv2 = torch.ones(C, device="cuda")
+    yr = F.batch_norm(xr, rm2, rv2, g2, b2, True, 0.1, 1e-5)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = F.relu(yr)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(rm, rm2, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rv, rv2, rtol=1e-4, atol=1e-4)
+    dy = torch.randn(shape, device="cuda")
+    (y.float() * dy).sum().backward()
+    (yr * dy).sum().backward()
+    torch.testing.assert_close(xb.grad.float(), xr.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(gamma.grad, g2.grad, rtol=2e-2, atol=2e-1)
+    torch.testing.assert_close(beta.grad, b2.grad, rtol=2e-2, atol=2e-1)
+    if res:
+        torch.testing.assert_close(rb.grad.float(), rr.grad, rtol=2e-2, atol=2e-2)
+
+
+def test_bn_eval_uses_running_stats():
+    from distributed_ml_pytorch_amd.ops.functional import batch_norm_act
+
+    C = 64
+    x = _bf(torch.randn(4, C, 8, 8, device="cuda")).contiguous(memory_format=CL)
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.randn(C, device="cuda")
+    rm = torch.randn(C, device="cuda")
+    rv = torch.rand(C, device="cuda") + 0.5
+    y = batch_norm_act(x, gamma, beta, rm, rv, False, 0.1, 1e-5, relu=True)
+    yr = F.relu(F.batch_norm(x.float(), rm, rv, gamma, beta, False, 0.1, 1e-5))
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+
+
+# -------------------------------------------------------------------- pooling
+def test_global_avg_pool():
+    from distributed_ml_pytorch_amd.ops.functional import global_avg_pool
+
+    x = _bf(torch.randn(32, 512, 4, 4, device="cuda")).contiguous(memory_format=CL)
+    x.requires_grad_(True)
+    y = global_avg_pool(x)
+    xr = x.detach().float().requires_grad_(True)
+    yr = xr.mean(dim=(2, 3))
+    torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
+    dy = torch.randn_like(yr)
+    (y.float() * dy).sum().backward()
+    (yr * dy).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-3)
+
+
+@pytest.mark.parametrize("shape,k", [((8, 64, 8, 8), 2), ((4, 192, 5, 5), 2), ((2, 16, 9, 9), 3)])
+def test_max_pool(shape, k):
+    from distributed_ml_pytorch_amd.ops.functional import max_pool2d
+
+    x = _bf(torch.randn(shape, device="cuda")).contiguous(memory_format=CL).requires_grad_(True)
+    y = max_pool2d(x, k)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.max_pool2d(xr, k)
+    torch.testing.assert_close(y.float(), yr, rtol=0, atol=0)
+    dy = torch.randn_like(yr)
+    (y.float() * dy).sum().backward()
+    (yr * dy).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
