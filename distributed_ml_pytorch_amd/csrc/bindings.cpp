@@ -300,9 +300,127 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t K) {
   return dx;
 }
 
+// ---------------------------------------------------------------- convolution
+// x: bf16 channels_last [B, CI, H, W]; w: bf16 channels_last [CO, CI, R, S].
+struct ConvGeom {
+  int B, CI, H, W, CO, R, S, OH, OW;
+};
+
+ConvGeom conv_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad) {
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv: 4-D tensors expected");
+  ConvGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(0),
+             (int)w.size(2), (int)w.size(3), 0, 0};
+  TORCH_CHECK(w.size(1) == g.CI, "conv: weight/input channel mismatch");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "conv: bad stride/pad");
+  g.OH = (g.H + 2 * (int)pad - g.R) / (int)stride + 1;
+  g.OW = (g.W + 2 * (int)pad - g.S) / (int)stride + 1;
+  TORCH_CHECK(g.OH > 0 && g.OW > 0, "conv: empty output");
+  TORCH_CHECK(g.CI % 64 == 0 && g.CO % 64 == 0,
+              "native conv needs CI % 64 == 0 and CO % 64 == 0 (got ", g.CI, ", ", g.CO, ")");
+  TORCH_CHECK((long long)g.B * g.H * g.W * g.CI < (1LL << 31) &&
+                  (long long)g.B * g.OH * g.OW * g.CO < (1LL << 31),
+              "native conv: tensor too large for 32-bit pixel indexing");
+  return g;
+}
+
+std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bool want_stats) {
+  check_nhwc_bf16(x, "x");
+  check_gpu(w, "w");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv weight must be bf16 channels_last");
+  auto g = conv_geom(x, w, stride, pad);
+  auto y = at::empty({g.B, g.CO, g.OH, g.OW},
+                     x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor part;
+  int64_t G = 0;
+  if (want_stats) {
+    G = dmp::conv_fwd_num_mblocks((long long)g.B * g.OH * g.OW, g.CO);
+    part = at::empty({2 * G * g.CO}, x.options().dtype(at::kFloat));
+  }
+  dmp::launch_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                       reinterpret_cast<uint16_t*>(y.data_ptr()),
+                       want_stats ? part.data_ptr<float>() : nullptr, g.B, g.H, g.W, g.CI, g.OH,
+                       g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, cur_stream());
+  return {y, part, at::scalar_tensor(G, at::kLong)};
+}
+
+Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc_bf16(dy, "dy");
+  check_gpu(w, "w");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv weight must be bf16 channels_last");
+  const int B = (int)dy.size(0);
+  auto xshape = at::empty({0}, dy.options());
+  ConvGeom g{B, (int)w.size(1), (int)H, (int)W, (int)w.size(0), (int)w.size(2), (int)w.size(3),
+             (int)dy.size(2), (int)dy.size(3)};
+  TORCH_CHECK(dy.size(1) == g.CO, "dgrad: dy channels mismatch");
+  TORCH_CHECK((g.H + 2 * pad - g.R) / stride + 1 == g.OH && (g.W + 2 * pad - g.S) / stride + 1 == g.OW,
+              "dgrad: geometry mismatch");
+  TORCH_CHECK(g.CI % 64 == 0 && g.CO % 64 == 0, "native dgrad needs CI, CO % 64 == 0");
+  auto wt = at::empty({g.CI, g.R, g.S, g.CO}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  dmp::launch_conv_weight_transpose(reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                    reinterpret_cast<uint16_t*>(wt.data_ptr()), g.CO, g.R * g.S,
+                                    g.CI, cur_stream());
+  auto dx = at::empty({B, g.CI, g.H, g.W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dmp::launch_conv_dgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(wt.data_ptr()),
+                         reinterpret_cast<uint16_t*>(dx.data_ptr()), B, g.H, g.W, g.CI, g.OH,
+                         g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, cur_stream());
+  return dx;
+}
+
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc_bf16(dy, "dy");
+  check_nhwc_bf16(x, "x");
+  check_gpu(dw, "dw");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 4 &&
+                  dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "dw must be an fp32 channels_last [CO, CI, R, S] tensor");
+  auto g = conv_geom(x, dw, stride, pad);
+  TORCH_CHECK(dy.size(0) == g.B && dy.size(1) == g.CO && dy.size(2) == g.OH && dy.size(3) == g.OW,
+              "wgrad: dy shape mismatch");
+  dmp::launch_conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(x.data_ptr()), dw.data_ptr<float>(),
+                         g.B, g.H, g.W, g.CI, g.OH, g.OW, g.CO, g.R, g.S, (int)stride, (int)pad,
+                         cur_stream());
+}
+
+std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optional<Tensor> res,
+                                         optional<Tensor> gamma, optional<Tensor> beta,
+                                         optional<Tensor> running_mean,
+                                         optional<Tensor> running_var, double momentum,
+                                         double eps, bool relu) {
+  check_nhwc_bf16(x, "x");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: bad C");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() == 2 * G * C, "bad partials");
+  if (res) {
+    check_nhwc_bf16(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "res shape mismatch");
+  }
+  auto y = at::empty_like(x);
+  auto stats = at::empty({4, C}, x.options().dtype(at::kFloat));
+  dmp::launch_bn_fwd_partials(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                              res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr,
+                              reinterpret_cast<uint16_t*>(y.data_ptr()), ptr_or_null<float>(gamma),
+                              ptr_or_null<float>(beta), ptr_or_null<float>(running_mean),
+                              ptr_or_null<float>(running_var), stats.data_ptr<float>(),
+                              part.data_ptr<float>(), (int)G, M, (int)C, (float)momentum,
+                              (float)eps, relu, cur_stream());
+  return {y, stats};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
+  m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM conv forward (+BN partials)");
+  m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM conv data gradient");
+  m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient (fp32 accumulate)");
+  m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials");
   m.doc() = "gfx950 (MI355X) HIP kernels for distributed_ml_pytorch_amd";
   m.def("asgd_fused_step", &asgd_fused_step, "fused flat ASGD/SGD update");
   m.def("ps_apply", &ps_apply, "parameter-server delta apply");

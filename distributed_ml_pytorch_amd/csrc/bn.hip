@@ -87,25 +87,47 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(
 }
 
 // -------- forward finalize: stats = [mean | invstd | scale | shift] -------
-__global__ void __launch_bounds__(256) bn_fwd_finalize_kernel(
+// Block = 64 channels x 16 partial-slices (1024 threads): coalesced loads of
+// the [G][C] partial arrays, LDS tree over the slices.
+__device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int G, int C,
+                                                int c, float& S, float& Q) {
+  __shared__ float rs[16][64], rq[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    for (int g = ty; g < G; g += 16) {
+      a += part[(long long)g * C + c];
+      b += part[(long long)(G + g) * C + c];
+    }
+  }
+  rs[ty][tx] = a;
+  rq[ty][tx] = b;
+  __syncthreads();
+  if (ty == 0) {
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { sa += rs[k][tx]; sb += rq[k][tx]; }
+    S = sa;
+    Q = sb;
+  }
+}
+
+__global__ void __launch_bounds__(1024) bn_fwd_finalize_kernel(
     const float* __restrict__ part, int G, long long M, int C, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ running_mean,
     float* __restrict__ running_var, float momentum, float eps, float* __restrict__ stats,
     int use_running) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  float S = 0.f, Q = 0.f;
+  if (!use_running) reduce_partials(part, G, C, c, S, Q);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
   float mean, var;
   if (use_running) {
     mean = running_mean[c];
     var = running_var[c];
   } else {
-    double S = 0.0, Q = 0.0;
-    for (int g = 0; g < G; ++g) { S += part[(long long)g * C + c]; Q += part[(long long)(G + g) * C + c]; }
-    const double dm = S / (double)M;
-    double dv = Q / (double)M - dm * dm;
-    if (dv < 0.0) dv = 0.0;
-    mean = (float)dm;
-    var = (float)dv;
+    mean = S / (float)M;
+    var = fmaxf(Q / (float)M - mean * mean, 0.f);
     if (running_mean) {
       const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
       running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
@@ -153,16 +175,16 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(
 }
 
 // -------- backward finalize: coef = [A | Bc | Cc] -----------------------------
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(
     const float* __restrict__ part, int G, long long M, int C, const float* __restrict__ gamma,
     const float* __restrict__ stats, float* __restrict__ dgamma, float* __restrict__ dbeta,
     float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double S = 0.0, Q = 0.0;
-  for (int g = 0; g < G; ++g) { S += part[(long long)g * C + c]; Q += part[(long long)(G + g) * C + c]; }
-  const float db = (float)S;   // sum dz
-  const float dg = (float)Q;   // sum dz * xhat
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  float S = 0.f, Q = 0.f;
+  reduce_partials(part, G, C, c, S, Q);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  const float db = S;   // sum dz
+  const float dg = Q;   // sum dz * xhat
   if (dgamma) dgamma[c] += dg;
   if (dbeta) dbeta[c] += db;
   const float mean = stats[c], inv = stats[C + c];
@@ -205,9 +227,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
 // ---------------------------------------------------------------- launchers
 int bn_num_partials(long long M, int C) {
   long long vecs = M * (C / 8);
-  long long g = vecs / (256 * 8);
+  long long g = vecs / (256 * 16);
   if (g < 1) g = 1;
-  if (g > 1024) g = 1024;
+  if (g > 512) g = 512;
   if (g > M) g = M;
   return (int)g;
 }
@@ -223,7 +245,7 @@ void launch_bn_fwd(const u16* x, const u16* res, u16* y, const float* gamma, con
     hipLaunchKernelGGL((bn_partial_kernel<0, false>), dim3(G), dim3(256), lds, s, x, nullptr,
                        nullptr, nullptr, part, M, C);
   }
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, M,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, G, M,
                      C, gamma, beta, running_mean, running_var, momentum, eps, stats,
                      training ? 0 : 1);
   const long long nvec = M * C / 8;
@@ -247,7 +269,7 @@ void launch_bn_bwd(const u16* x, const u16* dy, const u16* y, const float* gamma
     hipLaunchKernelGGL((bn_partial_kernel<1, true>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, M, C);
   else
     hipLaunchKernelGGL((bn_partial_kernel<1, false>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, M, C);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, M,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, G, M,
                      C, gamma, stats, dgamma, dbeta, coef);
   const long long nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, 256));
@@ -260,4 +282,25 @@ void launch_bn_bwd(const u16* x, const u16* dy, const u16* y, const float* gamma
   }
 }
 
+}  // namespace dmp
+
+namespace dmp {
+// BN forward whose statistics were already reduced per block by the producing
+// conv's epilogue (conv.hip STATS): finalize + apply only, no stats pass over x.
+void launch_bn_fwd_partials(const u16* x, const u16* res, u16* y, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            float* stats, const float* part, int G, long long M, int C,
+                            float momentum, float eps, bool relu, hipStream_t s) {
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, G, M,
+                     C, gamma, beta, running_mean, running_var, momentum, eps, stats, 0);
+  const long long nvec = M * C / 8;
+  const dim3 grid(stream_grid(nvec, 256));
+  if (relu) {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<true, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
+  } else {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<false, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
+  }
+}
 }  // namespace dmp

@@ -50,3 +50,26 @@ void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, in
                         int C, int K, hipStream_t s);
 
 }  // namespace dmp
+
+namespace dmp {
+// conv.hip
+int conv_fwd_num_mblocks(long long M, int CO);
+void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int B, int H,
+                     int W, int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
+                     hipStream_t s);
+void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int B, int H, int W,
+                       int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
+                       hipStream_t s);
+void launch_conv_weight_transpose(const uint16_t* w, uint16_t* wt, int CO, int RS, int CI,
+                                  hipStream_t s);
+void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int B, int H, int W,
+                       int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
+                       hipStream_t s);
+}  // namespace dmp
+
+namespace dmp {
+void launch_bn_fwd_partials(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            float* stats, const float* part, int G, long long M, int C,
+                            float momentum, float eps, bool relu, hipStream_t s);
+}  // namespace dmp

@@ -92,6 +92,8 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            if isinstance(m, L.Conv2d):
+                m.emit_bn_stats = True      # every conv here feeds a BatchNorm
         if zero_init_residual:
             for m in self.modules():
                 if isinstance(m, Bottleneck):

@@ -1,21 +1,97 @@
 """2-D convolution dispatch.
 
-Native path: NHWC bf16 implicit-GEMM on MFMA (``csrc/conv.hip``) for the
-shapes it supports; everything else goes to ``F.conv2d`` in channels_last.
+Native path (``csrc/conv.hip``): NHWC bf16 implicit GEMM on MFMA for
+``groups == 1, dilation == 1, CI % 64 == 0, CO % 64 == 0`` (every ResNet conv
+except the 3-channel stem, AlexNet conv2-5).  The weight operand is the
+arena's bf16 shadow (no per-step cast) and the weight gradient is accumulated
+in fp32 straight into the arena grad view (no AccumulateGrad, no cast
+kernels).  When the conv feeds a BatchNorm (``emit_bn_stats``) its epilogue
+also emits per-block channel sums, so the BN forward skips its statistics
+pass over the activation.
+
+Everything else goes to ``F.conv2d`` (MIOpen) in channels_last.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
+from torch.autograd import Function
 
-_NATIVE_CONV = None  # resolved lazily; set by ops.conv_native when built
+from ._ext import native
+
+_NATIVE_ENABLED = True
 
 
-def conv2d(x, w, b, stride, padding, dilation, groups, master=None):
+def set_native_conv(enabled: bool):
+    global _NATIVE_ENABLED
+    _NATIVE_ENABLED = bool(enabled)
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+class _NativeConv(Function):
+    @staticmethod
+    def forward(ctx, x, w16, master, stride, pad, want_stats):
+        y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats)
+        ctx.save_for_backward(x, w16)
+        ctx.master = master
+        ctx.geom = (x.shape[2], x.shape[3], stride, pad)
+        if want_stats:
+            ctx.mark_non_differentiable(part)
+            return y, part
+        return y, None
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w16 = ctx.saved_tensors
+        H, W, stride, pad = ctx.geom
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = native().conv_dgrad(dy, w16, H, W, stride, pad)
+        master = ctx.master
+        gw = None
+        if master is not None and master.requires_grad:
+            g = master.grad if getattr(master, "_dmp_arena", False) else None
+            if g is not None and g.is_contiguous(memory_format=torch.channels_last):
+                native().conv_wgrad(dy, x, g, stride, pad)
+                cb = getattr(master, "_dmp_grad_ready", None)
+                if cb is not None:
+                    cb(master)
+            else:
+                gw = torch.zeros(master.shape, dtype=torch.float32, device=x.device,
+                                 memory_format=torch.channels_last)
+                native().conv_wgrad(dy, x, gw, stride, pad)
+                gw = gw.to(master.dtype)
+        return dx, None, gw, None, None, None
+
+
+def native_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
+    if not (_NATIVE_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+        return False
+    if groups != 1 or _pair(dilation) != (1, 1):
+        return False
+    st, pd = _pair(stride), _pair(padding)
+    if st[0] != st[1] or pd[0] != pd[1] or not isinstance(pd[0], int):
+        return False
+    co, ci = weight.shape[0], weight.shape[1]
+    return ci % 64 == 0 and co % 64 == 0
+
+
+def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=False):
+    """Returns ``y`` (and attaches BN partials to it when ``want_stats``)."""
     if x.is_cuda and x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
-        if _NATIVE_CONV is not None:
-            y = _NATIVE_CONV(x, w, b, stride, padding, dilation, groups, master)
-            if y is not None:
-                return y
+        if master is not None and b is None and native_conv_supported(
+                x, master, stride, padding, dilation, groups):
+            w16 = getattr(master, "_dmp_w16", None)
+            if w16 is None or not w16.is_contiguous(memory_format=torch.channels_last):
+                w16 = master.detach().to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last)
+            y, part = _NativeConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
+                                        bool(want_stats))
+            if part is not None:
+                y._dmp_bn_part = part
+            return y
     return F.conv2d(x, w, b, stride, padding, dilation, groups)

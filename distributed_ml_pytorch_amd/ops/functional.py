@@ -108,13 +108,20 @@ def softmax_cross_entropy(logits, labels, label_smoothing: float = 0.0, ignore_i
 class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
-                relu):
+                relu, part=None):
         if x.dim() == 4:
             x = x.contiguous(memory_format=CL)
             if residual is not None:
                 residual = residual.contiguous(memory_format=CL)
-        y, stats = native().bn_fwd(x, residual, gamma, beta, running_mean, running_var,
-                                   float(momentum), float(eps), bool(training), bool(relu))
+        if part is not None and training:
+            # statistics already reduced per block by the producing conv's epilogue
+            C = x.shape[1]
+            y, stats = native().bn_fwd_from_partials(
+                x, part, part.numel() // (2 * C), residual, gamma, beta, running_mean,
+                running_var, float(momentum), float(eps), bool(relu))
+        else:
+            y, stats = native().bn_fwd(x, residual, gamma, beta, running_mean, running_var,
+                                       float(momentum), float(eps), bool(training), bool(relu))
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.gamma, ctx.beta = gamma, beta
@@ -141,7 +148,8 @@ class _BNAct(Function):
             _notify(gamma, beta)
         ret_g = None if (dg_arena is not None or not need_g) else dg
         ret_b = None if (db_arena is not None or not need_b) else db
-        return dx, ret_g, ret_b, (dres if ctx.has_res else None), None, None, None, None, None, None
+        return (dx, ret_g, ret_b, (dres if ctx.has_res else None), None, None, None, None, None,
+                None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float,
@@ -150,8 +158,9 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, m
     if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0 and x.shape[1] <= 2048:
         if not training and (running_mean is None or running_var is None):
             training = True
+        part = getattr(x, "_dmp_bn_part", None) if training else None
         return _BNAct.apply(x, weight, bias, residual, running_mean, running_var, training,
-                            momentum, eps, relu)
+                            momentum, eps, relu, part)
     if x.is_cuda:
         raise RuntimeError(
             f"batch_norm_act: unsupported GPU input (dtype={x.dtype}, C={x.shape[1]}); "

@@ -12,15 +12,28 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import functional as DF
-from .conv import conv2d as _conv2d
+from .conv import conv2d as _conv2d, native_conv_supported
 
 
 class Conv2d(nn.Conv2d):
+    """Conv2d on the native NHWC implicit-GEMM kernels when the shape allows.
+
+    ``emit_bn_stats`` (set by models where a BatchNorm follows) makes the
+    native forward also produce the BN partial sums in its epilogue.
+    """
+
+    emit_bn_stats = False
+
     def forward(self, x):
+        if (x.is_cuda and self.bias is None
+                and native_conv_supported(x, self.weight, self.stride, self.padding,
+                                          self.dilation, self.groups)):
+            return _conv2d(x, None, None, self.stride, self.padding, self.dilation, self.groups,
+                           master=self.weight,
+                           want_stats=self.emit_bn_stats and self.training)
         w = DF.compute_weight(self.weight, x.dtype)
         b = DF.compute_weight(self.bias, x.dtype)
-        return _conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups,
-                       master=self.weight)
+        return _conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups)
 
 
 class Linear(nn.Linear):

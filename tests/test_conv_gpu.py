@@ -1,0 +1,93 @@
+"""Native NHWC implicit-GEMM conv (fwd / dgrad / wgrad / fused BN partials) vs fp32 PyTorch."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+CL = torch.channels_last
+
+SHAPES = [
+    # B, CI, H, W, CO, k, stride, pad
+    (4, 64, 32, 32, 64, 3, 1, 1),
+    (2, 64, 16, 16, 128, 3, 2, 1),
+    (2, 64, 16, 16, 128, 1, 2, 0),
+    (3, 128, 8, 8, 256, 3, 1, 1),
+    (2, 256, 8, 8, 512, 3, 2, 1),
+    (2, 192, 4, 4, 384, 3, 1, 1),      # AlexNet conv3 (CI=192: BK=64 tiles)
+    (2, 64, 5, 7, 64, 3, 1, 1),        # odd spatial, M not a tile multiple
+    (1, 512, 4, 4, 512, 3, 1, 1),
+]
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+@pytest.mark.parametrize("B,CI,H,W,CO,k,st,pd", SHAPES)
+def test_conv_fwd_dgrad_wgrad(B, CI, H, W, CO, k, st, pd):
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    torch.manual_seed(0)
+    x = torch.randn(B, CI, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(CO, CI, k, k, device="cuda") / (CI * k * k) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    y, part, G = nat.conv_fwd(x, w, st, pd, True)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, st, pd)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
+    assert _rel(y, yr) < 1e-2
+    # fused BN partial sums == per-channel sums of the (bf16-rounded) output
+    C = CO
+    G = int(G)
+    ps = part.view(2, G, C).sum(1)
+    yf = y.float()
+    torch.testing.assert_close(ps[0], yf.sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(ps[1], (yf * yf).sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+    # backward
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr.backward(dy.float())
+    dx = nat.conv_dgrad(dy, w, H, W, st, pd)
+    assert dx.shape == x.shape
+    assert _rel(dx, xr.grad) < 1e-2
+    dw = torch.zeros(CO, CI, k, k, device="cuda").contiguous(memory_format=CL)
+    nat.conv_wgrad(dy, x, dw, st, pd)
+    assert _rel(dw, wr.grad) < 1e-2
+    # accumulation semantics (fp32 atomics add into the existing grad)
+    nat.conv_wgrad(dy, x, dw, st, pd)
+    assert _rel(dw, 2 * wr.grad) < 1e-2
+
+
+def test_conv_layer_autograd_and_bn_fusion():
+    """Conv2d(native) -> BatchNorm2d(partials) matches the stock fp32 chain."""
+    from distributed_ml_pytorch_amd.ops import layers as L
+
+    torch.manual_seed(0)
+    conv = L.Conv2d(64, 128, 3, stride=1, padding=1, bias=False).cuda()
+    conv.emit_bn_stats = True
+    bn = L.BatchNorm2d(128, relu=True).cuda()
+    x = torch.randn(8, 64, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    x.requires_grad_(True)
+    y = bn(conv(x))
+    assert hasattr(conv(x.detach()), "_dmp_bn_part")
+    xr = x.detach().float().requires_grad_(True)
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.relu(F.batch_norm(F.conv2d(xr, wr, None, 1, 1), None, None,
+                             bn.weight.detach(), bn.bias.detach(), True))
+    assert _rel(y, yr) < 2e-2
+    g = torch.randn_like(yr)
+    (y.float() * g).sum().backward()
+    (yr * g).sum().backward()
+    assert _rel(x.grad, xr.grad) < 3e-2
+    assert _rel(conv.weight.grad, wr.grad) < 3e-2
+
+
+def test_unsupported_shapes_fall_back():
+    from distributed_ml_pytorch_amd.ops import layers as L
+
+    conv = L.Conv2d(3, 64, 3, padding=1, bias=False).cuda()   # stem: CI=3 -> MIOpen
+    x = torch.randn(2, 3, 8, 8, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    y = conv(x)
+    yr = F.conv2d(x.float(), conv.weight.float().to(torch.bfloat16).float(), None, 1, 1)
+    assert _rel(y, yr) < 1e-2

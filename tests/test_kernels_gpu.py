@@ -43,7 +43,7 @@ def test_asgd_fused_step(nat, momentum, wd, nesterov):
     torch.testing.assert_close(acc, racc, rtol=1e-6, atol=1e-6)
     if momentum:
         torch.testing.assert_close(mom, rm, rtol=1e-6, atol=1e-6)
-    torch.testing.assert_close(w16, rp.to(torch.bfloat16), rtol=0, atol=0)
+    torch.testing.assert_close(w16, p.to(torch.bfloat16), rtol=0, atol=0)
 
 
 def test_ps_apply_and_pull_land(nat):
