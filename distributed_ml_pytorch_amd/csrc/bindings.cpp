@@ -323,7 +323,8 @@ ConvGeom conv_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad
   return g;
 }
 
-std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bool want_stats) {
+std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bool want_stats,
+                             int64_t cfg) {
   check_nhwc_bf16(x, "x");
   check_gpu(w, "w");
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -334,18 +335,19 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
   Tensor part;
   int64_t G = 0;
   if (want_stats) {
-    G = dmp::conv_fwd_num_mblocks((long long)g.B * g.OH * g.OW, g.CO);
+    G = dmp::conv_fwd_num_mblocks((long long)g.B * g.OH * g.OW, g.CO, (int)cfg);
     part = at::empty({2 * G * g.CO}, x.options().dtype(at::kFloat));
   }
   dmp::launch_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                        reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()),
                        want_stats ? part.data_ptr<float>() : nullptr, g.B, g.H, g.W, g.CI, g.OH,
-                       g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, cur_stream());
+                       g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream());
   return {y, part, at::scalar_tensor(G, at::kLong)};
 }
 
-Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad) {
+Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                  int64_t cfg) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc_bf16(dy, "dy");
   check_gpu(w, "w");
@@ -367,11 +369,11 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   dmp::launch_conv_dgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                          reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                          reinterpret_cast<uint16_t*>(dx.data_ptr()), B, g.H, g.W, g.CI, g.OH,
-                         g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, cur_stream());
+                         g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream());
   return dx;
 }
 
-void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad) {
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t cfg) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc_bf16(dy, "dy");
   check_nhwc_bf16(x, "x");
@@ -385,7 +387,17 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad) {
   dmp::launch_conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                          reinterpret_cast<const uint16_t*>(x.data_ptr()), dw.data_ptr<float>(),
                          g.B, g.H, g.W, g.CI, g.OH, g.OW, g.CO, g.R, g.S, (int)stride, (int)pad,
-                         cur_stream());
+                         (int)cfg, cur_stream());
+}
+
+std::vector<std::vector<int64_t>> conv_configs() {
+  std::vector<std::vector<int64_t>> out;
+  for (int c = 0; c < dmp::conv_num_configs(); ++c) {
+    int info[4];
+    dmp::conv_config_info(c, info);
+    out.push_back({c, info[0], info[1], info[2], info[3]});
+  }
+  return out;
 }
 
 std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optional<Tensor> res,
@@ -417,9 +429,16 @@ std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optio
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
-  m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM conv forward (+BN partials)");
-  m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM conv data gradient");
-  m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient (fp32 accumulate)");
+  m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM conv forward (+BN partials)",
+        py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
+        py::arg("cfg") = -1);
+  m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM conv data gradient", py::arg("dy"),
+        py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"),
+        py::arg("cfg") = -1);
+  m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient (fp32 accumulate)",
+        py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
+        py::arg("cfg") = -1);
+  m.def("conv_configs", &conv_configs, "[(id, BM, BN, BK, threads)] of the compiled conv tiles");
   m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials");
   m.doc() = "gfx950 (MI355X) HIP kernels for distributed_ml_pytorch_amd";
   m.def("asgd_fused_step", &asgd_fused_step, "fused flat ASGD/SGD update");

@@ -4,18 +4,24 @@
 // /root/reference/example/models.py:8-9,28-38); these kernels replace the
 // ATen/MIOpen `convolution` + `convolution_backward` rows of SURVEY §2.3.
 //
-//   fwd   : Y[m][co]  = sum_k  X_gather[m][k] * W[co][k]     k = (r, s, ci), ci fastest
-//   dgrad : dX[m][ci] = sum_k dY_tgather[m][k] * Wt[ci][k]    k = (r, s, co), Wt = W^T per tap
-//           ("transposed gather": th = h + pad - r must be a multiple of stride)
-//   wgrad : dW[co][k] += sum_p dY[p][co] * X_gather[p][k]     split over p, fp32 atomics
-//           straight into the flat fp32 grad arena (channels_last weight layout).
+//   fwd   : Y[m][co]  = sum_k X_gather[m][k] * W[co][k]       k = (r, s, ci), ci fastest
+//   dgrad : dX = sum over the taps that actually reach each input pixel.  For
+//           stride st the input pixels split into st*st parity classes
+//           (h % st, w % st); class (ph, pw) is reached only by taps
+//           r = (ph+pad) mod st + i*st (same for s), so each class is a dense
+//           implicit GEMM over its own pixels with K = taps(class) * CO and no
+//           wasted MFMA work (blockIdx.z = class).  Wt[ci][r][s][co] = W^T per tap.
+//   wgrad : dW[co][k] += sum_p dY[p][co] * X_gather[p][k]       split over p, fp32
+//           atomics straight into the flat fp32 grad arena (channels_last layout).
+//           One block covers up to 3 taps (192 k-columns) so dY is re-read
+//           K/192 times, not once per tap.
 //
-// Tiles are staged through LDS with an XOR swizzle that makes the 16-lane
-// ds_read_b128 operand fetches bank-conflict free (derivation in the comments at
-// swz()).  fwd/dgrad compute D^T = W * X^T so each lane ends up owning 4
-// consecutive output channels of one pixel (8-byte NHWC stores), and can fold
-// per-channel BatchNorm partial sums into the epilogue (no extra pass over Y).
-// wgrad reads both [p][*] tiles with ds_read_b64_tr_b16 (hardware transpose).
+// LDS staging uses XOR swizzles that keep the operand reads bank-conflict free
+// (derivations at swz() / wg_off()).  fwd/dgrad compute D^T = W * X^T so a lane
+// owns 4 consecutive output channels of one pixel (8-byte NHWC stores) and the
+// fwd epilogue can reduce per-channel BatchNorm partial sums (no extra pass).
+// Several tile configurations are compiled; the host side times them per
+// shape on first use (ops/tuner.py) and keeps the fastest.
 #include "common.h"
 
 namespace dmp {
@@ -25,12 +31,12 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));
 
 struct ConvArgs {
-  const u16* x;     // gathered operand, NHWC [B][GH][GW][CI]
-  const u16* w;     // [CO][R][S][CI]
-  u16* y;           // [B][OH][OW][CO]
+  const u16* x;     // gathered operand NHWC [B][GH][GW][CI]   (fwd: X, dgrad: dY)
+  const u16* w;     // [CO][R][S][CI]                           (fwd: W, dgrad: Wt)
+  u16* y;           // output NHWC [B][OH][OW][CO]              (fwd: Y, dgrad: dX)
   float* part;      // optional BN partials [2][gridDim.x][CO]
   int B, GH, GW, CI, OH, OW, CO, R, S, stride, pad;
-  long long M;      // B*OH*OW
+  long long M;      // fwd: B*OH*OW; dgrad: rows of the largest parity class
 };
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -49,7 +55,8 @@ __device__ __forceinline__ int swz(int row, int c) {
   else return c ^ ((-(row >> 2)) & 3);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool TRANS, bool STATS>
+// MODE 0: forward conv.  MODE 1: data gradient, one parity class per blockIdx.z.
+template <int BM, int BN, int BK, int WM, int WN, int MODE, bool STATS>
 __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   constexpr int NT = 64 * WM * WN;
   constexpr int CPR = BK / 8;
@@ -69,21 +76,36 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   const int ch = tid % CPR, r0 = tid / CPR;
   const int GH = a.GH, GW = a.GW, CI = a.CI, st = a.stride;
 
-  // per-thread A rows: pixel base and the (h, w) origin of its receptive field
+  // class geometry (MODE 1) -------------------------------------------------
+  int ph = 0, pw = 0, r0h = 0, r0w = 0, nth = a.R, ntw = a.S, RH = a.OH, RW = a.OW;
+  long long Mc = a.M;
+  if (MODE == 1) {
+    ph = (int)blockIdx.z / st;
+    pw = (int)blockIdx.z - ph * st;
+    r0h = (ph + a.pad) % st;
+    r0w = (pw + a.pad) % st;
+    nth = a.R > r0h ? (a.R - r0h + st - 1) / st : 0;
+    ntw = a.S > r0w ? (a.S - r0w + st - 1) / st : 0;
+    RH = (a.OH - ph + st - 1) / st;    // output rows of this parity
+    RW = (a.OW - pw + st - 1) / st;
+    Mc = (long long)a.B * RH * RW;
+    if (m0 >= Mc) return;
+  }
+
   int a_pix[A_PER], a_h[A_PER], a_w[A_PER];
   bool a_ok[A_PER];
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) {
     const long long m = m0 + r0 + i * ROWSTEP;
-    a_ok[i] = m < a.M;
+    a_ok[i] = m < Mc;
     const long long mm = a_ok[i] ? m : 0;
-    const int ow = (int)(mm % a.OW);
-    const long long t = mm / a.OW;
-    const int oh = (int)(t % a.OH);
-    const int b = (int)(t / a.OH);
+    const int ow = (int)(mm % RW);
+    const long long t = mm / RW;
+    const int oh = (int)(t % RH);
+    const int b = (int)(t / RH);
     a_pix[i] = b * GH * GW;
-    if (!TRANS) { a_h[i] = oh * st - a.pad; a_w[i] = ow * st - a.pad; }
-    else        { a_h[i] = oh + a.pad;      a_w[i] = ow + a.pad; }
+    if (MODE == 0) { a_h[i] = oh * st - a.pad; a_w[i] = ow * st - a.pad; }
+    else           { a_h[i] = oh;              a_w[i] = ow; }
   }
   const long long K = (long long)a.R * a.S * CI;
   const u16* b_row[B_PER];
@@ -96,40 +118,35 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
     b_row[i] = a.w + (long long)(b_ok[i] ? n : 0) * K + ch * 8;
   }
 
-  const int kpr = CI / BK;          // k-tiles per (r, s) tap
-  const int KT = a.R * a.S * kpr;
+  const int kpr = CI / BK;          // k-tiles per tap
+  const int KT = nth * ntw * kpr;
   bf16x8 ra[A_PER], rb[B_PER];
   const bf16x8 zero = {};
 
   auto load = [&](int kt) {
-    const int rs = kt / kpr;
-    const int cb = (kt - rs * kpr) * BK + ch * 8;
-    const int r = rs / a.S, s = rs - r * a.S;
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      int ih, iw;
-      bool ok = a_ok[i];
-      if (!TRANS) {
-        ih = a_h[i] + r;
-        iw = a_w[i] + s;
-      } else {
-        const int th = a_h[i] - r, tw = a_w[i] - s;
-        ok = ok && th >= 0 && tw >= 0;
-        if (st == 1) { ih = th; iw = tw; }
-        else {
-          ok = ok && (th % st) == 0 && (tw % st) == 0;
-          ih = th / st;
-          iw = tw / st;
-        }
-      }
-      ok = ok && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
-      ra[i] = ok ? *reinterpret_cast<const bf16x8*>(
-                       a.x + ((long long)a_pix[i] + ih * GW + iw) * CI + cb)
-                 : zero;
+    const int t = kt / kpr;
+    const int cb = (kt - t * kpr) * BK;
+    int r, s, dh, dw;
+    if (MODE == 0) {
+      r = t / a.S; s = t - r * a.S; dh = r; dw = s;
+    } else {
+      const int ti = t / ntw, tj = t - ti * ntw;
+      r = r0h + ti * st; s = r0w + tj * st;
+      dh = (ph + a.pad - r) / st;        // exact: (ph + pad - r) is a multiple of st
+      dw = (pw + a.pad - s) / st;
     }
 #pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+      const int ih = a_h[i] + dh, iw = a_w[i] + dw;
+      const bool ok = a_ok[i] && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
+      ra[i] = ok ? *reinterpret_cast<const bf16x8*>(
+                       a.x + ((long long)a_pix[i] + ih * GW + iw) * CI + cb + ch * 8)
+                 : zero;
+    }
+    const long long woff = (long long)(r * a.S + s) * CI + cb;
+#pragma unroll
     for (int i = 0; i < B_PER; ++i)
-      rb[i] = b_ok[i] ? *reinterpret_cast<const bf16x8*>(b_row[i] + (long long)kt * BK) : zero;
+      rb[i] = b_ok[i] ? *reinterpret_cast<const bf16x8*>(b_row[i] + woff) : zero;
   };
 
   auto store = [&](int buf) {
@@ -177,18 +194,20 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
     }
   };
 
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) load(kt + 1);
-    compute(cur);
-    if (kt + 1 < KT) store(cur ^ 1);
+  if (KT > 0) {
+    load(0);
+    store(0);
     __syncthreads();
+    for (int kt = 0; kt < KT; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < KT) load(kt + 1);
+      compute(cur);
+      if (kt + 1 < KT) store(cur ^ 1);
+      __syncthreads();
+    }
   }
 
-  // epilogue: D^T layout -> lane owns channels n..n+3 of pixel m
+  // epilogue: D^T layout -> lane owns channels n..n+3 of output row m
   float s_sum[TN][4], s_sq[TN][4];
   if (STATS) {
 #pragma unroll
@@ -199,14 +218,23 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const long long m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+    long long pix = m;
+    if (MODE == 1) {
+      const long long mm = m < Mc ? m : 0;
+      const int j = (int)(mm % RW);
+      const long long t = mm / RW;
+      const int ii = (int)(t % RH);
+      const long long b = t / RH;
+      pix = (b * a.OH + (long long)ii * st + ph) * a.OW + (long long)j * st + pw;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
       bf16x4 o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o.v[r] = f2bf(acc[i][j][r]);
-      if (m < a.M && n < a.CO) {
-        *reinterpret_cast<bf16x4*>(a.y + m * a.CO + n) = o;
+      if (m < Mc && n < a.CO) {
+        *reinterpret_cast<bf16x4*>(a.y + pix * a.CO + n) = o;
         if (STATS) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -219,7 +247,6 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
     }
   }
   if (STATS) {
-    // reduce over the 16 pixels (lane & 15) that share a channel quad
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -230,8 +257,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
           s_sq[j][r] += __shfl_xor(s_sq[j][r], o, 64);
         }
       }
-    // then over the WM waves of the block (lds is free after the last barrier)
     float* red = reinterpret_cast<float*>(lds);   // [WM][BN] sums, then [WM][BN] squares
+    if (KT == 0) __syncthreads();
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -263,46 +290,52 @@ struct WgradArgs {
   float* dw;        // [CO][R][S][CI] fp32, accumulated
   int B, GH, GW, CI, OH, OW, CO, R, S, stride, pad;
   long long P;
-  int p_chunk;      // rows of P per block (multiple of BP)
+  int p_chunk;      // rows of P per block (multiple of 64)
 };
 
-// 32-B granule swizzle for the [p][64] bf16 images read with ds_read_b64_tr_b16:
-// a half-wave's transposed read touches rows {8g+q, g=0,1, q=0..3} (+4 for the
-// second read) at one 32-B granule; granule ^= f(row>>1) with
-// f(j) = (j&1) | ((j>>1)&2) puts those 8 rows in 8 distinct bank granules.
+// 32-B granule swizzle for [p][ROWE] bf16 images read by ds_read_b64_tr_b16.
+// A transposed read of one half-wave touches rows {8g+q : g=0,1, q=0..3} (and
+// +4 for the second read) in one granule.  Row strides of 128/384 B put rows of
+// equal parity on one bank offset -> f spreads rows {0,2,8,10} over 4 granules;
+// 256-B rows put every row on one offset -> f spreads all 8 rows.
+template <int ROWE>
 __device__ __forceinline__ int wg_off(int row, int col) {
-  const int j = row >> 1;
-  const int f = (j & 1) | ((j >> 1) & 2);
-  return row * 64 + ((((col >> 4) ^ f) & 3) << 4) + (col & 15);
+  int f;
+  if constexpr (ROWE == 128) f = (row & 3) | (((row >> 3) & 1) << 2);
+  else f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  return row * ROWE + ((((col >> 4) ^ f)) << 4) + (col & 15);
 }
 
-// D[co][k] += sum_p dY[p][co] * Xg[p][k]. Block tile BMW (co) x BNW (k) over a
-// chunk of P; both operands staged as swizzled [p][64] images.
-template <int BMW, int BNW, int BP, int WM, int WN>
-__global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(WgradArgs a) {
-  static_assert(BMW == 64 && BNW == 64, "wg_off swizzle assumes 64-wide images");
-  constexpr int NT = 64 * WM * WN;
-  constexpr int LDA = BMW;
-  constexpr int LDB = BNW;
-  constexpr int ACH = BMW / 8, BCH = BNW / 8;    // 16-B chunks per row
-  constexpr int A_PER = BP * ACH / NT;
-  constexpr int B_PER = BP * BCH / NT;
-  constexpr int TM = BMW / WM / 16, TN = BNW / WN / 16;
-  constexpr int STAGE = BP * (LDA + LDB);
-  static_assert(BP * ACH % NT == 0 && BP * BCH % NT == 0, "tile/thread mismatch");
+// Block: 4 waves side by side along k (WN=4), each 64 (co) x BNW/4 (k).
+template <int BNW>
+__global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
+  constexpr int BMW = 64, BP = 64, NT = 256;
+  constexpr int TM = 4, TN = BNW / 64;
+  constexpr int ACH = BMW / 8, BCH = BNW / 8;
+  constexpr int A_PER = BP * ACH / NT;          // 2
+  constexpr int B_PER = BP * BCH / NT;          // BNW/32
+  constexpr int STAGE = BP * (BMW + BNW);
   __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const int kx0 = blockIdx.x * BNW;            // column in K = (r, s, ci)
+  const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
+  const int kx0 = blockIdx.x * BNW;            // first column in K = (r, s, ci)
   const int co0 = blockIdx.y * BMW;
   const long long p_begin = (long long)blockIdx.z * a.p_chunk;
   const long long p_end = min(a.P, p_begin + a.p_chunk);
-  const int rs = kx0 / a.CI;
-  const int ci0 = kx0 - rs * a.CI;
-  const int r = rs / a.S, s = rs - (rs / a.S) * a.S;
   const int GH = a.GH, GW = a.GW, CI = a.CI;
 
+  // fixed per-thread load slots: (row, chunk) and, for X, the chunk's tap/channel
+  int b_r[B_PER], b_s[B_PER], b_ci[B_PER];
+#pragma unroll
+  for (int i = 0; i < B_PER; ++i) {
+    const int idx = tid + i * NT;
+    const int c = idx % BCH;
+    const int kc = kx0 + c * 8;
+    const int rs = kc / CI;
+    b_ci[i] = kc - rs * CI;
+    b_r[i] = rs / a.S;
+    b_s[i] = rs - b_r[i] * a.S;
+  }
   bf16x8 ra[A_PER], rb[B_PER];
   const bf16x8 zero = {};
   auto load = [&](long long pb) {
@@ -316,7 +349,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * NT;
-      const int row = idx / BCH, c = idx - row * BCH;
+      const int row = idx / BCH;
       const long long p = pb + row;
       bool ok = p < p_end;
       const long long pp = ok ? p : 0;
@@ -324,27 +357,27 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(WgradArgs a) {
       const long long t = pp / a.OW;
       const int oh = (int)(t % a.OH);
       const int b = (int)(t / a.OH);
-      const int ih = oh * a.stride - a.pad + r, iw = ow * a.stride - a.pad + s;
+      const int ih = oh * a.stride - a.pad + b_r[i], iw = ow * a.stride - a.pad + b_s[i];
       ok = ok && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
       rb[i] = ok ? *reinterpret_cast<const bf16x8*>(
-                       a.x + (((long long)b * GH + ih) * GW + iw) * CI + ci0 + c * 8)
+                       a.x + (((long long)b * GH + ih) * GW + iw) * CI + b_ci[i])
                  : zero;
     }
   };
   auto store = [&](int buf) {
     u16* As = lds + buf * STAGE;
-    u16* Bs = As + BP * LDA;
+    u16* Bs = As + BP * BMW;
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int idx = tid + i * NT;
       const int row = idx / ACH, c = idx - row * ACH;
-      *reinterpret_cast<bf16x8*>(As + wg_off(row, c * 8)) = ra[i];
+      *reinterpret_cast<bf16x8*>(As + wg_off<BMW>(row, c * 8)) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int idx = tid + i * NT;
       const int row = idx / BCH, c = idx - row * BCH;
-      *reinterpret_cast<bf16x8*>(Bs + wg_off(row, c * 8)) = rb[i];
+      *reinterpret_cast<bf16x8*>(Bs + wg_off<BNW>(row, c * 8)) = rb[i];
     }
   };
 
@@ -354,29 +387,35 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // transposed operand fetch: lane (g = lane>>4, i = lane&15) gets column
-  // col0 + i of rows pk + 8g .. 8g+7 as 8 consecutive k elements.
+  // lane (g = lane>>4, li = lane&15) receives column col0+li of rows
+  // pk+8g .. pk+8g+7 = 8 consecutive reduction elements (two tr reads).
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pc = li & 3;
-  auto tr8 = [&](const u16* base, int ld, int pk, int col0) -> bf16x8 {
-    (void)ld;
+  auto tr8A = [&](const u16* base, int pk, int col0) -> bf16x8 {
     const int row = pk + 8 * g + q;
     const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off(row, col0 + 4 * pc)));
+        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off<BMW>(row, col0 + 4 * pc)));
     const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off(row + 4, col0 + 4 * pc)));
-    const s16x8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, v);
+        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off<BMW>(row + 4, col0 + 4 * pc)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto tr8B = [&](const u16* base, int pk, int col0) -> bf16x8 {
+    const int row = pk + 8 * g + q;
+    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off<BNW>(row, col0 + 4 * pc)));
+    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off<BNW>(row + 4, col0 + 4 * pc)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
   auto compute = [&](int buf) {
     const u16* As = lds + buf * STAGE;
-    const u16* Bs = As + BP * LDA;
+    const u16* Bs = As + BP * BMW;
 #pragma unroll
     for (int pk = 0; pk < BP; pk += 32) {
       bf16x8 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = tr8(As, LDA, pk, wm * (BMW / WM) + i * 16);
+      for (int i = 0; i < TM; ++i) af[i] = tr8A(As, pk, i * 16);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = tr8(Bs, LDB, pk, wn * (BNW / WN) + j * 16);
+      for (int j = 0; j < TN; ++j) bf[j] = tr8B(Bs, pk, wn * (BNW / 4) + j * 16);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -396,16 +435,16 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_wgrad_kernel(WgradArgs a) {
     if (it + 1 < nsteps) store(cur ^ 1);
     __syncthreads();
   }
-  // D layout: lane holds rows co = 4*(lane>>4)+r, column k = lane & 15
+  // D layout: lane holds rows co = 4*(lane>>4)+r of column k = lane & 15
   const long long K = (long long)a.R * a.S * a.CI;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int kk = kx0 + wn * (BNW / WN) + j * 16 + (lane & 15);
+      const int kk = kx0 + wn * (BNW / 4) + j * 16 + (lane & 15);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int co = co0 + wm * (BMW / WM) + i * 16 + 4 * (lane >> 4) + rr;
+        const int co = co0 + i * 16 + 4 * (lane >> 4) + rr;
         atomicAdd(a.dw + (long long)co * K + kk, acc[i][j][rr]);
       }
     }
@@ -426,61 +465,110 @@ __global__ void __launch_bounds__(256) conv_weight_transpose_kernel(
 }
 
 // ---------------------------------------------------------------- launchers
-template <int BM, int BN, int BK, int WM, int WN, bool TRANS>
-static void launch_igemm(const ConvArgs& a, bool stats, hipStream_t s) {
-  const dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)((a.CO + BN - 1) / BN));
-  const dim3 block(64 * WM * WN);
-  if (stats)
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, TRANS, true>), grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, TRANS, false>), grid, block, 0, s, a);
+// Tile configurations (BM, BN, BK, WM, WN).  Index = the `cfg` id used by the
+// host-side tuner; -1 selects the heuristic default.
+#define DMP_CONV_CONFIGS(X)   \
+  X(0, 256, 64, 64, 4, 1)     \
+  X(1, 256, 64, 32, 4, 2)     \
+  X(2, 128, 64, 64, 2, 2)     \
+  X(3, 128, 64, 32, 2, 2)     \
+  X(4, 64, 64, 64, 2, 2)      \
+  X(5, 64, 64, 32, 2, 2)      \
+  X(6, 256, 128, 64, 2, 2)    \
+  X(7, 256, 128, 32, 4, 2)    \
+  X(8, 128, 128, 64, 2, 2)    \
+  X(9, 128, 128, 32, 2, 4)    \
+  X(10, 64, 128, 64, 1, 4)    \
+  X(11, 128, 64, 32, 4, 2)
+
+constexpr int kNumConvConfigs = 12;
+
+static int config_bm(int cfg) {
+  switch (cfg) {
+#define X(id, BM, BN, BK, WM, WN) case id: return BM;
+    DMP_CONV_CONFIGS(X)
+#undef X
+  }
+  return 128;
 }
 
-// Tile choice: the widest N tile that the output channels fill, then the
-// tallest M tile that still gives >= ~2 blocks per CU on 256 CUs.
-int conv_tile_m(long long M, int CO) {
-  const int bn = CO >= 128 ? 128 : 64;
-  const long long nb = (CO + bn - 1) / bn;
-  if ((M + 255) / 256 * nb >= 512) return 256;
-  if ((M + 127) / 128 * nb >= 256) return 128;
+static int config_bn(int cfg) {
+  switch (cfg) {
+#define X(id, BM, BN, BK, WM, WN) case id: return BN;
+    DMP_CONV_CONFIGS(X)
+#undef X
+  }
   return 64;
 }
 
-template <bool TRANS>
-static void dispatch_igemm(const ConvArgs& a, bool stats, hipStream_t s) {
-  const int bm = conv_tile_m(a.M, a.CO);
-  const bool bk64 = (a.CI % 64) == 0;
-  if (a.CO >= 128) {
-    if (bm == 256) { if (bk64) launch_igemm<256, 128, 64, 2, 2, TRANS>(a, stats, s); else launch_igemm<256, 128, 32, 2, 2, TRANS>(a, stats, s); }
-    else if (bm == 128) { if (bk64) launch_igemm<128, 128, 64, 2, 2, TRANS>(a, stats, s); else launch_igemm<128, 128, 32, 2, 2, TRANS>(a, stats, s); }
-    else { if (bk64) launch_igemm<64, 128, 64, 1, 4, TRANS>(a, stats, s); else launch_igemm<64, 128, 32, 1, 4, TRANS>(a, stats, s); }
-  } else {
-    if (bm == 256) { if (bk64) launch_igemm<256, 64, 64, 4, 1, TRANS>(a, stats, s); else launch_igemm<256, 64, 32, 4, 1, TRANS>(a, stats, s); }
-    else if (bm == 128) { if (bk64) launch_igemm<128, 64, 64, 2, 2, TRANS>(a, stats, s); else launch_igemm<128, 64, 32, 2, 2, TRANS>(a, stats, s); }
-    else { if (bk64) launch_igemm<64, 64, 64, 2, 2, TRANS>(a, stats, s); else launch_igemm<64, 64, 32, 2, 2, TRANS>(a, stats, s); }
+int conv_num_configs() { return kNumConvConfigs; }
+
+void conv_config_info(int cfg, int* info) {
+  switch (cfg) {
+#define X(id, BM, BN, BK, WM, WN) \
+  case id: info[0] = BM; info[1] = BN; info[2] = BK; info[3] = 64 * WM * WN; return;
+    DMP_CONV_CONFIGS(X)
+#undef X
+  }
+  info[0] = info[1] = info[2] = info[3] = 0;
+}
+
+// heuristic default: widest N tile the channels fill, tallest M tile that
+// still yields >= ~2 blocks per CU.
+int conv_default_config(long long M, int CO) {
+  if (CO >= 128) {
+    const long long nb = CO / 128;
+    if ((M + 255) / 256 * nb >= 512) return 7;
+    if ((M + 127) / 128 * nb >= 256) return 9;
+    return 10;
+  }
+  if ((M + 255) / 256 >= 512) return 1;
+  if ((M + 127) / 128 >= 256) return 11;
+  return 5;
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int MODE, bool STATS>
+static void launch_cfg(const ConvArgs& a, int classes, hipStream_t s) {
+  const dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)((a.CO + BN - 1) / BN),
+                  (unsigned)classes);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, MODE, STATS>), grid,
+                     dim3(64 * WM * WN), 0, s, a);
+}
+
+template <int MODE, bool STATS>
+static void dispatch(const ConvArgs& a, int cfg, int classes, hipStream_t s) {
+  switch (cfg) {
+#define X(id, BM, BN, BK, WM, WN) \
+  case id: launch_cfg<BM, BN, BK, WM, WN, MODE, STATS>(a, classes, s); return;
+    DMP_CONV_CONFIGS(X)
+#undef X
   }
 }
 
-int conv_fwd_num_mblocks(long long M, int CO) {
-  const int bm = conv_tile_m(M, CO);
+int conv_fwd_num_mblocks(long long M, int CO, int cfg) {
+  if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(M, CO);
+  const int bm = config_bm(cfg);
   return (int)((M + bm - 1) / bm);
 }
 
 void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int H, int W,
-                     int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
+                     int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                      hipStream_t s) {
   ConvArgs a{x, w, y, part, B, H, W, CI, OH, OW, CO, R, S, stride, pad,
              (long long)B * OH * OW};
-  dispatch_igemm<false>(a, part != nullptr, s);
+  if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(a.M, CO);
+  if (part) dispatch<0, true>(a, cfg, 1, s);
+  else dispatch<0, false>(a, cfg, 1, s);
 }
 
-// dX (B,H,W,CI) from dY (B,OH,OW,CO) and Wt [CI][R][S][CO]
+// dX (B,H,W,CI) from dY (B,OH,OW,CO) and Wt [CI][R][S][CO]; stride*stride parity classes.
 void launch_conv_dgrad(const u16* dy, const u16* wt, u16* dx, int B, int H, int W, int CI,
-                       int OH, int OW, int CO, int R, int S, int stride, int pad,
+                       int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s) {
-  ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad,
-             (long long)B * H * W};
-  dispatch_igemm<true>(a, false, s);
+  const long long rows = (long long)B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
+  ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad, rows};
+  if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(rows * stride * stride, CI);
+  dispatch<1, false>(a, cfg, stride * stride, s);
 }
 
 void launch_conv_weight_transpose(const u16* w, u16* wt, int CO, int RS, int CI, hipStream_t s) {
@@ -489,23 +577,31 @@ void launch_conv_weight_transpose(const u16* w, u16* wt, int CO, int RS, int CI,
                      w, wt, CO, RS, CI);
 }
 
+// cfg: low 2 bits select BNW (0 -> auto, 1 -> 64, 2 -> 128, 3 -> 192), the rest
+// the minimum rows of P per block (in units of 512; 0 -> auto).
 void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int W, int CI,
-                       int OH, int OW, int CO, int R, int S, int stride, int pad,
+                       int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s) {
-  constexpr int BMW = 64, BNW = 64, BP = 64;
   WgradArgs a{dy, x, dw, B, H, W, CI, OH, OW, CO, R, S, stride, pad, (long long)B * OH * OW, 0};
   const long long K = (long long)R * S * CI;
-  const long long tiles = (K / BNW) * (CO / BMW);
-  // enough P-splits for >= ~1024 blocks, but >= 1024 rows of P per block so the
-  // fp32 atomics stay a small fraction of the traffic
-  long long splits = (1024 + tiles - 1) / tiles;
+  int bnw = 64;
+  const int sel = cfg < 0 ? 0 : (cfg & 3);
+  if (sel == 0) bnw = (K % 192 == 0) ? 192 : (K % 128 == 0 ? 128 : 64);
+  else bnw = sel == 1 ? 64 : (sel == 2 ? 128 : 192);
+  if (K % bnw != 0) bnw = 64;
+  const long long tiles = (K / bnw) * (CO / 64);
+  long long min_chunk = cfg < 0 ? 0 : (long long)(cfg >> 2) * 512;
+  if (min_chunk <= 0) min_chunk = 2048;
+  long long splits = (768 + tiles - 1) / tiles;
   long long chunk = (a.P + splits - 1) / splits;
-  if (chunk < 1024) chunk = 1024;
-  chunk = (chunk + BP - 1) / BP * BP;
+  if (chunk < min_chunk) chunk = min_chunk;
+  chunk = (chunk + 63) / 64 * 64;
   splits = (a.P + chunk - 1) / chunk;
   a.p_chunk = (int)chunk;
-  const dim3 grid((unsigned)(K / BNW), (unsigned)(CO / BMW), (unsigned)splits);
-  hipLaunchKernelGGL((conv_wgrad_kernel<BMW, BNW, BP, 2, 2>), grid, dim3(256), 0, s, a);
+  const dim3 grid((unsigned)(K / bnw), (unsigned)(CO / 64), (unsigned)splits);
+  if (bnw == 192) hipLaunchKernelGGL((conv_wgrad_kernel<192>), grid, dim3(256), 0, s, a);
+  else if (bnw == 128) hipLaunchKernelGGL((conv_wgrad_kernel<128>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<64>), grid, dim3(256), 0, s, a);
 }
 
 }  // namespace dmp

@@ -53,17 +53,20 @@ void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, in
 
 namespace dmp {
 // conv.hip
-int conv_fwd_num_mblocks(long long M, int CO);
+int conv_num_configs();
+void conv_config_info(int cfg, int* info);
+int conv_default_config(long long M, int CO);
+int conv_fwd_num_mblocks(long long M, int CO, int cfg);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int B, int H,
                      int W, int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
-                     hipStream_t s);
+                     int cfg, hipStream_t s);
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int B, int H, int W,
-                       int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
+                       int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s);
 void launch_conv_weight_transpose(const uint16_t* w, uint16_t* wt, int CO, int RS, int CI,
                                   hipStream_t s);
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int B, int H, int W,
-                       int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
+                       int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s);
 }  // namespace dmp
 

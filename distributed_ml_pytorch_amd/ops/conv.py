@@ -7,7 +7,8 @@ arena's bf16 shadow (no per-step cast) and the weight gradient is accumulated
 in fp32 straight into the arena grad view (no AccumulateGrad, no cast
 kernels).  When the conv feeds a BatchNorm (``emit_bn_stats``) its epilogue
 also emits per-block channel sums, so the BN forward skips its statistics
-pass over the activation.
+pass over the activation.  Tile configurations are chosen per shape by
+timing them on first use (:mod:`.tuner`).
 
 Everything else goes to ``F.conv2d`` (MIOpen) in channels_last.
 """
@@ -18,8 +19,10 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from ._ext import native
+from .tuner import TUNER
 
 _NATIVE_ENABLED = True
+_CONFIGS = None
 
 
 def set_native_conv(enabled: bool):
@@ -31,10 +34,55 @@ def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
 
 
+def _configs():
+    global _CONFIGS
+    if _CONFIGS is None:
+        _CONFIGS = [tuple(c) for c in native().conv_configs()]   # (id, BM, BN, BK, threads)
+    return _CONFIGS
+
+
+def _igemm_candidates(out_channels: int):
+    return [c[0] for c in _configs() if c[2] <= max(64, out_channels)]
+
+
+def _wgrad_candidates(K: int):
+    cands = []
+    for sel, bnw in ((1, 64), (2, 128), (3, 192)):
+        if K % bnw:
+            continue
+        for chunk in (2, 4, 8):          # x512 rows of P per block
+            cands.append(sel | (chunk << 2))
+    return cands
+
+
+def _fwd_cfg(x, w16, stride, pad):
+    key = ("fwd", *x.shape, w16.shape[0], w16.shape[2], w16.shape[3], stride, pad)
+    return TUNER.best(key, lambda c: native().conv_fwd(x, w16, stride, pad, True, c),
+                      _igemm_candidates(w16.shape[0]))
+
+
+def _dgrad_cfg(dy, w16, H, W, stride, pad):
+    key = ("dgrad", *dy.shape, w16.shape[1], H, W, w16.shape[2], w16.shape[3], stride, pad)
+    return TUNER.best(key, lambda c: native().conv_dgrad(dy, w16, H, W, stride, pad, c),
+                      _igemm_candidates(w16.shape[1]))
+
+
+def _wgrad_cfg(dy, x, shape, stride, pad):
+    key = ("wgrad", *x.shape, *shape, stride, pad)
+    if key in TUNER.cache or not TUNER.enabled:
+        return TUNER.cache.get(key, -1)
+    scratch = torch.zeros(shape, dtype=torch.float32, device=x.device,
+                          memory_format=torch.channels_last)
+    K = shape[1] * shape[2] * shape[3]
+    return TUNER.best(key, lambda c: native().conv_wgrad(dy, x, scratch, stride, pad, c),
+                      _wgrad_candidates(K))
+
+
 class _NativeConv(Function):
     @staticmethod
     def forward(ctx, x, w16, master, stride, pad, want_stats):
-        y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats)
+        cfg = _fwd_cfg(x, w16, stride, pad)
+        y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats, cfg)
         ctx.save_for_backward(x, w16)
         ctx.master = master
         ctx.geom = (x.shape[2], x.shape[3], stride, pad)
@@ -47,22 +95,25 @@ class _NativeConv(Function):
     def backward(ctx, dy, _dpart):
         x, w16 = ctx.saved_tensors
         H, W, stride, pad = ctx.geom
+        dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = native().conv_dgrad(dy, w16, H, W, stride, pad)
+            cfg = _dgrad_cfg(dy, w16, H, W, stride, pad)
+            dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg)
         master = ctx.master
         gw = None
         if master is not None and master.requires_grad:
+            wcfg = _wgrad_cfg(dy, x, tuple(master.shape), stride, pad)
             g = master.grad if getattr(master, "_dmp_arena", False) else None
             if g is not None and g.is_contiguous(memory_format=torch.channels_last):
-                native().conv_wgrad(dy, x, g, stride, pad)
+                native().conv_wgrad(dy, x, g, stride, pad, wcfg)
                 cb = getattr(master, "_dmp_grad_ready", None)
                 if cb is not None:
                     cb(master)
             else:
-                gw = torch.zeros(master.shape, dtype=torch.float32, device=x.device,
-                                 memory_format=torch.channels_last)
-                native().conv_wgrad(dy, x, gw, stride, pad)
+                gw = torch.zeros(tuple(master.shape), dtype=torch.float32, device=x.device)
+                gw = gw.contiguous(memory_format=torch.channels_last)
+                native().conv_wgrad(dy, x, gw, stride, pad, wcfg)
                 gw = gw.to(master.dtype)
         return dx, None, gw, None, None, None
 
@@ -80,7 +131,7 @@ def native_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
 
 
 def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=False):
-    """Returns ``y`` (and attaches BN partials to it when ``want_stats``)."""
+    """Returns ``y`` (with BN partials attached as ``y._dmp_bn_part`` when ``want_stats``)."""
     if x.is_cuda and x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
         if master is not None and b is None and native_conv_supported(

@@ -1,0 +1,80 @@
+"""Per-shape kernel selection by measurement ("measure, don't guess").
+
+The conv kernels are compiled for several tile configurations
+(``_native.conv_configs()``).  The first time a (pass, shape) is seen, every
+eligible configuration is timed with HIP events on the current stream and the
+fastest is cached for the process.  Tuning never runs while a stream is being
+captured into a graph (the heuristic default is used then) and can be
+disabled with ``DMP_CONV_TUNE=0``.  ``DMP_CONV_TUNE_CACHE=path.json`` persists
+choices across processes.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+
+import torch
+
+_lock = threading.Lock()
+
+
+class KernelTuner:
+    def __init__(self):
+        self.cache: dict[tuple, int] = {}
+        self.timings: dict[tuple, dict] = {}
+        self.enabled = os.environ.get("DMP_CONV_TUNE", "1") != "0"
+        self.path = os.environ.get("DMP_CONV_TUNE_CACHE")
+        self.reps = int(os.environ.get("DMP_CONV_TUNE_REPS", "3"))
+        if self.path and os.path.exists(self.path):
+            try:
+                with open(self.path) as f:
+                    for k, v in json.load(f).items():
+                        self.cache[tuple(json.loads(k))] = int(v)
+            except (OSError, ValueError):
+                pass
+
+    def best(self, key: tuple, runner, candidates) -> int:
+        got = self.cache.get(key)
+        if got is not None:
+            return got
+        if not self.enabled or not candidates or torch.cuda.is_current_stream_capturing():
+            return -1
+        with _lock:
+            if key in self.cache:
+                return self.cache[key]
+            times = {}
+            for c in candidates:
+                runner(c)                       # first touch / warm caches
+                a = torch.cuda.Event(enable_timing=True)
+                b = torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(self.reps):
+                    runner(c)
+                b.record()
+                b.synchronize()
+                times[c] = a.elapsed_time(b) / self.reps
+            best = min(times, key=times.get)
+            self.cache[key] = best
+            self.timings[key] = times
+            if self.path:
+                self._save()
+            return best
+
+    def _save(self):
+        try:
+            with open(self.path, "w") as f:
+                json.dump({json.dumps(list(k)): v for k, v in self.cache.items()}, f)
+        except OSError:
+            pass
+
+    def report(self) -> list[dict]:
+        out = []
+        for k, times in self.timings.items():
+            best = self.cache[k]
+            out.append({"key": list(k), "best": best, "best_ms": times[best],
+                        "worst_ms": max(times.values())})
+        return out
+
+
+TUNER = KernelTuner()

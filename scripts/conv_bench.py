@@ -59,17 +59,21 @@ def main():
         flops = 2.0 * B * OH * OH * CO * CI * k * k
         dy = torch.randn(B, CO, OH, OH, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
         dw = torch.zeros(CO, CI, k, k, device="cuda").contiguous(memory_format=CL)
-        tn_f = timeit(lambda: nat.conv_fwd(x, w, st, pd, True), a.iters)
+        from distributed_ml_pytorch_amd.ops import conv as C
+        cf = C._fwd_cfg(x, w, st, pd)
+        cd = C._dgrad_cfg(dy, w, H, W, st, pd)
+        cw = C._wgrad_cfg(dy, x, tuple(w.shape), st, pd)
+        tn_f = timeit(lambda: nat.conv_fwd(x, w, st, pd, True, cf), a.iters)
         tm_f = timeit(lambda: F.conv2d(x, w, None, st, pd), a.iters)
-        tn_d = timeit(lambda: nat.conv_dgrad(dy, w, H, W, st, pd), a.iters)
-        tn_w = timeit(lambda: nat.conv_wgrad(dy, x, dw, st, pd), a.iters)
+        tn_d = timeit(lambda: nat.conv_dgrad(dy, w, H, W, st, pd, cd), a.iters)
+        tn_w = timeit(lambda: nat.conv_wgrad(dy, x, dw, st, pd, cw), a.iters)
 
         def mi_bwd(mask):
             return torch.ops.aten.convolution_backward(dy, x, w, None, [st, st], [pd, pd], [1, 1],
                                                        False, [0, 0], 1, mask)
         tm_d = timeit(lambda: mi_bwd([True, False, False]), a.iters)
         tm_w = timeit(lambda: mi_bwd([False, True, False]), a.iters)
-        name = f"B{B} {CI}->{CO} {H}x{W} k{k} s{st}"
+        name = f"B{B} {CI}->{CO} {H}x{W} k{k} s{st} [{cf},{cd},{cw}]"
         for p, tn, tm in (("fwd", tn_f, tm_f), ("dgrad", tn_d, tm_d), ("wgrad", tn_w, tm_w)):
             print(f"{name:44s} {p:6s} {tn:10.4f} {tm:10.4f} {flops / tn / 1e9:9.1f} {flops / tm / 1e9:9.1f}")
             tot_n += tn

@@ -59,6 +59,37 @@ def test_conv_fwd_dgrad_wgrad(B, CI, H, W, CO, k, st, pd):
     assert _rel(dw, 2 * wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 9, 11, 128, 3, 2, 1), (2, 128, 8, 8, 64, 1, 1, 0)])
+def test_every_tile_config(shape):
+    """The tuner may pick any compiled tile: each must be exact on odd shapes."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    B, CI, H, W, CO, k, st, pd = shape
+    x = torch.randn(B, CI, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(CO, CI, k, k, device="cuda") * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr = F.conv2d(x.float(), w.float(), None, st, pd)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    F.conv2d(xr, wr, None, st, pd).backward(dy.float())
+    for cfg in [c[0] for c in nat.conv_configs()]:
+        y, part, G = nat.conv_fwd(x, w, st, pd, True, cfg)
+        assert _rel(y, yr) < 1e-2, cfg
+        ps = part.view(2, int(G), CO).sum(1)
+        torch.testing.assert_close(ps[0], y.float().sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+        dx = nat.conv_dgrad(dy, w, H, W, st, pd, cfg)
+        assert _rel(dx, xr.grad) < 1e-2, cfg
+    K = CI * k * k
+    for sel in (1, 2, 3):
+        if K % (64 * sel):
+            continue
+        for chunk in (2, 8):
+            dw = torch.zeros(CO, CI, k, k, device="cuda").contiguous(memory_format=CL)
+            nat.conv_wgrad(dy, x, dw, st, pd, sel | (chunk << 2))
+            assert _rel(dw, wr.grad) < 1e-2, (sel, chunk)
+
+
 def test_conv_layer_autograd_and_bn_fusion():
     """Conv2d(native) -> BatchNorm2d(partials) matches the stock fp32 chain."""
     from distributed_ml_pytorch_amd.ops import layers as L
