@@ -293,7 +293,9 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t K) {
   TORCH_CHECK(dy.size(2) == H / K && dy.size(3) == W / K, "maxpool_bwd: shape mismatch");
   Tensor dx = (H % K == 0 && W % K == 0)
                   ? at::empty({N, C, H, W}, dy.options().memory_format(mf))
-                  : at::zeros({N, C, H, W}, dy.options().memory_format(mf));
+                  // (at::zeros ignores the memory format of its options: allocate
+                  //  channels_last explicitly, then clear the un-pooled border)
+                  : at::empty({N, C, H, W}, dy.options().memory_format(mf)).zero_();
   dmp::launch_maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
                           reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)H, (int)W, C, (int)K,
                           cur_stream());

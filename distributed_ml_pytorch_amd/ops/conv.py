@@ -71,8 +71,8 @@ def _wgrad_cfg(dy, x, shape, stride, pad):
     key = ("wgrad", *x.shape, *shape, stride, pad)
     if key in TUNER.cache or not TUNER.enabled:
         return TUNER.cache.get(key, -1)
-    scratch = torch.zeros(shape, dtype=torch.float32, device=x.device,
-                          memory_format=torch.channels_last)
+    scratch = torch.empty(shape, dtype=torch.float32, device=x.device,
+                          memory_format=torch.channels_last).zero_()
     K = shape[1] * shape[2] * shape[3]
     return TUNER.best(key, lambda c: native().conv_wgrad(dy, x, scratch, stride, pad, c),
                       _wgrad_candidates(K))
