@@ -16,12 +16,19 @@
 //           One block covers up to 3 taps (192 k-columns) so dY is re-read
 //           K/192 times, not once per tap.
 //
-// LDS staging uses XOR swizzles that keep the operand reads bank-conflict free
-// (derivations at swz() / wg_off()).  fwd/dgrad compute D^T = W * X^T so a lane
-// owns 4 consecutive output channels of one pixel (8-byte NHWC stores) and the
-// fwd epilogue can reduce per-channel BatchNorm partial sums (no extra pass).
-// Several tile configurations are compiled; the host side times them per
-// shape on first use (ops/tuner.py) and keeps the fastest.
+// Staging: every operand tile is fetched with global_load_lds_dwordx4 (LDS DMA,
+// 16 B per lane, no VGPR round trip).  The LDS image is lane-linear, so the
+// bank-conflict swizzle is applied on the per-lane SOURCE address (the read side
+// applies the same involution), and gather lanes whose tap falls in the zero
+// padding fetch from a zeroed 16-B page instead of branching.  This keeps the
+// VALU work per MFMA low: the first register-staged version of these kernels
+// measured ~10 VALU instructions per MFMA (SQ_INSTS_VALU / SQ_INSTS_MFMA) and
+// was issue-bound.
+//
+// fwd/dgrad compute D^T = W * X^T so a lane owns 4 consecutive output channels of
+// one pixel (8-byte NHWC stores) and the fwd epilogue can reduce per-channel
+// BatchNorm partial sums (no extra pass over Y).  Several tile configurations are
+// compiled; the host side times them per shape on first use (ops/tuner.py).
 #include "common.h"
 
 namespace dmp {
@@ -29,6 +36,9 @@ namespace dmp {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));
+
+// 16 zero bytes per lane-chunk: the source of every padded / out-of-range fetch.
+__device__ __attribute__((aligned(256))) u16 g_conv_zero[128];
 
 struct ConvArgs {
   const u16* x;     // gathered operand NHWC [B][GH][GW][CI]   (fwd: X, dgrad: dY)
@@ -44,11 +54,17 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
-// 16-byte chunk swizzle for a row-major [rows][BK] bf16 LDS tile.
+__device__ __forceinline__ void glds16(const u16* src, u16* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base,
+                                   16, 0, 0);
+}
+
+// 16-byte chunk swizzle (an involution) for a row-major [rows][BK] bf16 tile.
 //  BK=64 (128-B rows, 2 rows per 256-B bank row): chunk ^= (row>>1)&7
 //  BK=32 ( 64-B rows, 4 rows per bank row):       chunk ^= (-(row>>2))&3
 // Both make each ds_read_b128 lane group (rows l&15, chunk c + (l>>4)) hit 16
-// distinct 16-B slots.
+// distinct 16-B slots.  Rows r and r+16 share the same XOR, so fragment rows
+// 16 apart differ by a constant offset (folded into ds_read immediates).
 template <int BK>
 __device__ __forceinline__ int swz(int row, int c) {
   if constexpr (BK == 64) return c ^ ((row >> 1) & 7);
@@ -58,22 +74,24 @@ __device__ __forceinline__ int swz(int row, int c) {
 // MODE 0: forward conv.  MODE 1: data gradient, one parity class per blockIdx.z.
 template <int BM, int BN, int BK, int WM, int WN, int MODE, bool STATS>
 __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
-  constexpr int NT = 64 * WM * WN;
-  constexpr int CPR = BK / 8;
-  constexpr int ROWSTEP = NT / CPR;
-  constexpr int A_PER = BM / ROWSTEP;
-  constexpr int B_PER = (BN + ROWSTEP - 1) / ROWSTEP;
+  constexpr int NW = WM * WN;
+  constexpr int CPR = BK / 8;                 // 16-B chunks per tile row
+  constexpr int RPI = 64 / CPR;               // tile rows per glds wave-instruction (1 KiB)
+  constexpr int A_INS = BM / RPI;
+  constexpr int B_INS = (BN + RPI - 1) / RPI;
+  constexpr int A_PW = (A_INS + NW - 1) / NW;
+  constexpr int B_PW = (B_INS + NW - 1) / NW;
   constexpr int TM = BM / WM / 16;
   constexpr int TN = BN / WN / 16;
-  constexpr int STAGE = (BM + BN) * BK;
-  static_assert(BM % ROWSTEP == 0, "A tile must split evenly over threads");
+  constexpr int A_EL = BM * BK, B_EL = B_INS * RPI * BK;
+  constexpr int STAGE = A_EL + B_EL;
   __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const long long m0 = (long long)blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
-  const int ch = tid % CPR, r0 = tid / CPR;
   const int GH = a.GH, GW = a.GW, CI = a.CI, st = a.stride;
 
   // class geometry (MODE 1) -------------------------------------------------
@@ -92,38 +110,41 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
     if (m0 >= Mc) return;
   }
 
-  int a_pix[A_PER], a_h[A_PER], a_w[A_PER];
-  bool a_ok[A_PER];
+  // per-lane gather state for the A tile: lane's row in each glds instruction
+  int a_pix[A_PW], a_h[A_PW], a_w[A_PW], a_c[A_PW];
+  bool a_ok[A_PW];
 #pragma unroll
-  for (int i = 0; i < A_PER; ++i) {
-    const long long m = m0 + r0 + i * ROWSTEP;
-    a_ok[i] = m < Mc;
-    const long long mm = a_ok[i] ? m : 0;
+  for (int j = 0; j < A_PW; ++j) {
+    const int ins = wid + j * NW;
+    const int row = ins * RPI + lane / CPR;
+    a_c[j] = swz<BK>(row, lane % CPR) * 8;      // logical chunk this lane fetches
+    const long long m = m0 + row;
+    a_ok[j] = ins < A_INS && m < Mc;
+    const long long mm = a_ok[j] ? m : 0;
     const int ow = (int)(mm % RW);
     const long long t = mm / RW;
     const int oh = (int)(t % RH);
     const int b = (int)(t / RH);
-    a_pix[i] = b * GH * GW;
-    if (MODE == 0) { a_h[i] = oh * st - a.pad; a_w[i] = ow * st - a.pad; }
-    else           { a_h[i] = oh;              a_w[i] = ow; }
+    a_pix[j] = b * GH * GW;
+    if (MODE == 0) { a_h[j] = oh * st - a.pad; a_w[j] = ow * st - a.pad; }
+    else           { a_h[j] = oh;              a_w[j] = ow; }
   }
   const long long K = (long long)a.R * a.S * CI;
-  const u16* b_row[B_PER];
-  bool b_ok[B_PER];
+  const u16* b_src[B_PW];
+  bool b_ok[B_PW];
 #pragma unroll
-  for (int i = 0; i < B_PER; ++i) {
-    const int row = r0 + i * ROWSTEP;
+  for (int j = 0; j < B_PW; ++j) {
+    const int ins = wid + j * NW;
+    const int row = ins * RPI + lane / CPR;
     const int n = n0 + row;
-    b_ok[i] = row < BN && n < a.CO;
-    b_row[i] = a.w + (long long)(b_ok[i] ? n : 0) * K + ch * 8;
+    b_ok[j] = ins < B_INS && row < BN && n < a.CO;
+    b_src[j] = a.w + (long long)(b_ok[j] ? n : 0) * K + swz<BK>(row, lane % CPR) * 8;
   }
 
   const int kpr = CI / BK;          // k-tiles per tap
   const int KT = nth * ntw * kpr;
-  bf16x8 ra[A_PER], rb[B_PER];
-  const bf16x8 zero = {};
 
-  auto load = [&](int kt) {
+  auto stage = [&](int buf, int kt) {
     const int t = kt / kpr;
     const int cb = (kt - t * kpr) * BK;
     int r, s, dh, dw;
@@ -135,32 +156,27 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
       dh = (ph + a.pad - r) / st;        // exact: (ph + pad - r) is a multiple of st
       dw = (pw + a.pad - s) / st;
     }
+    u16* As = lds + buf * STAGE;
+    u16* Bs = As + A_EL;
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int ih = a_h[i] + dh, iw = a_w[i] + dw;
-      const bool ok = a_ok[i] && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
-      ra[i] = ok ? *reinterpret_cast<const bf16x8*>(
-                       a.x + ((long long)a_pix[i] + ih * GW + iw) * CI + cb + ch * 8)
-                 : zero;
+    for (int j = 0; j < A_PW; ++j) {
+      const int ins = wid + j * NW;
+      if (A_INS % NW == 0 || ins < A_INS) {
+        const int ih = a_h[j] + dh, iw = a_w[j] + dw;
+        const bool ok = a_ok[j] && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
+        const u16* src = ok ? a.x + ((long long)a_pix[j] + ih * GW + iw) * CI + cb + a_c[j]
+                            : g_conv_zero;
+        glds16(src, As + ins * (RPI * BK));
+      }
     }
     const long long woff = (long long)(r * a.S + s) * CI + cb;
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i)
-      rb[i] = b_ok[i] ? *reinterpret_cast<const bf16x8*>(b_row[i] + woff) : zero;
-  };
-
-  auto store = [&](int buf) {
-    u16* As = lds + buf * STAGE;
-    u16* Bs = As + BM * BK;
-#pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int row = r0 + i * ROWSTEP;
-      *reinterpret_cast<bf16x8*>(As + row * BK + swz<BK>(row, ch) * 8) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int row = r0 + i * ROWSTEP;
-      if (row < BN) *reinterpret_cast<bf16x8*>(Bs + row * BK + swz<BK>(row, ch) * 8) = rb[i];
+    for (int j = 0; j < B_PW; ++j) {
+      const int ins = wid + j * NW;
+      if (B_INS % NW == 0 || ins < B_INS) {
+        const u16* src = b_ok[j] ? b_src[j] + woff : g_conv_zero;
+        glds16(src, Bs + ins * (RPI * BK));
+      }
     }
   };
 
@@ -170,23 +186,29 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
-    const u16* As = lds + buf * STAGE;
-    const u16* Bs = As + BM * BK;
+  // fragment offsets (elements) for k-step 0/1; rows 16 apart add 16*BK
+  int offA[BK / 32], offB[BK / 32];
+  {
+    const int ra = wm * (BM / WM) + (lane & 15);
+    const int rb = wn * (BN / WN) + (lane & 15);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       const int c = ks * 4 + (lane >> 4);
+      offA[ks] = ra * BK + swz<BK>(ra, c) * 8;
+      offB[ks] = A_EL + rb * BK + swz<BK>(rb, c) * 8;
+    }
+  }
+  auto compute = [&](int buf) {
+    const u16* base = lds + buf * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 af[TM], bw[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / WM) + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(As + row * BK + swz<BK>(row, c) * 8);
-      }
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(base + offA[ks] + i * 16 * BK);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * (BN / WN) + j * 16 + (lane & 15);
-        bw[j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + swz<BK>(row, c) * 8);
-      }
+      for (int j = 0; j < TN; ++j)
+        bw[j] = *reinterpret_cast<const bf16x8*>(base + offB[ks] + j * 16 * BK);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -195,14 +217,12 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   };
 
   if (KT > 0) {
-    load(0);
-    store(0);
-    __syncthreads();
+    stage(0, 0);
+    __syncthreads();   // waits vmcnt(0): the DMA has landed
     for (int kt = 0; kt < KT; ++kt) {
       const int cur = kt & 1;
-      if (kt + 1 < KT) load(kt + 1);
+      if (kt + 1 < KT) stage(cur ^ 1, kt + 1);
       compute(cur);
-      if (kt + 1 < KT) store(cur ^ 1);
       __syncthreads();
     }
   }
@@ -270,7 +290,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
         }
     }
     __syncthreads();
-    for (int nl = tid; nl < BN; nl += NT) {
+    for (int nl = tid; nl < BN; nl += 64 * NW) {
       const int n = n0 + nl;
       if (n < a.CO) {
         float ss = 0.f, qq = 0.f;
@@ -293,91 +313,102 @@ struct WgradArgs {
   int p_chunk;      // rows of P per block (multiple of 64)
 };
 
-// 32-B granule swizzle for [p][ROWE] bf16 images read by ds_read_b64_tr_b16.
-// A transposed read of one half-wave touches rows {8g+q : g=0,1, q=0..3} (and
-// +4 for the second read) in one granule.  Row strides of 128/384 B put rows of
-// equal parity on one bank offset -> f spreads rows {0,2,8,10} over 4 granules;
-// 256-B rows put every row on one offset -> f spreads all 8 rows.
+// 32-B granule swizzle (an involution) for [p][ROWE] bf16 images read by
+// ds_read_b64_tr_b16.  A transposed read of one half-wave touches rows
+// {8g+q : g=0,1, q=0..3} (and +4 for the second read) in one granule.  Row
+// strides of 128/384 B put rows of equal parity on one bank offset -> f spreads
+// rows {0,2,8,10} over 4 granules; 256-B rows put every row on one offset -> f
+// spreads all 8 rows.
+template <int ROWE>
+__device__ __forceinline__ int wg_f(int row) {
+  if constexpr (ROWE == 128) return (row & 3) | (((row >> 3) & 1) << 2);
+  else return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+}
 template <int ROWE>
 __device__ __forceinline__ int wg_off(int row, int col) {
-  int f;
-  if constexpr (ROWE == 128) f = (row & 3) | (((row >> 3) & 1) << 2);
-  else f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
-  return row * ROWE + ((((col >> 4) ^ f)) << 4) + (col & 15);
+  return row * ROWE + ((((col >> 4) ^ wg_f<ROWE>(row))) << 4) + (col & 15);
 }
 
 // Block: 4 waves side by side along k (WN=4), each 64 (co) x BNW/4 (k).
 template <int BNW>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
-  constexpr int BMW = 64, BP = 64, NT = 256;
+  constexpr int BMW = 64, BP = 64, NW = 4;
   constexpr int TM = 4, TN = BNW / 64;
-  constexpr int ACH = BMW / 8, BCH = BNW / 8;
-  constexpr int A_PER = BP * ACH / NT;          // 2
-  constexpr int B_PER = BP * BCH / NT;          // BNW/32
-  constexpr int STAGE = BP * (BMW + BNW);
-  __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE];
+  constexpr int A_EL = BP * BMW, B_EL = BP * BNW;
+  constexpr int A_INS = A_EL / 512, B_INS = B_EL / 512;     // 1 KiB per glds instruction
+  constexpr int A_PW = A_INS / NW, B_PW = B_INS / NW;
+  constexpr int STAGE = A_EL + B_EL;
+  static_assert(A_INS % NW == 0 && B_INS % NW == 0, "instruction split");
+  // [2][STAGE] staging, then the [2][BP] row table (int4 per row)
+  __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE + 2 * BP * 8];
+  int4* rowtab = reinterpret_cast<int4*>(lds + 2 * STAGE);
 
-  const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wn = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kx0 = blockIdx.x * BNW;            // first column in K = (r, s, ci)
   const int co0 = blockIdx.y * BMW;
   const long long p_begin = (long long)blockIdx.z * a.p_chunk;
   const long long p_end = min(a.P, p_begin + a.p_chunk);
   const int GH = a.GH, GW = a.GW, CI = a.CI;
+  const int nsteps = (int)((p_end - p_begin + BP - 1) / BP);
+  if (nsteps <= 0) return;
 
-  // fixed per-thread load slots: (row, chunk) and, for X, the chunk's tap/channel
-  int b_r[B_PER], b_s[B_PER], b_ci[B_PER];
+  // per-lane DMA slots (fixed across stages): A = dY rows, B = X rows x tap columns
+  int a_row[A_PW], a_col[A_PW];
 #pragma unroll
-  for (int i = 0; i < B_PER; ++i) {
-    const int idx = tid + i * NT;
-    const int c = idx % BCH;
-    const int kc = kx0 + c * 8;
-    const int rs = kc / CI;
-    b_ci[i] = kc - rs * CI;
-    b_r[i] = rs / a.S;
-    b_s[i] = rs - b_r[i] * a.S;
+  for (int j = 0; j < A_PW; ++j) {
+    const int e = (wn + j * NW) * 512 + lane * 8;        // element index in the A image
+    const int row = e / BMW, pch = (e % BMW) / 8;
+    const int u = (pch >> 1) ^ wg_f<BMW>(row);
+    a_row[j] = row;
+    a_col[j] = co0 + u * 16 + (pch & 1) * 8;
   }
-  bf16x8 ra[A_PER], rb[B_PER];
-  const bf16x8 zero = {};
-  auto load = [&](long long pb) {
+  int b_row[B_PW], b_r[B_PW], b_s[B_PW], b_ci[B_PW];
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int idx = tid + i * NT;
-      const int row = idx / ACH, c = idx - row * ACH;
-      const long long p = pb + row;
-      ra[i] = (p < p_end) ? *reinterpret_cast<const bf16x8*>(a.dy + p * a.CO + co0 + c * 8) : zero;
-    }
-#pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int idx = tid + i * NT;
-      const int row = idx / BCH;
-      const long long p = pb + row;
-      bool ok = p < p_end;
-      const long long pp = ok ? p : 0;
-      const int ow = (int)(pp % a.OW);
-      const long long t = pp / a.OW;
-      const int oh = (int)(t % a.OH);
-      const int b = (int)(t / a.OH);
-      const int ih = oh * a.stride - a.pad + b_r[i], iw = ow * a.stride - a.pad + b_s[i];
-      ok = ok && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
-      rb[i] = ok ? *reinterpret_cast<const bf16x8*>(
-                       a.x + (((long long)b * GH + ih) * GW + iw) * CI + b_ci[i])
-                 : zero;
+  for (int j = 0; j < B_PW; ++j) {
+    const int e = (wn + j * NW) * 512 + lane * 8;
+    const int row = e / BNW, pch = (e % BNW) / 8;
+    const int u = (pch >> 1) ^ wg_f<BNW>(row);
+    const int kc = kx0 + u * 16 + (pch & 1) * 8;
+    const int rs = kc / CI;
+    b_row[j] = row;
+    b_ci[j] = kc - rs * CI;
+    b_r[j] = rs / a.S;
+    b_s[j] = rs - b_r[j] * a.S;
+  }
+  // row table for stage `st`: {pixel base, oh*stride-pad, ow*stride-pad, valid}
+  auto fill_rows = [&](int tab, int stg) {
+    if (tid < BP) {
+      const long long p = p_begin + (long long)stg * BP + tid;
+      int4 e = make_int4(0, -(1 << 20), -(1 << 20), 0);
+      if (stg < nsteps && p < p_end) {
+        const int ow = (int)(p % a.OW);
+        const long long t = p / a.OW;
+        const int oh = (int)(t % a.OH);
+        const int b = (int)(t / a.OH);
+        e = make_int4(b * GH * GW, oh * a.stride - a.pad, ow * a.stride - a.pad, 1);
+      }
+      rowtab[tab * BP + tid] = e;
     }
   };
-  auto store = [&](int buf) {
+  auto stage = [&](int buf, int stg) {
+    const long long pb = p_begin + (long long)stg * BP;
     u16* As = lds + buf * STAGE;
-    u16* Bs = As + BP * BMW;
+    u16* Bs = As + A_EL;
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-      const int idx = tid + i * NT;
-      const int row = idx / ACH, c = idx - row * ACH;
-      *reinterpret_cast<bf16x8*>(As + wg_off<BMW>(row, c * 8)) = ra[i];
+    for (int j = 0; j < A_PW; ++j) {
+      const long long p = pb + a_row[j];
+      const u16* src = p < p_end ? a.dy + p * a.CO + a_col[j] : g_conv_zero;
+      glds16(src, As + (wn + j * NW) * 512);
     }
+    const int4* tb = rowtab + (stg & 1) * BP;
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-      const int idx = tid + i * NT;
-      const int row = idx / BCH, c = idx - row * BCH;
-      *reinterpret_cast<bf16x8*>(Bs + wg_off<BNW>(row, c * 8)) = rb[i];
+    for (int j = 0; j < B_PW; ++j) {
+      const int4 e = tb[b_row[j]];
+      const int ih = e.y + b_r[j], iw = e.z + b_s[j];
+      const bool ok = e.w && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
+      const u16* src = ok ? a.x + ((long long)e.x + ih * GW + iw) * CI + b_ci[j] : g_conv_zero;
+      glds16(src, Bs + (wn + j * NW) * 512);
     }
   };
 
@@ -390,32 +421,26 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   // lane (g = lane>>4, li = lane&15) receives column col0+li of rows
   // pk+8g .. pk+8g+7 = 8 consecutive reduction elements (two tr reads).
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pc = li & 3;
-  auto tr8A = [&](const u16* base, int pk, int col0) -> bf16x8 {
+  auto tr8 = [&](const u16* img, int rowe_sel, int pk, int col0) -> bf16x8 {
     const int row = pk + 8 * g + q;
+    const int o0 = rowe_sel == 0 ? wg_off<BMW>(row, col0 + 4 * pc) : wg_off<BNW>(row, col0 + 4 * pc);
+    const int o1 = rowe_sel == 0 ? wg_off<BMW>(row + 4, col0 + 4 * pc) : wg_off<BNW>(row + 4, col0 + 4 * pc);
     const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off<BMW>(row, col0 + 4 * pc)));
+        (__attribute__((address_space(3))) s16x4_t*)(img + o0));
     const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off<BMW>(row + 4, col0 + 4 * pc)));
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  auto tr8B = [&](const u16* base, int pk, int col0) -> bf16x8 {
-    const int row = pk + 8 * g + q;
-    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off<BNW>(row, col0 + 4 * pc)));
-    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4_t*)(base + wg_off<BNW>(row + 4, col0 + 4 * pc)));
+        (__attribute__((address_space(3))) s16x4_t*)(img + o1));
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
   auto compute = [&](int buf) {
     const u16* As = lds + buf * STAGE;
-    const u16* Bs = As + BP * BMW;
+    const u16* Bs = As + A_EL;
 #pragma unroll
     for (int pk = 0; pk < BP; pk += 32) {
       bf16x8 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = tr8A(As, pk, i * 16);
+      for (int i = 0; i < TM; ++i) af[i] = tr8(As, 0, pk, i * 16);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = tr8B(Bs, pk, wn * (BNW / 4) + j * 16);
+      for (int j = 0; j < TN; ++j) bf[j] = tr8(Bs, 1, pk, wn * (BNW / 4) + j * 16);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -423,16 +448,16 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
     }
   };
 
-  const int nsteps = (int)((p_end - p_begin + BP - 1) / BP);
-  if (nsteps <= 0) return;
-  load(p_begin);
-  store(0);
+  fill_rows(0, 0);
+  fill_rows(1, 1);
+  __syncthreads();
+  stage(0, 0);
   __syncthreads();
   for (int it = 0; it < nsteps; ++it) {
     const int cur = it & 1;
-    if (it + 1 < nsteps) load(p_begin + (long long)(it + 1) * BP);
+    if (it + 1 < nsteps) stage(cur ^ 1, it + 1);
     compute(cur);
-    if (it + 1 < nsteps) store(cur ^ 1);
+    fill_rows(cur, it + 2);       // table slot `cur` was last read by stage(it)
     __syncthreads();
   }
   // D layout: lane holds rows co = 4*(lane>>4)+r of column k = lane & 15
@@ -479,9 +504,11 @@ __global__ void __launch_bounds__(256) conv_weight_transpose_kernel(
   X(8, 128, 128, 64, 2, 2)    \
   X(9, 128, 128, 32, 2, 4)    \
   X(10, 64, 128, 64, 1, 4)    \
-  X(11, 128, 64, 32, 4, 2)
+  X(11, 128, 64, 32, 4, 2)    \
+  X(12, 256, 64, 64, 4, 2)    \
+  X(13, 128, 128, 64, 2, 4)
 
-constexpr int kNumConvConfigs = 12;
+constexpr int kNumConvConfigs = 14;
 
 static int config_bm(int cfg) {
   switch (cfg) {
@@ -490,15 +517,6 @@ static int config_bm(int cfg) {
 #undef X
   }
   return 128;
-}
-
-static int config_bn(int cfg) {
-  switch (cfg) {
-#define X(id, BM, BN, BK, WM, WN) case id: return BN;
-    DMP_CONV_CONFIGS(X)
-#undef X
-  }
-  return 64;
 }
 
 int conv_num_configs() { return kNumConvConfigs; }
