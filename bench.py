@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--momentum", type=float, default=0.0)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--graph", type=int, default=1, help="capture fwd+bwd+update in a hipGraph")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra steps after timing, for rocprofv3 windows")
     return ap.parse_args()
@@ -68,6 +69,7 @@ def main():
                       n_push=a.n_push, n_pull=a.n_pull, staleness=a.staleness, mode=a.mode,
                       ps=ps, dtype=a.dtype, cuda=True, evaluate=False, verbose=False)
     w = Worker(cfg, info)
+    graphed = w.enable_graph(bool(a.graph)) if a.mode != "sync" else False
     pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device, n_batches=4,
                            dtype=w.compute_dtype, seed=info.rank)
     for _ in range(a.warmup):
@@ -116,7 +118,7 @@ def main():
                        "global_batch": global_batch, "per_gpu_batch": a.batch,
                        "seq_len": None, "image": "3x32x32",
                        "parallelism": par, "n_push": a.n_push, "n_pull": a.n_pull,
-                       "staleness": a.staleness, "lr": a.lr,
+                       "staleness": a.staleness, "lr": a.lr, "hip_graph": bool(graphed),
                        "master_dtype": "fp32"},
             "final_loss": round(final_loss, 4),
         }

@@ -348,8 +348,24 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
   return {y, part, at::scalar_tensor(G, at::kLong)};
 }
 
+void conv_weight_transpose_batched(Tensor src, Tensor dst, Tensor table, int64_t max_elems) {
+  check_gpu(src, "src");
+  check_gpu(dst, "dst");
+  TORCH_CHECK(src.scalar_type() == at::kBFloat16 && dst.scalar_type() == at::kBFloat16 &&
+                  src.numel() == dst.numel(),
+              "batched transpose: src/dst must be equal-size bf16 buffers");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.dim() == 2 &&
+                  table.size(1) == 4 && table.is_contiguous(),
+              "batched transpose: table must be a [n, 4] int64 GPU tensor");
+  dmp::launch_conv_weight_transpose_batched(reinterpret_cast<const uint16_t*>(src.data_ptr()),
+                                            reinterpret_cast<uint16_t*>(dst.data_ptr()),
+                                            reinterpret_cast<const long long*>(table.data_ptr()),
+                                            (int)table.size(0), (long long)max_elems,
+                                            cur_stream());
+}
+
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
-                  int64_t cfg) {
+                  int64_t cfg, optional<Tensor> wt_pre) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc_bf16(dy, "dy");
   check_gpu(w, "w");
@@ -363,10 +379,19 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   TORCH_CHECK((g.H + 2 * pad - g.R) / stride + 1 == g.OH && (g.W + 2 * pad - g.S) / stride + 1 == g.OW,
               "dgrad: geometry mismatch");
   TORCH_CHECK(g.CI % 64 == 0 && g.CO % 64 == 0, "native dgrad needs CI, CO % 64 == 0");
-  auto wt = at::empty({g.CI, g.R, g.S, g.CO}, w.options().memory_format(at::MemoryFormat::Contiguous));
-  dmp::launch_conv_weight_transpose(reinterpret_cast<const uint16_t*>(w.data_ptr()),
-                                    reinterpret_cast<uint16_t*>(wt.data_ptr()), g.CO, g.R * g.S,
-                                    g.CI, cur_stream());
+  Tensor wt;
+  if (wt_pre.has_value() && wt_pre->defined()) {
+    wt = *wt_pre;   // pre-transposed [CI][R][S][CO] (batched per step by the arena)
+    check_gpu(wt, "wt");
+    TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() &&
+                    wt.numel() == (int64_t)g.CI * g.R * g.S * g.CO,
+                "dgrad: pre-transposed weight must be contiguous bf16 [CI, R, S, CO]");
+  } else {
+    wt = at::empty({g.CI, g.R, g.S, g.CO}, w.options().memory_format(at::MemoryFormat::Contiguous));
+    dmp::launch_conv_weight_transpose(reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                      reinterpret_cast<uint16_t*>(wt.data_ptr()), g.CO, g.R * g.S,
+                                      g.CI, cur_stream());
+  }
   auto dx = at::empty({B, g.CI, g.H, g.W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   dmp::launch_conv_dgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                          reinterpret_cast<const uint16_t*>(wt.data_ptr()),
@@ -436,7 +461,9 @@ PYBIND11_MODULE(_native, m) {
         py::arg("cfg") = -1);
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM conv data gradient", py::arg("dy"),
         py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"),
-        py::arg("cfg") = -1);
+        py::arg("cfg") = -1, py::arg("wt") = py::none());
+  m.def("conv_weight_transpose_batched", &conv_weight_transpose_batched,
+        "transpose every conv weight of a flat bf16 shadow in one launch");
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient (fp32 accumulate)",
         py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("cfg") = -1);

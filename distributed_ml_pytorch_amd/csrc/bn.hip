@@ -93,13 +93,22 @@ __device__ __forceinline__ void reduce_partials(const float* __restrict__ part, 
                                                 int c, float& S, float& Q) {
   __shared__ float rs[16][64], rq[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  float a = 0.f, b = 0.f;
+  // 4 independent accumulator pairs keep 8 loads in flight per thread (the
+  // partial arrays come from conv epilogues with up to a few thousand blocks)
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
   if (c < C) {
-    for (int g = ty; g < G; g += 16) {
-      a += part[(long long)g * C + c];
-      b += part[(long long)(G + g) * C + c];
+    const float* ps = part + c;
+    const float* pq = part + (long long)G * C + c;
+    int g = ty;
+    for (; g + 48 < G; g += 64) {
+      a0 += ps[(long long)g * C];        b0 += pq[(long long)g * C];
+      a1 += ps[(long long)(g + 16) * C]; b1 += pq[(long long)(g + 16) * C];
+      a2 += ps[(long long)(g + 32) * C]; b2 += pq[(long long)(g + 32) * C];
+      a3 += ps[(long long)(g + 48) * C]; b3 += pq[(long long)(g + 48) * C];
     }
+    for (; g < G; g += 16) { a0 += ps[(long long)g * C]; b0 += pq[(long long)g * C]; }
   }
+  const float a = (a0 + a1) + (a2 + a3), b = (b0 + b1) + (b2 + b3);
   rs[ty][tx] = a;
   rq[ty][tx] = b;
   __syncthreads();

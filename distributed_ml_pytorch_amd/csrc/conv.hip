@@ -623,3 +623,35 @@ void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int
 }
 
 }  // namespace dmp
+
+namespace dmp {
+// All conv weights of a model transposed in ONE launch: table[i] = {offset,
+// CO, RS, CI} of weight i inside the flat bf16 shadow; W[co][rs][ci] at
+// src+offset -> Wt[ci][rs][co] at dst+offset.  blockIdx.y = weight index.
+__global__ void __launch_bounds__(256) conv_weight_transpose_batched_kernel(
+    const u16* __restrict__ src, u16* __restrict__ dst, const long long* __restrict__ table) {
+  const long long* t = table + 4 * blockIdx.y;
+  const long long off = t[0];
+  const int CO = (int)t[1], RS = (int)t[2], CI = (int)t[3];
+  const long long total = (long long)CO * RS * CI;
+  const u16* w = src + off;
+  u16* wt = dst + off;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int ci = (int)(i % CI);
+    const long long r = i / CI;
+    const int rs = (int)(r % RS);
+    const int co = (int)(r / RS);
+    wt[((long long)ci * RS + rs) * CO + co] = w[i];
+  }
+}
+
+void launch_conv_weight_transpose_batched(const u16* src, u16* dst, const long long* table, int n,
+                                          long long max_elems, hipStream_t s) {
+  if (n <= 0) return;
+  int gx = (int)((max_elems + 255) / 256);
+  if (gx > 256) gx = 256;
+  hipLaunchKernelGGL(conv_weight_transpose_batched_kernel, dim3(gx, n), dim3(256), 0, s, src, dst,
+                     table);
+}
+}  // namespace dmp

@@ -76,3 +76,9 @@ void launch_bn_fwd_partials(const uint16_t* x, const uint16_t* res, uint16_t* y,
                             float* stats, const float* part, int G, long long M, int C,
                             float momentum, float eps, bool relu, hipStream_t s);
 }  // namespace dmp
+
+namespace dmp {
+void launch_conv_weight_transpose_batched(const uint16_t* src, uint16_t* dst,
+                                          const long long* table, int n, long long max_elems,
+                                          hipStream_t s);
+}  // namespace dmp

@@ -81,6 +81,9 @@ def _wgrad_cfg(dy, x, shape, stride, pad):
 class _NativeConv(Function):
     @staticmethod
     def forward(ctx, x, w16, master, stride, pad, want_stats):
+        # the BN-partials output never receives a gradient: do not let autograd
+        # materialise (zero-fill) one for it every backward
+        ctx.set_materialize_grads(False)
         cfg = _fwd_cfg(x, w16, stride, pad)
         y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats, cfg)
         ctx.save_for_backward(x, w16)
@@ -93,14 +96,22 @@ class _NativeConv(Function):
 
     @staticmethod
     def backward(ctx, dy, _dpart):
+        if dy is None:
+            return None, None, None, None, None, None
         x, w16 = ctx.saved_tensors
         H, W, stride, pad = ctx.geom
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
+        master = ctx.master
         if ctx.needs_input_grad[0]:
             cfg = _dgrad_cfg(dy, w16, H, W, stride, pad)
-            dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg)
-        master = ctx.master
+            wt = None
+            ref = getattr(master, "_dmp_arena_ref", None)
+            arena = ref() if ref is not None else None
+            shadow = getattr(master, "_dmp_w16", None)
+            if arena is not None and shadow is not None and shadow.data_ptr() == w16.data_ptr():
+                wt = arena.transposed_conv_shadow(master)
+            dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt)
         gw = None
         if master is not None and master.requires_grad:
             wcfg = _wgrad_cfg(dy, x, tuple(master.shape), stride, pad)

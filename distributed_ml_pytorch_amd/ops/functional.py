@@ -77,6 +77,7 @@ def compute_weight(p: torch.Tensor | None, dtype: torch.dtype):
 class _SoftmaxXent(Function):
     @staticmethod
     def forward(ctx, logits, labels, smoothing, ignore_index):
+        ctx.set_materialize_grads(False)
         loss, hits, dlogits = native().softmax_xent(logits.contiguous(), labels.contiguous(), True,
                                                     float(smoothing), int(ignore_index))
         ctx.save_for_backward(dlogits)
@@ -86,6 +87,8 @@ class _SoftmaxXent(Function):
     @staticmethod
     def backward(ctx, gloss, ghits):
         (dlogits,) = ctx.saved_tensors
+        if gloss is None:
+            return None, None, None, None
         return dlogits * gloss.to(dlogits.dtype), None, None, None
 
 

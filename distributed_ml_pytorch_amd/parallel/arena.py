@@ -21,6 +21,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import weakref
+
 import torch
 
 ALIGN = 64
@@ -78,6 +80,13 @@ class FlatArena:
         self.w16 = (torch.zeros(self.numel, dtype=shadow_dtype, device=dev)
                     if shadow_dtype is not None else None)
         self._ready_cb = None
+        # bumped whenever the bf16 shadow may have changed; keys the cache of
+        # transposed conv weights used by the data-gradient kernels
+        self.version = 0
+        self._wt = None
+        self._wt_version = -1
+        self._wt_table = None
+        self._wt_max = 0
         with torch.no_grad():
             for p, s in zip(self.params, self.slots):
                 cl = channels_last and p.dim() == 4
@@ -87,6 +96,7 @@ class FlatArena:
                 if self.g32 is not None:
                     p.grad = _strided_view(self.g32, s.offset, p, cl)
                 p._dmp_arena = True
+                p._dmp_arena_ref = weakref.ref(self)
                 if self.w16 is not None:
                     p._dmp_w16 = _strided_view(self.w16, s.offset, p, cl)
         self.refresh_shadow()
@@ -99,7 +109,43 @@ class FlatArena:
         return self.g32 if grads else self.p32
 
     # ----------------------------------------------------------------- shadow
+    def bump(self):
+        self.version += 1
+
+    def transposed_conv_shadow(self, p: torch.Tensor):
+        """bf16 ``[CI, R, S, CO]`` transpose of conv weight ``p``'s shadow.
+
+        All 4-D weights are transposed together in ONE kernel launch the first
+        time this is called after the shadow changed (instead of one launch per
+        conv per backward).
+        """
+        if self.w16 is None or not self.w16.is_cuda:
+            return None
+        if self._wt is None:
+            rows = []
+            self._wt_index = {}
+            for s, q in zip(self.slots, self.params):
+                if len(s.shape) == 4:
+                    co, ci, r, k = s.shape
+                    self._wt_index[id(q)] = s
+                    rows.append([s.offset, co, r * k, ci])
+                    self._wt_max = max(self._wt_max, s.numel)
+            self._wt = torch.empty_like(self.w16)
+            self._wt_table = torch.tensor(rows, dtype=torch.int64, device=self.device)
+        s = self._wt_index.get(id(p))
+        if s is None:
+            return None
+        if self._wt_version != self.version:
+            from ..ops._ext import native
+
+            native().conv_weight_transpose_batched(self.w16, self._wt, self._wt_table,
+                                                   self._wt_max)
+            self._wt_version = self.version
+        co, ci, r, k = s.shape
+        return self._wt[s.offset:s.offset + s.numel].view(ci, r, k, co)
+
     def refresh_shadow(self):
+        self.bump()
         if self.w16 is None:
             return
         if self.p32.is_cuda:
@@ -111,6 +157,9 @@ class FlatArena:
 
     # ------------------------------------------------------------------ grads
     def zero_grad(self):
+        # a new step begins: the shadow may have been rewritten by the update /
+        # a pull landing since the last backward
+        self.bump()
         if self.g32 is not None:
             self.g32.zero_()
 

@@ -115,15 +115,25 @@ class Asynchronous(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        lr = self.param_groups[0]["lr"]
-        self._local_update(lr)
+        self.local_step()
+        self.comm_step()
+        return loss
+
+    @torch.no_grad()
+    def local_step(self):
+        """Device-only half of a step (graph-capturable): fused accumulate + SGD."""
+        self._local_update(self.param_groups[0]["lr"])
+        self.arena.bump()
+
+    @torch.no_grad()
+    def comm_step(self):
+        """Host-scheduled half: push / pull / land on the reference cadence."""
         if self.idx % self.n_push == 0:
             self.client.push(self.idx)
         if self.idx % self.n_pull == 0:
             self.client.request_pull(self.idx)
         self.client.land_due(self.idx)
         self.idx += 1
-        return loss
 
     def finish(self):
         """Land outstanding pulls, flush sends, tell the PS we are done."""

@@ -137,6 +137,7 @@ class PSClient:
                     arena.w16.copy_(arena.p32)
         self.version = max(self.version, pend.version)
         self.pulls += 1
+        arena.bump()
 
     def land_due(self, step: int, force: bool = False):
         while self.pending and (force or self.pending[0].step <= step - self.staleness):

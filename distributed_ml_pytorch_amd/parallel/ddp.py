@@ -120,9 +120,18 @@ class FusedSGD(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self.local_step()
+        return loss
+
+    def comm_step(self):
+        pass
+
+    @torch.no_grad()
+    def local_step(self):
         g = self.param_groups[0]
         a = self.arena
         lr = g["lr"]
+        a.bump()
         if self.grad_scale != 1.0:
             # fold the 1/W average into lr (and rescale weight decay so wd*p is not scaled)
             lr_eff = lr * self.grad_scale
@@ -146,4 +155,3 @@ class FusedSGD(Optimizer):
             a.p32.add_(d, alpha=-lr_eff)
             if a.w16 is not None:
                 a.w16.copy_(a.p32)
-        return loss

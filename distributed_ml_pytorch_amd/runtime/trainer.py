@@ -150,8 +150,59 @@ class Worker:
                 x = x.contiguous(memory_format=torch.channels_last)
         return x, y.to(self.device, non_blocking=True)
 
+    # ------------------------------------------------------------ hipGraph path
+    def enable_graph(self, enabled: bool = True):
+        """Replay forward+backward+fused update as ONE captured hipGraph per step.
+
+        The push/pull/land half of the ASGD step (which depends on the step
+        index) stays eager between replays.  Not used for sync-DP (its RCCL
+        bucket all-reduces fire from inside backward).
+        """
+        self.use_graph = bool(enabled) and self.device.type == "cuda" and self.ddp is None
+        self.graph = None
+        return self.use_graph
+
+    def _graph_body(self):
+        self.opt.zero_grad()
+        logits = self.model(self._gx)
+        loss, hits = softmax_cross_entropy(logits, self._gy, self.cfg.label_smoothing)
+        loss.backward()
+        self.opt.local_step()
+        return loss.detach(), hits
+
+    def _capture(self, x, y):
+        self._gx = x.detach().clone()
+        self._gy = y.detach().clone()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):          # real steps: tune kernels, warm allocator/libraries
+                self._graph_body()
+                self.opt.comm_step()
+                self.step_idx += 1
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._gloss, self._ghits = self._graph_body()
+        self.graph = g
+        self._graph_key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
+
+    def _graph_step(self, x, y):
+        key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
+        if self.graph is None or key != self._graph_key:
+            self._capture(x, y)
+        self._gx.copy_(x, non_blocking=True)
+        self._gy.copy_(y, non_blocking=True)
+        self.graph.replay()
+        self.opt.comm_step()
+        self.step_idx += 1
+        # the captured outputs are overwritten by the next replay
+        return self._gloss.clone(), self._ghits.clone()
+
     def train_step(self, x, y):
         """One fwd+bwd+update. Returns (loss, hits) as device tensors (no sync)."""
+        if getattr(self, "use_graph", False):
+            return self._graph_step(x, y)
         self.opt.zero_grad()
         logits = self.model(x)
         loss, hits = softmax_cross_entropy(logits, y, self.cfg.label_smoothing)
