@@ -171,26 +171,28 @@ class Worker:
         return loss.detach(), hits
 
     def _capture(self, x, y):
+        """Run this step eagerly on a side stream (tunes kernels, warms the
+        allocator and libraries), then capture the step body for later replays."""
         self._gx = x.detach().clone()
         self._gy = y.detach().clone()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            for _ in range(2):          # real steps: tune kernels, warm allocator/libraries
-                self._graph_body()
-                self.opt.comm_step()
-                self.step_idx += 1
+            loss, hits = self._graph_body()
+            self.opt.comm_step()
+            self.step_idx += 1
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._gloss, self._ghits = self._graph_body()
         self.graph = g
         self._graph_key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
+        return loss.clone(), hits.clone()
 
     def _graph_step(self, x, y):
         key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
         if self.graph is None or key != self._graph_key:
-            self._capture(x, y)
+            return self._capture(x, y)
         self._gx.copy_(x, non_blocking=True)
         self._gy.copy_(y, non_blocking=True)
         self.graph.replay()
