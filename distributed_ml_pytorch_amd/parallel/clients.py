@@ -286,9 +286,11 @@ class ShardedPSClient(PSClient):
     the pull is due (``staleness`` steps later).
     """
 
-    def __init__(self, group=None, **kw):
+    def __init__(self, group=None, force_collectives: bool = False, **kw):
         super().__init__(**kw)
         self.group = group
+        # run the RCCL path even at world size 1 (single-GPU validation)
+        self.force = force_collectives
 
     def init(self):
         self.world = dist.get_world_size(self.group) if dist.is_initialized() else 1
@@ -297,7 +299,7 @@ class ShardedPSClient(PSClient):
         if n % self.world:
             raise ValueError(f"arena length {n} not divisible by world size {self.world}")
         self.shard_n = n // self.world
-        if self.world > 1:
+        if self.world > 1 or self.force:
             # identical starting point everywhere (the reference let every worker
             # start from its own random init and converge through pulls)
             dist.broadcast(self.arena.p32, 0, group=self.group)
@@ -319,7 +321,7 @@ class ShardedPSClient(PSClient):
         buf = self._handoff()
         self.pushes += 1
         self.bytes_sent += buf.numel() * buf.element_size() * (self.world - 1) // max(self.world, 1)
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             if self.cuda:
                 self.nat.ps_apply(self.master, buf, None, 1.0)
             else:
@@ -354,7 +356,7 @@ class ShardedPSClient(PSClient):
         buf, free_ev = self._pull_bufs.popleft() if len(self._pull_bufs) > self.staleness else \
             (torch.empty(n, dtype=torch.float32, device=self.device), None)
         self.bytes_recv += n * 4 * (self.world - 1) // max(self.world, 1)
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             buf.copy_(self.master)
             self.pending.append(_Pending(step, buf))
             return

@@ -27,8 +27,9 @@ from .arena import FlatArena
 
 class BucketedAllReduce:
     def __init__(self, arena: FlatArena, group=None, bucket_mb: float = 32.0,
-                 overlap: bool = True):
+                 overlap: bool = True, force_collectives: bool = False):
         self.arena = arena
+        self.force = force_collectives
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.overlap = overlap
@@ -60,7 +61,7 @@ class BucketedAllReduce:
         self.seen = set()
 
     def _launch(self, b: int):
-        if self.works[b] is not None or self.world == 1:
+        if self.works[b] is not None or (self.world == 1 and not self.force):
             return
         lo, hi, _ = self.buckets[b]
         view = self.arena.g32[lo:hi]

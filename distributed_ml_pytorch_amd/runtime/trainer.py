@@ -183,7 +183,8 @@ class Worker:
             self.step_idx += 1
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: RCCL's watchdog thread queries events while we capture
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._gloss, self._ghits = self._graph_body()
         self.graph = g
         self._graph_key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
