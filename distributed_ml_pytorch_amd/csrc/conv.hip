@@ -303,178 +303,6 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   }
 }
 
-// ------------------------------------------------------------------- wgrad
-struct WgradArgs {
-  const u16* dy;    // [P][CO]  (P = B*OH*OW)
-  const u16* x;     // [B][GH][GW][CI]
-  float* dw;        // [CO][R][S][CI] fp32, accumulated
-  int B, GH, GW, CI, OH, OW, CO, R, S, stride, pad;
-  long long P;
-  int p_chunk;      // rows of P per block (multiple of 64)
-};
-
-// 32-B granule swizzle (an involution) for [p][ROWE] bf16 images read by
-// ds_read_b64_tr_b16.  A transposed read of one half-wave touches rows
-// {8g+q : g=0,1, q=0..3} (and +4 for the second read) in one granule.  Row
-// strides of 128/384 B put rows of equal parity on one bank offset -> f spreads
-// rows {0,2,8,10} over 4 granules; 256-B rows put every row on one offset -> f
-// spreads all 8 rows.
-template <int ROWE>
-__device__ __forceinline__ int wg_f(int row) {
-  if constexpr (ROWE == 128) return (row & 3) | (((row >> 3) & 1) << 2);
-  else return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
-}
-template <int ROWE>
-__device__ __forceinline__ int wg_off(int row, int col) {
-  return row * ROWE + ((((col >> 4) ^ wg_f<ROWE>(row))) << 4) + (col & 15);
-}
-
-// Block: 4 waves side by side along k (WN=4), each 64 (co) x BNW/4 (k).
-template <int BNW>
-__global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
-  constexpr int BMW = 64, BP = 64, NW = 4;
-  constexpr int TM = 4, TN = BNW / 64;
-  constexpr int A_EL = BP * BMW, B_EL = BP * BNW;
-  constexpr int A_INS = A_EL / 512, B_INS = B_EL / 512;     // 1 KiB per glds instruction
-  constexpr int A_PW = A_INS / NW, B_PW = B_INS / NW;
-  constexpr int STAGE = A_EL + B_EL;
-  static_assert(A_INS % NW == 0 && B_INS % NW == 0, "instruction split");
-  // [2][STAGE] staging, then the [2][BP] row table (int4 per row)
-  __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE + 2 * BP * 8];
-  int4* rowtab = reinterpret_cast<int4*>(lds + 2 * STAGE);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wn = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kx0 = blockIdx.x * BNW;            // first column in K = (r, s, ci)
-  const int co0 = blockIdx.y * BMW;
-  const long long p_begin = (long long)blockIdx.z * a.p_chunk;
-  const long long p_end = min(a.P, p_begin + a.p_chunk);
-  const int GH = a.GH, GW = a.GW, CI = a.CI;
-  const int nsteps = (int)((p_end - p_begin + BP - 1) / BP);
-  if (nsteps <= 0) return;
-
-  // per-lane DMA slots (fixed across stages): A = dY rows, B = X rows x tap columns
-  int a_row[A_PW], a_col[A_PW];
-#pragma unroll
-  for (int j = 0; j < A_PW; ++j) {
-    const int e = (wn + j * NW) * 512 + lane * 8;        // element index in the A image
-    const int row = e / BMW, pch = (e % BMW) / 8;
-    const int u = (pch >> 1) ^ wg_f<BMW>(row);
-    a_row[j] = row;
-    a_col[j] = co0 + u * 16 + (pch & 1) * 8;
-  }
-  int b_row[B_PW], b_r[B_PW], b_s[B_PW], b_ci[B_PW];
-#pragma unroll
-  for (int j = 0; j < B_PW; ++j) {
-    const int e = (wn + j * NW) * 512 + lane * 8;
-    const int row = e / BNW, pch = (e % BNW) / 8;
-    const int u = (pch >> 1) ^ wg_f<BNW>(row);
-    const int kc = kx0 + u * 16 + (pch & 1) * 8;
-    const int rs = kc / CI;
-    b_row[j] = row;
-    b_ci[j] = kc - rs * CI;
-    b_r[j] = rs / a.S;
-    b_s[j] = rs - b_r[j] * a.S;
-  }
-  // row table for stage `st`: {pixel base, oh*stride-pad, ow*stride-pad, valid}
-  auto fill_rows = [&](int tab, int stg) {
-    if (tid < BP) {
-      const long long p = p_begin + (long long)stg * BP + tid;
-      int4 e = make_int4(0, -(1 << 20), -(1 << 20), 0);
-      if (stg < nsteps && p < p_end) {
-        const int ow = (int)(p % a.OW);
-        const long long t = p / a.OW;
-        const int oh = (int)(t % a.OH);
-        const int b = (int)(t / a.OH);
-        e = make_int4(b * GH * GW, oh * a.stride - a.pad, ow * a.stride - a.pad, 1);
-      }
-      rowtab[tab * BP + tid] = e;
-    }
-  };
-  auto stage = [&](int buf, int stg) {
-    const long long pb = p_begin + (long long)stg * BP;
-    u16* As = lds + buf * STAGE;
-    u16* Bs = As + A_EL;
-#pragma unroll
-    for (int j = 0; j < A_PW; ++j) {
-      const long long p = pb + a_row[j];
-      const u16* src = p < p_end ? a.dy + p * a.CO + a_col[j] : g_conv_zero;
-      glds16(src, As + (wn + j * NW) * 512);
-    }
-    const int4* tb = rowtab + (stg & 1) * BP;
-#pragma unroll
-    for (int j = 0; j < B_PW; ++j) {
-      const int4 e = tb[b_row[j]];
-      const int ih = e.y + b_r[j], iw = e.z + b_s[j];
-      const bool ok = e.w && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
-      const u16* src = ok ? a.x + ((long long)e.x + ih * GW + iw) * CI + b_ci[j] : g_conv_zero;
-      glds16(src, Bs + (wn + j * NW) * 512);
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // lane (g = lane>>4, li = lane&15) receives column col0+li of rows
-  // pk+8g .. pk+8g+7 = 8 consecutive reduction elements (two tr reads).
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, pc = li & 3;
-  auto tr8 = [&](const u16* img, int rowe_sel, int pk, int col0) -> bf16x8 {
-    const int row = pk + 8 * g + q;
-    const int o0 = rowe_sel == 0 ? wg_off<BMW>(row, col0 + 4 * pc) : wg_off<BNW>(row, col0 + 4 * pc);
-    const int o1 = rowe_sel == 0 ? wg_off<BMW>(row + 4, col0 + 4 * pc) : wg_off<BNW>(row + 4, col0 + 4 * pc);
-    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4_t*)(img + o0));
-    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4_t*)(img + o1));
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  auto compute = [&](int buf) {
-    const u16* As = lds + buf * STAGE;
-    const u16* Bs = As + A_EL;
-#pragma unroll
-    for (int pk = 0; pk < BP; pk += 32) {
-      bf16x8 af[TM], bf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = tr8(As, 0, pk, i * 16);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = tr8(Bs, 1, pk, wn * (BNW / 4) + j * 16);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-    }
-  };
-
-  fill_rows(0, 0);
-  fill_rows(1, 1);
-  __syncthreads();
-  stage(0, 0);
-  __syncthreads();
-  for (int it = 0; it < nsteps; ++it) {
-    const int cur = it & 1;
-    if (it + 1 < nsteps) stage(cur ^ 1, it + 1);
-    compute(cur);
-    fill_rows(cur, it + 2);       // table slot `cur` was last read by stage(it)
-    __syncthreads();
-  }
-  // D layout: lane holds rows co = 4*(lane>>4)+r of column k = lane & 15
-  const long long K = (long long)a.R * a.S * a.CI;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int kk = kx0 + wn * (BNW / 4) + j * 16 + (lane & 15);
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int co = co0 + i * 16 + 4 * (lane >> 4) + rr;
-        atomicAdd(a.dw + (long long)co * K + kk, acc[i][j][rr]);
-      }
-    }
-}
-
 // W[co][r][s][ci] -> Wt[ci][r][s][co]  (bf16)
 __global__ void __launch_bounds__(256) conv_weight_transpose_kernel(
     const u16* __restrict__ w, u16* __restrict__ wt, int CO, int RS, int CI) {
@@ -595,32 +423,6 @@ void launch_conv_weight_transpose(const u16* w, u16* wt, int CO, int RS, int CI,
                      w, wt, CO, RS, CI);
 }
 
-// cfg: low 2 bits select BNW (0 -> auto, 1 -> 64, 2 -> 128, 3 -> 192), the rest
-// the minimum rows of P per block (in units of 512; 0 -> auto).
-void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int W, int CI,
-                       int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                       hipStream_t s) {
-  WgradArgs a{dy, x, dw, B, H, W, CI, OH, OW, CO, R, S, stride, pad, (long long)B * OH * OW, 0};
-  const long long K = (long long)R * S * CI;
-  int bnw = 64;
-  const int sel = cfg < 0 ? 0 : (cfg & 3);
-  if (sel == 0) bnw = (K % 192 == 0) ? 192 : (K % 128 == 0 ? 128 : 64);
-  else bnw = sel == 1 ? 64 : (sel == 2 ? 128 : 192);
-  if (K % bnw != 0) bnw = 64;
-  const long long tiles = (K / bnw) * (CO / 64);
-  long long min_chunk = cfg < 0 ? 0 : (long long)(cfg >> 2) * 512;
-  if (min_chunk <= 0) min_chunk = 2048;
-  long long splits = (768 + tiles - 1) / tiles;
-  long long chunk = (a.P + splits - 1) / splits;
-  if (chunk < min_chunk) chunk = min_chunk;
-  chunk = (chunk + 63) / 64 * 64;
-  splits = (a.P + chunk - 1) / chunk;
-  a.p_chunk = (int)chunk;
-  const dim3 grid((unsigned)(K / bnw), (unsigned)(CO / 64), (unsigned)splits);
-  if (bnw == 192) hipLaunchKernelGGL((conv_wgrad_kernel<192>), grid, dim3(256), 0, s, a);
-  else if (bnw == 128) hipLaunchKernelGGL((conv_wgrad_kernel<128>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<64>), grid, dim3(256), 0, s, a);
-}
 
 }  // namespace dmp
 

@@ -46,12 +46,15 @@ def _igemm_candidates(out_channels: int):
 
 
 def _wgrad_candidates(K: int):
+    """cfg = BNW sel | BP32 << 2 | NS3 << 3 | (min P rows / 512) << 4 (csrc/conv_wgrad.hip)."""
     cands = []
     for sel, bnw in ((1, 64), (2, 128), (3, 192)):
         if K % bnw:
             continue
-        for chunk in (2, 4, 8):          # x512 rows of P per block
-            cands.append(sel | (chunk << 2))
+        for bp32 in (0, 1):
+            for ns3 in (0, 1):
+                for chunk in (2, 4, 8):          # x512 rows of P per block
+                    cands.append(sel | (bp32 << 2) | (ns3 << 3) | (chunk << 4))
     return cands
 
 

@@ -49,14 +49,12 @@ def main():
         d = t(lambda: nat.conv_dgrad(dy, w, H, W, st, pd, cid))
         print(f"cfg {cid:2d} {c[1:]}: fwd+stats {f1:.4f} ({fl / f1 / 1e9:6.1f} TF)  fwd {f0:.4f} "
               f"({fl / f0 / 1e9:6.1f})  dgrad {d:.4f} ({fl / d / 1e9:6.1f})")
-    K = CI * k * k
-    for sel in (1, 2, 3):
-        if K % (64 * sel):
-            continue
-        for ch in (2, 4, 8, 16):
-            cfg = sel | (ch << 2)
-            ww = t(lambda: nat.conv_wgrad(dy, x, dw, st, pd, cfg))
-            print(f"wgrad bnw={64 * sel} chunk={512 * ch}: {ww:.4f} ({fl / ww / 1e9:6.1f} TF)")
+    from distributed_ml_pytorch_amd.ops.conv import _wgrad_candidates
+
+    for cfg in _wgrad_candidates(CI * k * k):
+        ww = t(lambda: nat.conv_wgrad(dy, x, dw, st, pd, cfg))
+        print(f"wgrad bnw={64 * (cfg & 3)} bp={32 if cfg & 4 else 64} ns={3 if cfg & 8 else 2} "
+              f"chunk={512 * (cfg >> 4)}: {ww:.4f} ({fl / ww / 1e9:6.1f} TF)")
 
 
 if __name__ == "__main__":

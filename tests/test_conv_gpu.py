@@ -80,14 +80,12 @@ def test_every_tile_config(shape):
         torch.testing.assert_close(ps[0], y.float().sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
         dx = nat.conv_dgrad(dy, w, H, W, st, pd, cfg)
         assert _rel(dx, xr.grad) < 1e-2, cfg
-    K = CI * k * k
-    for sel in (1, 2, 3):
-        if K % (64 * sel):
-            continue
-        for chunk in (2, 8):
-            dw = torch.zeros(CO, CI, k, k, device="cuda").contiguous(memory_format=CL)
-            nat.conv_wgrad(dy, x, dw, st, pd, sel | (chunk << 2))
-            assert _rel(dw, wr.grad) < 1e-2, (sel, chunk)
+    from distributed_ml_pytorch_amd.ops.conv import _wgrad_candidates
+
+    for cfg in _wgrad_candidates(CI * k * k):
+        dw = torch.zeros(CO, CI, k, k, device="cuda").contiguous(memory_format=CL)
+        nat.conv_wgrad(dy, x, dw, st, pd, cfg)
+        assert _rel(dw, wr.grad) < 1e-2, cfg
 
 
 def test_conv_layer_autograd_and_bn_fusion():
