@@ -417,6 +417,76 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int
                          (int)cfg, cur_stream());
 }
 
+// few-input-channel (stem) convolutions: x any dense bf16 4-D layout,
+// w bf16 channels_last [CO, CI, R, S] with CO % 64 == 0 and R*S*CI <= 384
+struct SmallGeom {
+  int B, CI, H, W, CO, R, S, OH, OW;
+};
+
+SmallGeom small_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad) {
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "small conv: 4-D tensors expected");
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, "small conv: x must be bf16 GPU");
+  SmallGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(0),
+              (int)w.size(2), (int)w.size(3), 0, 0};
+  TORCH_CHECK(w.size(1) == g.CI, "small conv: weight/input channel mismatch");
+  TORCH_CHECK(stride >= 1 && pad >= 0 && g.R <= 255 && g.S <= 255, "small conv: bad geometry");
+  TORCH_CHECK(g.CO % 64 == 0, "small conv: CO must be a multiple of 64");
+  TORCH_CHECK(g.R * g.S * g.CI <= dmp::conv_small_max_k(), "small conv: R*S*CI too large");
+  g.OH = (g.H + 2 * (int)pad - g.R) / (int)stride + 1;
+  g.OW = (g.W + 2 * (int)pad - g.S) / (int)stride + 1;
+  TORCH_CHECK(g.OH > 0 && g.OW > 0, "small conv: empty output");
+  TORCH_CHECK((long long)g.B * g.OH * g.OW * g.CO < (1LL << 31) && x.numel() < (1LL << 30),
+              "small conv: tensor too large for 32-bit indexing");
+  return g;
+}
+
+std::vector<Tensor> conv_small_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad,
+                                   bool want_stats) {
+  check_gpu(w, "w");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv weight must be bf16 channels_last");
+  auto g = small_geom(x, w, stride, pad);
+  auto y = at::empty({g.B, g.CO, g.OH, g.OW},
+                     x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const long long P = (long long)g.B * g.OH * g.OW;
+  Tensor part;
+  int64_t G = 0;
+  if (want_stats) {
+    G = dmp::conv_small_fwd_blocks(P);
+    part = at::empty({2 * G * g.CO}, x.options().dtype(at::kFloat));
+  }
+  dmp::launch_conv_small_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                             (int)(2 * x.numel()), (int)x.stride(0),
+                             (int)x.stride(2), (int)x.stride(3), (int)x.stride(1),
+                             reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                             reinterpret_cast<uint16_t*>(y.data_ptr()),
+                             want_stats ? part.data_ptr<float>() : nullptr, g.B, g.H, g.W, g.CI,
+                             g.OH, g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, cur_stream());
+  return {y, part, at::scalar_tensor(G, at::kLong)};
+}
+
+void conv_small_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc_bf16(dy, "dy");
+  check_gpu(dw, "dw");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 4 &&
+                  dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "dw must be an fp32 channels_last [CO, CI, R, S] tensor");
+  auto g = small_geom(x, dw, stride, pad);
+  TORCH_CHECK(dy.size(0) == g.B && dy.size(1) == g.CO && dy.size(2) == g.OH && dy.size(3) == g.OW,
+              "small wgrad: dy shape mismatch");
+  const long long P = (long long)g.B * g.OH * g.OW;
+  const int G = dmp::conv_small_wgrad_blocks(P, g.CO, g.R, g.S, g.CI);
+  auto ws = at::empty({(int64_t)G * g.CO * g.R * g.S * g.CI}, dw.options());
+  dmp::launch_conv_small_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                               reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                               (int)(2 * x.numel()), (int)x.stride(0),
+                               (int)x.stride(2), (int)x.stride(3), (int)x.stride(1),
+                               dw.data_ptr<float>(), ws.data_ptr<float>(), g.B,
+                               g.H, g.W, g.CI, g.OH, g.OW, g.CO, g.R, g.S, (int)stride, (int)pad,
+                               cur_stream());
+}
+
 std::vector<std::vector<int64_t>> conv_configs() {
   std::vector<std::vector<int64_t>> out;
   for (int c = 0; c < dmp::conv_num_configs(); ++c) {
@@ -469,6 +539,10 @@ PYBIND11_MODULE(_native, m) {
         py::arg("cfg") = -1);
   m.def("conv_configs", &conv_configs, "[(id, BM, BN, BK, threads)] of the compiled conv tiles");
   m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials");
+  m.def("conv_small_fwd", &conv_small_fwd, "few-input-channel conv forward (+BN partials)",
+        py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"));
+  m.def("conv_small_wgrad", &conv_small_wgrad, "few-input-channel conv weight gradient (fp32 +=)",
+        py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"));
   m.doc() = "gfx950 (MI355X) HIP kernels for distributed_ml_pytorch_amd";
   m.def("asgd_fused_step", &asgd_fused_step, "fused flat ASGD/SGD update");
   m.def("ps_apply", &ps_apply, "parameter-server delta apply");

@@ -430,29 +430,49 @@ namespace dmp {
 // All conv weights of a model transposed in ONE launch: table[i] = {offset,
 // CO, RS, CI} of weight i inside the flat bf16 shadow; W[co][rs][ci] at
 // src+offset -> Wt[ci][rs][co] at dst+offset.  blockIdx.y = weight index.
+// Every (rs) slice is a CO x CI matrix transposed through LDS in 64 x 64
+// tiles: 128-B coalesced row reads and row writes (CO, CI multiples of 64 --
+// the only weights the native dgrad consumes).
 __global__ void __launch_bounds__(256) conv_weight_transpose_batched_kernel(
     const u16* __restrict__ src, u16* __restrict__ dst, const long long* __restrict__ table) {
+  __shared__ u16 tile[64][66];
   const long long* t = table + 4 * blockIdx.y;
   const long long off = t[0];
   const int CO = (int)t[1], RS = (int)t[2], CI = (int)t[3];
-  const long long total = (long long)CO * RS * CI;
+  const int tco = CO / 64, tci = CI / 64;
+  const int ntiles = RS * tco * tci;
   const u16* w = src + off;
   u16* wt = dst + off;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int ci = (int)(i % CI);
-    const long long r = i / CI;
-    const int rs = (int)(r % RS);
-    const int co = (int)(r / RS);
-    wt[((long long)ci * RS + rs) * CO + co] = w[i];
+  const int tid = threadIdx.x, r = tid >> 2, c = (tid & 3) * 16;
+  for (int tt = blockIdx.x; tt < ntiles; tt += gridDim.x) {
+    const int rs = tt / (tco * tci), rem = tt - rs * tco * tci;
+    const int co0 = (rem / tci) * 64, ci0 = (rem % tci) * 64;
+    // read row co0+r, columns ci0+c .. +15
+    const uint4* g = reinterpret_cast<const uint4*>(w + ((long long)(co0 + r) * RS + rs) * CI + ci0 + c);
+    const uint4 v0 = g[0], v1 = g[1];
+    const u16* e0 = reinterpret_cast<const u16*>(&v0);
+    const u16* e1 = reinterpret_cast<const u16*>(&v1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { tile[r][c + k] = e0[k]; tile[r][c + 8 + k] = e1[k]; }
+    __syncthreads();
+    // write row ci0+r of Wt[.][rs][.], columns co0+c .. +15
+    uint4 o0, o1;
+    u16* f0 = reinterpret_cast<u16*>(&o0);
+    u16* f1 = reinterpret_cast<u16*>(&o1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { f0[k] = tile[c + k][r]; f1[k] = tile[c + 8 + k][r]; }
+    uint4* d = reinterpret_cast<uint4*>(wt + ((long long)(ci0 + r) * RS + rs) * CO + co0 + c);
+    d[0] = o0;
+    d[1] = o1;
+    __syncthreads();
   }
 }
 
 void launch_conv_weight_transpose_batched(const u16* src, u16* dst, const long long* table, int n,
                                           long long max_elems, hipStream_t s) {
   if (n <= 0) return;
-  int gx = (int)((max_elems + 255) / 256);
-  if (gx > 256) gx = 256;
+  long long tiles = max_elems / 4096;
+  int gx = (int)(tiles < 1 ? 1 : (tiles > 1024 ? 1024 : tiles));
   hipLaunchKernelGGL(conv_weight_transpose_batched_kernel, dim3(gx, n), dim3(256), 0, s, src, dst,
                      table);
 }

@@ -1,0 +1,363 @@
+// Few-input-channel convolutions (network stems: CIFAR ResNet 3x3x3, ImageNet
+// ResNet 7x7x3, AlexNet 11x11x3) on gfx950.
+//
+// K = R*S*CI is tiny (27 .. 363), so the implicit GEMM has nothing to feed the
+// matrix cores with and MIOpen spends its time in layout shuffles and
+// zero-fills around a K=27 GEMM.  These are VALU kernels shaped so that most
+// per-FMA operand traffic is an LDS broadcast:
+//
+//   forward  lane = 4 consecutive output pixels, wave = 16 of the 64 output
+//            channels of the tile (64 fp32 accumulators per lane).  The weight
+//            tile [K][64] sits in LDS as fp32; all lanes of a wave read the same
+//            row (broadcast ds_read_b128), so 4 LDS reads feed 64 FMAs.  Patch
+//            taps are gathered 8 at a time through an LDS tap table (no integer
+//            division in the loop).  Epilogue: bf16 NHWC store + per-channel BN
+//            partial sums (recursive-halving butterfly over the lanes, lane l
+//            ends up owning channel l & 15), same [2][G][CO] layout as the
+//            implicit-GEMM epilogue (conv.hip).
+//   wgrad    dW[co][k] = sum_p dY[p][co] * patch_p[k]: a block owns a chunk of
+//            P, a 64-channel x 32-tap output tile; 64-pixel slabs of dY and of
+//            the patches are staged to LDS as fp32, each lane accumulates a 4 x 8
+//            outer product per pixel, the 4 waves split the slab rows and are
+//            summed through LDS, then fp32 atomics into the arena gradient.
+// The input image is read with explicit element strides (any dense layout of
+// the bf16 activations).
+#include "common.h"
+
+namespace dmp {
+
+struct SmallConvArgs {
+  const u16* x;     // input, element strides below (bf16)
+  const u16* w;     // [CO][R][S][CI] bf16
+  const u16* dy;    // [P][CO] bf16 (wgrad)
+  u16* y;           // [P][CO] bf16 (forward)
+  float* part;      // [2][G][CO] BN partials (forward, optional)
+  float* dw;        // [CO][R][S][CI] fp32 (wgrad, accumulated)
+  float* ws;        // wgrad: [G][CO][K] per-block partial tiles
+  int sb, sh, sw, sc;           // input strides in elements (input < 2^30 elements)
+  int xbytes;                   // input extent in bytes (buffer descriptor bound)
+  int B, H, W, CI, OH, OW, CO, R, S, stride, pad, K;
+  long long P;
+  int chunk;        // wgrad: pixels per block
+};
+
+// tap table entry: r | s << 8 | ci << 16 (k >= K -> -1)
+__device__ __forceinline__ int tap_of(const SmallConvArgs& a, int k) {
+  if (k >= a.K) return -1;
+  const int ci = k % a.CI, rs = k / a.CI;
+  return (rs / a.S) | ((rs % a.S) << 8) | (ci << 16);
+}
+
+// raw buffer descriptor over the input image (gfx9 dword3); a load whose
+// offset is past num_records returns 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc(const SmallConvArgs& a) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, a.xbytes, 0x00020000);
+}
+
+// boff = b * sb (element offset of the image).  Padding / masked taps get an
+// out-of-range offset and read 0 from the buffer unit: no branch per tap, so a
+// thread's gathers issue back to back and retire under one wait.
+__device__ __forceinline__ float load_tap(const SmallConvArgs& a, __amdgpu_buffer_rsrc_t rs,
+                                          int tap, int boff, int ih0, int iw0) {
+  const int ih = ih0 + (tap & 255), iw = iw0 + ((tap >> 8) & 255), ci = tap >> 16;
+  const bool ok = tap >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+  const int off = ok ? 2 * (boff + ih * a.sh + iw * a.sw + ci * a.sc) : 0x7ffffff0;
+  return bf2f(__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
+}
+
+// output pixel p (< 2^31) -> {b * sb, oh * stride - pad, ow * stride - pad}
+__device__ __forceinline__ int3 decode_pixel(const SmallConvArgs& a, int p) {
+  const int ow = p % a.OW, t = p / a.OW;
+  const int oh = t % a.OH, b = t / a.OH;
+  return make_int3(b * a.sb, oh * a.stride - a.pad, ow * a.stride - a.pad);
+}
+
+// v[0..2H) -> v[0..H): lanes with bit H set keep the upper half
+template <int H>
+__device__ __forceinline__ void halve(float* v, int lane) {
+  const bool up = lane & H;
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const float send = up ? v[i] : v[i + H];
+    const float keep = up ? v[i + H] : v[i];
+    v[i] = keep + __shfl_xor(send, H, 64);
+  }
+}
+// forward: lane = 4 consecutive output pixels, wave = 16 output channels of the
+// 64-channel tile -> each broadcast weight read (4 x ds_read_b128) feeds 64 FMAs
+__global__ void __launch_bounds__(256) conv_small_fwd_kernel(SmallConvArgs a) {
+  constexpr int TC = 8;                          // taps gathered per pass
+  extern __shared__ float smem[];
+  float* wl = smem;                              // [K][64] fp32
+  const int K = a.K, Kp = (K + TC - 1) / TC * TC;
+  int* taps = reinterpret_cast<int*>(smem + K * 64);   // [Kp]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int co0 = blockIdx.y * 64;
+  for (int i = tid; i < K * 64; i += 256) {
+    const int k = i >> 6, c = i & 63;
+    wl[i] = bf2f(a.w[(long long)(co0 + c) * K + k]);
+  }
+  for (int k = tid; k < Kp; k += 256) taps[k] = tap_of(a, k);
+  __syncthreads();
+
+  const int pbase = blockIdx.x * 256 + lane * 4;
+  int pb[4], ph[4], pw[4];
+  bool pv_ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pv_ok[i] = pbase + i < a.P;
+    const int3 d = decode_pixel(a, pv_ok[i] ? pbase + i : 0);
+    pb[i] = d.x;
+    ph[i] = d.y;
+    pw[i] = d.z;
+  }
+  float acc[4][16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc[i][c] = 0.f;
+  const float* wcol = wl + wid * 16;
+  const __amdgpu_buffer_rsrc_t rs = image_rsrc(a);
+  for (int k0 = 0; k0 < K; k0 += TC) {
+    float pv[4][TC];
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const int tap = taps[k0 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pv[i][j] = load_tap(a, rs, pv_ok[i] ? tap : -1, pb[i], ph[i], pw[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      if (k0 + j < K) {
+        const float4* wr = reinterpret_cast<const float4*>(wcol + (k0 + j) * 64);
+        float wv[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 w4 = wr[q];
+          wv[4 * q] = w4.x; wv[4 * q + 1] = w4.y; wv[4 * q + 2] = w4.z; wv[4 * q + 3] = w4.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int c = 0; c < 16; ++c) acc[i][c] += pv[i][j] * wv[c];
+      }
+    }
+  }
+  // round to the stored bf16 values (BN statistics describe what is stored)
+  float s1[16], s2[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) { s1[c] = 0.f; s2[c] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u32 packed[8];
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) {
+      const u16 lo = f2bf(acc[i][c]), hi = f2bf(acc[i][c + 1]);
+      packed[c / 2] = (u32)lo | ((u32)hi << 16);
+      if (pv_ok[i]) {
+        const float flo = bf2f(lo), fhi = bf2f(hi);
+        s1[c] += flo; s2[c] += flo * flo;
+        s1[c + 1] += fhi; s2[c + 1] += fhi * fhi;
+      }
+    }
+    if (pv_ok[i]) {
+      uint4* dst = reinterpret_cast<uint4*>(a.y + (long long)(pbase + i) * a.CO + co0 + wid * 16);
+      dst[0] = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+      dst[1] = make_uint4(packed[4], packed[5], packed[6], packed[7]);
+    }
+  }
+  if (a.part == nullptr) return;
+  // 16 channels x 64 lanes: halve over lane bits 3..0 (lane ends up owning
+  // channel lane & 15), then fold lane bits 4, 5
+  halve<8>(s1, lane); halve<4>(s1, lane); halve<2>(s1, lane); halve<1>(s1, lane);
+  halve<8>(s2, lane); halve<4>(s2, lane); halve<2>(s2, lane); halve<1>(s2, lane);
+  float t1 = s1[0], t2 = s2[0];
+  t1 += __shfl_xor(t1, 16, 64); t2 += __shfl_xor(t2, 16, 64);
+  t1 += __shfl_xor(t1, 32, 64); t2 += __shfl_xor(t2, 32, 64);
+  if (lane < 16) {
+    const int c = co0 + wid * 16 + lane;
+    a.part[(long long)blockIdx.x * a.CO + c] = t1;
+    a.part[(long long)(gridDim.x + blockIdx.x) * a.CO + c] = t2;
+  }
+}
+
+// wgrad: blockIdx.z = 32-tap pass.  Lane = (co quad cq = lane & 15, tap octet
+// ko = lane >> 4) -> 4 x 8 outputs per lane, 32 FMAs per (float4 dY + 2 float4
+// patch) LDS reads; the 4 waves split each 64-pixel slab's rows and are summed
+// through LDS.  Each block stores its [64][32] tile to ws[blockIdx.x] (plain
+// stores); conv_small_wgrad_reduce then adds the G tiles into dW -- every
+// block hitting the same 1.7k addresses with fp32 atomics serialises at the
+// memory-side atomic units.
+__global__ void __launch_bounds__(256) conv_small_wgrad_kernel(SmallConvArgs a) {
+  constexpr int SLAB = 64, KT = 32;
+  // [SLAB][64] dY slab + [SLAB][KT] patch slab; afterwards the same 24 KiB
+  // hold waves 1..3's [64][KT] tiles for the cross-wave sum
+  __shared__ __attribute__((aligned(16))) float smem[SLAB * 64 + SLAB * KT];
+  static_assert(3 * 64 * KT == SLAB * 64 + SLAB * KT, "reduction tile reuses the slabs");
+  __shared__ int taps[KT];
+  __shared__ int4 rows[SLAB];
+  float* dyl = smem;
+  float* pl = smem + SLAB * 64;
+  float* red = smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int co0 = blockIdx.y * 64, k0 = blockIdx.z * KT;
+  const int cq = lane & 15, ko = lane >> 4;
+  if (tid < KT) taps[tid] = tap_of(a, k0 + tid);
+  const __amdgpu_buffer_rsrc_t rs = image_rsrc(a);
+  const int p_begin = blockIdx.x * a.chunk;
+  const int p_end = min((int)a.P, p_begin + a.chunk);
+  float acc[4][8];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+  for (int p0 = p_begin; p0 < p_end; p0 += SLAB) {
+    __syncthreads();   // previous slab consumed
+    if (tid < SLAB) {
+      const int p = p0 + tid;
+      const int3 d = decode_pixel(a, p < p_end ? p : p_begin);
+      rows[tid] = make_int4(d.x, d.y, d.z, p < p_end);
+    }
+    {
+      const int r = tid >> 2, c = (tid & 3) * 16;
+      const int p = p0 + r;
+      float4* d = reinterpret_cast<float4*>(dyl + r * 64 + c);
+      if (p < p_end) {
+        const uint4* src = reinterpret_cast<const uint4*>(a.dy + (long long)p * a.CO + co0 + c);
+        const uint4 v0 = src[0], v1 = src[1];
+        const u32 u[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          d[q] = make_float4(bf2f((u16)(u[2 * q] & 0xffff)), bf2f((u16)(u[2 * q] >> 16)),
+                             bf2f((u16)(u[2 * q + 1] & 0xffff)), bf2f((u16)(u[2 * q + 1] >> 16)));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    __syncthreads();   // row table visible
+    // all gathers first, then the LDS stores (a store between them would
+    // order every later table read behind it and serialise the loads)
+    float g[SLAB * KT / 256];
+#pragma unroll
+    for (int it = 0; it < SLAB * KT / 256; ++it) {
+      const int i = it * 256 + tid;
+      const int r = i / KT, k = i % KT;
+      const int4 e = rows[r];
+      g[it] = load_tap(a, rs, e.w ? taps[k] : -1, e.x, e.y, e.z);
+    }
+#pragma unroll
+    for (int it = 0; it < SLAB * KT / 256; ++it) pl[it * 256 + tid] = g[it];
+    __syncthreads();
+#pragma unroll 4
+    for (int rr = 0; rr < SLAB / 4; ++rr) {
+      const int r = rr * 4 + wid;
+      const float4 d = *reinterpret_cast<const float4*>(dyl + r * 64 + cq * 4);
+      const float4 v0 = *reinterpret_cast<const float4*>(pl + r * KT + ko * 8);
+      const float4 v1 = *reinterpret_cast<const float4*>(pl + r * KT + ko * 8 + 4);
+      const float dv[4] = {d.x, d.y, d.z, d.w};
+      const float pv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[c][j] += dv[c] * pv[j];
+    }
+  }
+  // sum the 4 waves: waves 1..3 park their tiles, wave 0 adds and stores
+  __syncthreads();
+  if (wid > 0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[((wid - 1) * 64 + cq * 4 + c) * KT + ko * 8 + j] = acc[c][j];
+  }
+  __syncthreads();
+  if (wid == 0) {
+    float* tile = a.ws + (long long)blockIdx.x * a.CO * a.K;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int co = co0 + cq * 4 + c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kl = ko * 8 + j;
+        float v = acc[c][j];
+#pragma unroll
+        for (int w = 0; w < 3; ++w) v += red[(w * 64 + cq * 4 + c) * KT + kl];
+        if (k0 + kl < a.K) tile[(long long)co * a.K + k0 + kl] = v;
+      }
+    }
+  }
+}
+
+// dw[i] += sum_g ws[g][i]: one wave per 64 consecutive outputs, lanes stride G
+__global__ void __launch_bounds__(256) conv_small_wgrad_reduce(const float* __restrict__ ws,
+                                                               float* __restrict__ dw, int n,
+                                                               int G) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;   // 4 waves split G
+  __shared__ float red[4][64];
+  float v = 0.f;
+  if (i < n)
+    for (int g = part; g < G; g += 4) v += ws[(long long)g * n + i];
+  red[part][threadIdx.x & 63] = v;
+  __syncthreads();
+  if (threadIdx.x < 64 && i < n) dw[i] += red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+static SmallConvArgs small_args(const u16* x, int xbytes, int sb, int sh, int sw, int sc, int B, int H, int W, int CI, int OH, int OW, int CO,
+                                int R, int S, int stride, int pad) {
+  SmallConvArgs a{};
+  a.x = x;
+  a.xbytes = xbytes;
+  a.sb = sb; a.sh = sh; a.sw = sw; a.sc = sc;
+  a.B = B; a.H = H; a.W = W; a.CI = CI; a.OH = OH; a.OW = OW; a.CO = CO;
+  a.R = R; a.S = S; a.stride = stride; a.pad = pad; a.K = R * S * CI;
+  a.P = (long long)B * OH * OW;
+  return a;
+}
+
+int conv_small_max_k() { return 384; }   // forward weight tile [K][64] fp32 must fit LDS
+
+long long conv_small_fwd_blocks(long long P) { return (P + 255) / 256; }
+
+void launch_conv_small_fwd(const u16* x, int xbytes, int sb, int sh, int sw, int sc,
+                           const u16* w, u16* y, float* part, int B, int H, int W, int CI, int OH,
+                           int OW, int CO, int R, int S, int stride, int pad, hipStream_t s) {
+  SmallConvArgs a = small_args(x, xbytes, sb, sh, sw, sc, B, H, W, CI, OH, OW, CO, R, S, stride, pad);
+  a.w = w;
+  a.y = y;
+  a.part = part;
+  const int Kp = (a.K + 7) / 8 * 8;
+  const size_t lds = (size_t)a.K * 64 * 4 + (size_t)Kp * 4;
+  const dim3 grid((unsigned)conv_small_fwd_blocks(a.P), (unsigned)(CO / 64));
+  hipLaunchKernelGGL(conv_small_fwd_kernel, grid, dim3(256), lds, s, a);
+}
+
+int conv_small_wgrad_blocks(long long P, int CO, int R, int S, int CI) {
+  (void)CO; (void)R; (void)S; (void)CI;
+  // one pixel chunk per CU; whole 64-pixel slabs
+  long long chunk = (P + 255) / 256;
+  chunk = (chunk + 63) / 64 * 64;
+  if (chunk < 256) chunk = 256;
+  return (int)((P + chunk - 1) / chunk);
+}
+
+void launch_conv_small_wgrad(const u16* dy, const u16* x, int xbytes, int sb, int sh, int sw, int sc,
+                             float* dw, float* ws, int B, int H, int W, int CI, int OH, int OW,
+                             int CO, int R, int S, int stride, int pad, hipStream_t s) {
+  SmallConvArgs a = small_args(x, xbytes, sb, sh, sw, sc, B, H, W, CI, OH, OW, CO, R, S, stride, pad);
+  a.dy = dy;
+  a.dw = dw;
+  a.ws = ws;
+  const int G = conv_small_wgrad_blocks(a.P, CO, R, S, CI);
+  a.chunk = (int)((a.P + G - 1) / G);
+  a.chunk = (a.chunk + 63) / 64 * 64;
+  const dim3 grid((unsigned)G, (unsigned)(CO / 64), (unsigned)((a.K + 31) / 32));
+  hipLaunchKernelGGL(conv_small_wgrad_kernel, grid, dim3(256), 0, s, a);
+  const int n = CO * a.K;
+  hipLaunchKernelGGL(conv_small_wgrad_reduce, dim3((n + 63) / 64), dim3(256), 0, s, ws, dw, n, G);
+}
+
+}  // namespace dmp

@@ -43,9 +43,14 @@ __device__ __forceinline__ f32x4 mfma16w(const bf16x8& a, const bf16x8& b, f32x4
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
+// LDS DMA issued from inline asm on purpose: the compiler models the builtin as
+// an LDS store it cannot disambiguate from the ring buffer being read, and
+// inserts s_waitcnt vmcnt(0) in front of the very next ds_read -- serialising
+// every stage's DMA with the MFMA work.  Completion is tracked by hand
+// (wait_vm below), which is the whole point of the multi-stage ring.
 __device__ __forceinline__ void glds16w(const u16* src, u16* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base,
-                                   16, 0, 0);
+  const unsigned m0 = (unsigned)(size_t)(__attribute__((address_space(3))) void*)lds_wave_base;
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(m0));
 }
 
 // wait until at most N vector-memory ops (our DMAs) of this wave are outstanding,

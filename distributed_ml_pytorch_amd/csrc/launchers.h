@@ -68,6 +68,18 @@ void launch_conv_weight_transpose(const uint16_t* w, uint16_t* wt, int CO, int R
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int B, int H, int W,
                        int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s);
+
+// conv_small.hip: few-input-channel (stem) convolutions, VALU
+int conv_small_max_k();
+long long conv_small_fwd_blocks(long long P);
+void launch_conv_small_fwd(const uint16_t* x, int xbytes, int sb, int sh, int sw, int sc, const uint16_t* w,
+                           uint16_t* y, float* part, int B, int H, int W, int CI, int OH, int OW,
+                           int CO, int R, int S, int stride, int pad, hipStream_t s);
+int conv_small_wgrad_blocks(long long P, int CO, int R, int S, int CI);
+// ws: scratch of conv_small_wgrad_blocks(...) * CO * R*S*CI floats
+void launch_conv_small_wgrad(const uint16_t* dy, const uint16_t* x, int xbytes, int sb, int sh, int sw, int sc,
+                             float* dw, float* ws, int B, int H, int W, int CI, int OH, int OW,
+                             int CO, int R, int S, int stride, int pad, hipStream_t s);
 }  // namespace dmp
 
 namespace dmp {

@@ -10,6 +10,11 @@ also emits per-block channel sums, so the BN forward skips its statistics
 pass over the activation.  Tile configurations are chosen per shape by
 timing them on first use (:mod:`.tuner`).
 
+Few-input-channel convolutions (CIFAR-style stems: ``R*S*CI <= 32``,
+``CO % 64 == 0``, input not requiring grad) run on the VALU kernels of
+``csrc/conv_small.hip`` with the same fused BN-statistics epilogue and direct
+fp32 arena weight-gradient accumulation.
+
 Everything else goes to ``F.conv2d`` (MIOpen) in channels_last.
 """
 from __future__ import annotations
@@ -23,6 +28,7 @@ from .tuner import TUNER
 
 _NATIVE_ENABLED = True
 _CONFIGS = None
+_SMALL_MAX_K = 32
 
 
 def set_native_conv(enabled: bool):
@@ -132,6 +138,58 @@ class _NativeConv(Function):
         return dx, None, gw, None, None, None
 
 
+class _SmallConv(Function):
+    """Stem conv: forward + weight gradient only (the input is data)."""
+
+    @staticmethod
+    def forward(ctx, x, w16, master, stride, pad, want_stats):
+        ctx.set_materialize_grads(False)
+        y, part, _ = native().conv_small_fwd(x, w16, stride, pad, want_stats)
+        ctx.save_for_backward(x)
+        ctx.master = master
+        ctx.geom = (stride, pad)
+        if want_stats:
+            ctx.mark_non_differentiable(part)
+            return y, part
+        return y, None
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        if dy is None:
+            return None, None, None, None, None, None
+        (x,) = ctx.saved_tensors
+        stride, pad = ctx.geom
+        master = ctx.master
+        gw = None
+        if master is not None and master.requires_grad:
+            g = master.grad if getattr(master, "_dmp_arena", False) else None
+            if g is not None and g.is_contiguous(memory_format=torch.channels_last):
+                native().conv_small_wgrad(dy, x, g, stride, pad)
+                cb = getattr(master, "_dmp_grad_ready", None)
+                if cb is not None:
+                    cb(master)
+            else:
+                gw = torch.empty(tuple(master.shape), dtype=torch.float32, device=x.device,
+                                 memory_format=torch.channels_last).zero_()
+                native().conv_small_wgrad(dy, x, gw, stride, pad)
+                gw = gw.to(master.dtype)
+        return None, None, gw, None, None, None
+
+
+def small_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
+    if not (_NATIVE_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+        return False
+    if x.requires_grad or groups != 1 or _pair(dilation) != (1, 1):
+        return False
+    st, pd = _pair(stride), _pair(padding)
+    if st[0] != st[1] or pd[0] != pd[1] or not isinstance(pd[0], int):
+        return False
+    co, ci, r, s = weight.shape
+    # VALU kernels: a win over MIOpen only while K = R*S*CI is tiny (CIFAR-style
+    # 3x3x3 stems); 7x7 / 11x11 stems stay on MIOpen's MFMA path
+    return co % 64 == 0 and r * s * ci <= _SMALL_MAX_K
+
+
 def native_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
     if not (_NATIVE_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
         return False
@@ -156,6 +214,17 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
                     memory_format=torch.channels_last)
             y, part = _NativeConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
                                         bool(want_stats))
+            if part is not None:
+                y._dmp_bn_part = part
+            return y
+        if master is not None and b is None and small_conv_supported(
+                x, master, stride, padding, dilation, groups):
+            w16 = getattr(master, "_dmp_w16", None)
+            if w16 is None or not w16.is_contiguous(memory_format=torch.channels_last):
+                w16 = master.detach().to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last)
+            y, part = _SmallConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
+                                       bool(want_stats))
             if part is not None:
                 y._dmp_bn_part = part
             return y

@@ -12,7 +12,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import functional as DF
-from .conv import conv2d as _conv2d, native_conv_supported
+from .conv import conv2d as _conv2d, native_conv_supported, small_conv_supported
+from .linear import arena_linear_ok, linear as _arena_linear
 
 
 class Conv2d(nn.Conv2d):
@@ -26,8 +27,10 @@ class Conv2d(nn.Conv2d):
 
     def forward(self, x):
         if (x.is_cuda and self.bias is None
-                and native_conv_supported(x, self.weight, self.stride, self.padding,
-                                          self.dilation, self.groups)):
+                and (native_conv_supported(x, self.weight, self.stride, self.padding,
+                                           self.dilation, self.groups)
+                     or small_conv_supported(x, self.weight, self.stride, self.padding,
+                                             self.dilation, self.groups))):
             return _conv2d(x, None, None, self.stride, self.padding, self.dilation, self.groups,
                            master=self.weight,
                            want_stats=self.emit_bn_stats and self.training)
@@ -38,6 +41,8 @@ class Conv2d(nn.Conv2d):
 
 class Linear(nn.Linear):
     def forward(self, x):
+        if arena_linear_ok(x, self.weight, self.bias):
+            return _arena_linear(x, self.weight, self.bias)
         w = DF.compute_weight(self.weight, x.dtype)
         b = DF.compute_weight(self.bias, x.dtype)
         return F.linear(x, w, b)

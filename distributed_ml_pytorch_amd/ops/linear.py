@@ -1,0 +1,77 @@
+"""Fully-connected layer with arena-direct fp32 weight gradients.
+
+Forward and data gradient are plain bf16 GEMMs (hipBLASLt through
+``F.linear`` / ``matmul``) on the arena's bf16 weight shadow, so no per-step
+cast.  The weight gradient is ONE bf16 x bf16 -> fp32 GEMM that accumulates
+straight into the fp32 arena gradient view (``addmm`` with an fp32
+``out_dtype``, ``beta = 1``): no bf16 weight-gradient tensor, no mixed-dtype
+add kernel, no AccumulateGrad.  The bias gradient is an fp32 column sum added
+in place.  Both fire the parameter's grad-ready hook (bucketed all-reduce in
+sync DP) as soon as they land.
+
+Parity: the reference's ``nn.Linear`` layers (/root/reference/example/models.py
+LeNet/AlexNet/MLP heads) in fp32; here bf16 compute with fp32 master weights.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from .functional import _notify
+
+
+def _arena_grad(p):
+    if p is None or not p.requires_grad or not getattr(p, "_dmp_arena", False):
+        return None
+    g = p.grad
+    return g if g is not None and g.is_contiguous() else None
+
+
+class _ArenaLinear(Function):
+    @staticmethod
+    def forward(ctx, x, w16, b16, w, b):
+        ctx.save_for_backward(x, w16)
+        ctx.params = (w, b)
+        return F.linear(x, w16, b16)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w16 = ctx.saved_tensors
+        w, b = ctx.params
+        K, N = x.shape[-1], dy.shape[-1]
+        dy2 = dy.reshape(-1, N)
+        x2 = x.reshape(-1, K)
+        dx = (dy2 @ w16).view(x.shape) if ctx.needs_input_grad[0] else None
+        gw = gb = None
+        g = _arena_grad(w)
+        if g is not None:
+            torch.ops.aten.addmm.dtype_out(g, dy2.t(), x2, torch.float32, out=g)
+            _notify(w)
+        elif w is not None and w.requires_grad:
+            gw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).to(w.dtype)
+        if b is not None and b.requires_grad:
+            col = dy2.sum(0, dtype=torch.float32)
+            g = _arena_grad(b)
+            if g is not None:
+                g.add_(col)
+                _notify(b)
+            else:
+                gb = col.to(b.dtype)
+        return dx, None, None, gw, gb
+
+
+def arena_linear_ok(x, w, b) -> bool:
+    """The weight (and bias) live in an arena with a bf16 shadow matching ``x``."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and torch.is_grad_enabled()):
+        return False
+    w16 = getattr(w, "_dmp_w16", None)
+    if w16 is None or w16.dtype != x.dtype or not w16.is_contiguous():
+        return False
+    return b is None or getattr(b, "_dmp_w16", None) is not None
+
+
+def linear(x, w, b):
+    w16 = w._dmp_w16
+    b16 = b._dmp_w16 if b is not None else None
+    return _ArenaLinear.apply(x, w16, b16, w, b)

@@ -25,7 +25,8 @@ class KernelTuner:
         self.timings: dict[tuple, dict] = {}
         self.enabled = os.environ.get("DMP_CONV_TUNE", "1") != "0"
         self.path = os.environ.get("DMP_CONV_TUNE_CACHE")
-        self.reps = int(os.environ.get("DMP_CONV_TUNE_REPS", "3"))
+        self.reps = int(os.environ.get("DMP_CONV_TUNE_REPS", "5"))
+        self.rounds = int(os.environ.get("DMP_CONV_TUNE_ROUNDS", "2"))
         if self.path and os.path.exists(self.path):
             try:
                 with open(self.path) as f:
@@ -43,17 +44,22 @@ class KernelTuner:
         with _lock:
             if key in self.cache:
                 return self.cache[key]
-            times = {}
+            # every candidate is warmed once, then timed in `rounds` interleaved
+            # passes (min over passes): one cold or clock-ramping pass must not
+            # decide the pick
             for c in candidates:
-                runner(c)                       # first touch / warm caches
-                a = torch.cuda.Event(enable_timing=True)
-                b = torch.cuda.Event(enable_timing=True)
-                a.record()
-                for _ in range(self.reps):
-                    runner(c)
-                b.record()
-                b.synchronize()
-                times[c] = a.elapsed_time(b) / self.reps
+                runner(c)
+            times = {c: float("inf") for c in candidates}
+            for _ in range(self.rounds):
+                for c in candidates:
+                    a = torch.cuda.Event(enable_timing=True)
+                    b = torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    for _ in range(self.reps):
+                        runner(c)
+                    b.record()
+                    b.synchronize()
+                    times[c] = min(times[c], a.elapsed_time(b) / self.reps)
             best = min(times, key=times.get)
             self.cache[key] = best
             self.timings[key] = times

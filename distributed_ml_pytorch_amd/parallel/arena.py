@@ -125,13 +125,13 @@ class FlatArena:
             rows = []
             self._wt_index = {}
             for s, q in zip(self.slots, self.params):
-                if len(s.shape) == 4:
+                if len(s.shape) == 4 and s.shape[0] % 64 == 0 and s.shape[1] % 64 == 0:
                     co, ci, r, k = s.shape
                     self._wt_index[id(q)] = s
                     rows.append([s.offset, co, r * k, ci])
                     self._wt_max = max(self._wt_max, s.numel)
             self._wt = torch.empty_like(self.w16)
-            self._wt_table = torch.tensor(rows, dtype=torch.int64, device=self.device)
+            self._wt_table = torch.tensor(rows, dtype=torch.int64).reshape(-1, 4).to(self.device)
         s = self._wt_index.get(id(p))
         if s is None:
             return None

@@ -30,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="256,64,32,32,64,3,1,1")
     ap.add_argument("--repeat", type=int, default=1, help="launches per timed region")
+    ap.add_argument("--wgrad-only", action="store_true")
     a = ap.parse_args()
     B, CI, H, W, CO, k, st, pd = map(int, a.shape.split(","))
     from distributed_ml_pytorch_amd.ops._ext import native
@@ -42,7 +43,7 @@ def main():
     dw = torch.zeros(CO, CI, k, k, device="cuda").contiguous(memory_format=CL)
     fl = 2.0 * B * OH * OH * CO * CI * k * k
     print(f"shape {a.shape}  GFLOP {fl / 1e9:.2f}")
-    for c in nat.conv_configs():
+    for c in ([] if a.wgrad_only else nat.conv_configs()):
         cid = c[0]
         f1 = t(lambda: nat.conv_fwd(x, w, st, pd, True, cid))
         f0 = t(lambda: nat.conv_fwd(x, w, st, pd, False, cid))

@@ -120,3 +120,62 @@ def test_unsupported_shapes_fall_back():
     y = conv(x)
     yr = F.conv2d(x.float(), conv.weight.float().to(torch.bfloat16).float(), None, 1, 1)
     assert _rel(y, yr) < 1e-2
+
+
+SMALL_SHAPES = [
+    # B, CI, H, W, CO, k, stride, pad   (stems: CIFAR ResNet, ImageNet ResNet, AlexNet)
+    (8, 3, 32, 32, 64, 3, 1, 1),
+    (2, 3, 40, 36, 64, 7, 2, 3),
+    (2, 3, 67, 67, 64, 11, 4, 2),
+    (3, 1, 28, 28, 128, 5, 1, 2),
+    (5, 3, 9, 11, 64, 3, 1, 1),        # pixel count not a multiple of 256
+]
+
+
+@pytest.mark.parametrize("B,CI,H,W,CO,k,st,pd", SMALL_SHAPES)
+def test_small_conv_fwd_wgrad(B, CI, H, W, CO, k, st, pd):
+    """Few-input-channel (stem) conv kernels vs fp32 PyTorch, both input layouts."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    torch.manual_seed(1)
+    xc = torch.randn(B, CI, H, W, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(CO, CI, k, k, device="cuda") / (CI * k * k) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(xc.float(), wr, None, st, pd)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr.backward(dy.float())
+    for x in (xc.contiguous(memory_format=CL), xc.contiguous()):
+        y, part, G = nat.conv_small_fwd(x, w, st, pd, True)
+        assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
+        assert _rel(y, yr) < 1e-2
+        ps = part.view(2, int(G), CO).sum(1)
+        yf = y.float()
+        torch.testing.assert_close(ps[0], yf.sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+        torch.testing.assert_close(ps[1], (yf * yf).sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+        dw = torch.zeros(CO, CI, k, k, device="cuda").contiguous(memory_format=CL)
+        nat.conv_small_wgrad(dy, x, dw, st, pd)
+        assert _rel(dw, wr.grad) < 1e-2
+        nat.conv_small_wgrad(dy, x, dw, st, pd)
+        assert _rel(dw, 2 * wr.grad) < 1e-2
+
+
+def test_weight_transpose_batched():
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    shapes = [(64, 64, 3, 3), (128, 64, 1, 1), (512, 256, 3, 3), (64, 128, 3, 3)]
+    offs, rows, off = [], [], 0
+    for s in shapes:
+        offs.append(off)
+        rows.append([off, s[0], s[2] * s[3], s[1]])
+        off += s[0] * s[1] * s[2] * s[3] + 64
+    src = torch.randn(off, device="cuda").to(torch.bfloat16)
+    dst = torch.zeros_like(src)
+    table = torch.tensor(rows, dtype=torch.int64, device="cuda")
+    native().conv_weight_transpose_batched(src, dst, table, max(s[0] * s[1] * s[2] * s[3] for s in shapes))
+    for o, (co, ci, r, k) in zip(offs, shapes):
+        n = co * ci * r * k
+        w = src[o:o + n].view(co, r, k, ci)
+        wt = dst[o:o + n].view(ci, r, k, co)
+        assert torch.equal(wt, w.permute(3, 1, 2, 0))
