@@ -319,9 +319,11 @@ ConvGeom conv_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad
   TORCH_CHECK(g.OH > 0 && g.OW > 0, "conv: empty output");
   TORCH_CHECK(g.CI % 64 == 0 && g.CO % 64 == 0,
               "native conv needs CI % 64 == 0 and CO % 64 == 0 (got ", g.CI, ", ", g.CO, ")");
-  TORCH_CHECK((long long)g.B * g.H * g.W * g.CI < (1LL << 31) &&
-                  (long long)g.B * g.OH * g.OW * g.CO < (1LL << 31),
-              "native conv: tensor too large for 32-bit pixel indexing");
+  // the kernels address operands with 32-bit byte offsets into buffer descriptors
+  TORCH_CHECK((long long)g.B * g.H * g.W * g.CI < (1LL << 30) &&
+                  (long long)g.B * g.OH * g.OW * g.CO < (1LL << 30) &&
+                  (long long)g.CO * g.CI * g.R * g.S < (1LL << 30),
+              "native conv: tensor too large for 32-bit byte offsets");
   return g;
 }
 
@@ -490,9 +492,9 @@ void conv_small_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pa
 std::vector<std::vector<int64_t>> conv_configs() {
   std::vector<std::vector<int64_t>> out;
   for (int c = 0; c < dmp::conv_num_configs(); ++c) {
-    int info[4];
+    int info[5];
     dmp::conv_config_info(c, info);
-    out.push_back({c, info[0], info[1], info[2], info[3]});
+    out.push_back({c, info[0], info[1], info[2], info[3], info[4]});
   }
   return out;
 }

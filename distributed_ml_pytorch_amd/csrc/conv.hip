@@ -37,8 +37,6 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));
 
-// 16 zero bytes per lane-chunk: the source of every padded / out-of-range fetch.
-__device__ __attribute__((aligned(256))) u16 g_conv_zero[128];
 
 struct ConvArgs {
   const u16* x;     // gathered operand NHWC [B][GH][GW][CI]   (fwd: X, dgrad: dY)
@@ -54,9 +52,26 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
-__device__ __forceinline__ void glds16(const u16* src, u16* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base,
-                                   16, 0, 0);
+// LDS DMA (buffer_load_dwordx4 ... lds, 16 B per lane into a lane-linear 1 KiB
+// wave slice at m0) from inline asm: with the builtin the compiler cannot tell
+// the ring slot being filled from the one being read and puts s_waitcnt
+// vmcnt(0) before the next ds_read, serialising the pipeline.  Completion is
+// tracked by hand (wait_vm), counted per wave.  Offsets >= the descriptor's
+// num_records read as zeros: that is how padding taps are fetched.
+constexpr unsigned kOOB = 0x80000000u;
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t rs, unsigned voff,
+                                       u16* lds_wave_base) {
+  const unsigned m0 = (unsigned)(size_t)(__attribute__((address_space(3))) void*)lds_wave_base;
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+               "{m0}"(m0));
+}
+
+// wait until at most N of this wave's vector-memory ops are outstanding (and
+// all of its LDS ops have completed)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0070);
 }
 
 // 16-byte chunk swizzle (an involution) for a row-major [rows][BK] bf16 tile.
@@ -72,7 +87,10 @@ __device__ __forceinline__ int swz(int row, int c) {
 }
 
 // MODE 0: forward conv.  MODE 1: data gradient, one parity class per blockIdx.z.
-template <int BM, int BN, int BK, int WM, int WN, int MODE, bool STATS>
+// NS-stage LDS-DMA ring: NS-1 k-tiles in flight while one is consumed.  (A
+// register-staged variant -- global_load into VGPRs, ds_write_b128 -- measured
+// 2-4x slower on every ResNet-18 shape: profiles/igemm_ablate_r1.txt.)
+template <int BM, int BN, int BK, int WM, int WN, int MODE, bool STATS, int NS>
 __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN;
   constexpr int CPR = BK / 8;                 // 16-B chunks per tile row
@@ -85,7 +103,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   constexpr int TN = BN / WN / 16;
   constexpr int A_EL = BM * BK, B_EL = B_INS * RPI * BK;
   constexpr int STAGE = A_EL + B_EL;
-  __shared__ __attribute__((aligned(16))) u16 lds[2 * STAGE];
+  // DMAs every wave has issued per stage (a wave may issue more; waiting on
+  // the minimum is conservative for it)
+  constexpr int INS_MIN = A_INS / NW + B_INS / NW;
+  static_assert(NS >= 2 && (NS - 2) * INS_MIN < 64, "pipeline depth");
+  __shared__ __attribute__((aligned(16))) u16 lds[NS * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -110,36 +132,42 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
     if (m0 >= Mc) return;
   }
 
-  // per-lane gather state for the A tile: lane's row in each glds instruction
-  int a_pix[A_PW], a_h[A_PW], a_w[A_PW], a_c[A_PW];
+  // per-lane gather state for the A tile (lane's row in each DMA piece), all
+  // 32-bit: byte offsets into the operand buffers; a padded / out-of-range
+  // fetch gets an offset past the descriptor's bound and the buffer unit
+  // returns zeros (no branch, no zero page, no 64-bit address math per piece)
+  int a_h[A_PW], a_w[A_PW];
+  unsigned a_base[A_PW];
   bool a_ok[A_PW];
 #pragma unroll
   for (int j = 0; j < A_PW; ++j) {
     const int ins = wid + j * NW;
     const int row = ins * RPI + lane / CPR;
-    a_c[j] = swz<BK>(row, lane % CPR) * 8;      // logical chunk this lane fetches
-    const long long m = m0 + row;
-    a_ok[j] = ins < A_INS && m < Mc;
-    const long long mm = a_ok[j] ? m : 0;
-    const int ow = (int)(mm % RW);
-    const long long t = mm / RW;
-    const int oh = (int)(t % RH);
-    const int b = (int)(t / RH);
-    a_pix[j] = b * GH * GW;
+    const int a_c = swz<BK>(row, lane % CPR) * 8;      // logical chunk this lane fetches
+    const int m = (int)m0 + row;
+    a_ok[j] = ins < A_INS && m < (int)Mc;
+    const int mm = a_ok[j] ? m : 0;
+    const int ow = mm % RW, t = mm / RW;
+    const int oh = t % RH, b = t / RH;
     if (MODE == 0) { a_h[j] = oh * st - a.pad; a_w[j] = ow * st - a.pad; }
     else           { a_h[j] = oh;              a_w[j] = ow; }
+    // may wrap for a padded (negative) origin; only used when the tap is in range
+    a_base[j] = 2u * (unsigned)(((b * GH + a_h[j]) * GW + a_w[j]) * CI + a_c);
   }
-  const long long K = (long long)a.R * a.S * CI;
-  const u16* b_src[B_PW];
-  bool b_ok[B_PW];
+  const int K = a.R * a.S * CI;
+  unsigned b_base[B_PW];
 #pragma unroll
   for (int j = 0; j < B_PW; ++j) {
     const int ins = wid + j * NW;
     const int row = ins * RPI + lane / CPR;
     const int n = n0 + row;
-    b_ok[j] = ins < B_INS && row < BN && n < a.CO;
-    b_src[j] = a.w + (long long)(b_ok[j] ? n : 0) * K + swz<BK>(row, lane % CPR) * 8;
+    const bool ok = ins < B_INS && row < BN && n < a.CO;
+    b_base[j] = ok ? 2u * (unsigned)(n * K + swz<BK>(row, lane % CPR) * 8) : kOOB;
   }
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, 0, (int)(2LL * a.B * GH * GW * CI), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.w, 0, (int)(2LL * a.CO * K), 0x00020000);
 
   const int kpr = CI / BK;          // k-tiles per tap
   const int KT = nth * ntw * kpr;
@@ -158,25 +186,22 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
     }
     u16* As = lds + buf * STAGE;
     u16* Bs = As + A_EL;
+    const unsigned adelta = 2u * (unsigned)((dh * GW + dw) * CI + cb);   // wave-uniform
 #pragma unroll
     for (int j = 0; j < A_PW; ++j) {
       const int ins = wid + j * NW;
       if (A_INS % NW == 0 || ins < A_INS) {
         const int ih = a_h[j] + dh, iw = a_w[j] + dw;
         const bool ok = a_ok[j] && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
-        const u16* src = ok ? a.x + ((long long)a_pix[j] + ih * GW + iw) * CI + cb + a_c[j]
-                            : g_conv_zero;
-        glds16(src, As + ins * (RPI * BK));
+        bdma16(rsA, ok ? a_base[j] + adelta : kOOB, As + ins * (RPI * BK));
       }
     }
-    const long long woff = (long long)(r * a.S + s) * CI + cb;
+    const unsigned wdelta = 2u * (unsigned)((r * a.S + s) * CI + cb);
 #pragma unroll
     for (int j = 0; j < B_PW; ++j) {
       const int ins = wid + j * NW;
-      if (B_INS % NW == 0 || ins < B_INS) {
-        const u16* src = b_ok[j] ? b_src[j] + woff : g_conv_zero;
-        glds16(src, Bs + ins * (RPI * BK));
-      }
+      if (B_INS % NW == 0 || ins < B_INS)
+        bdma16(rsB, b_base[j] == kOOB ? kOOB : b_base[j] + wdelta, Bs + ins * (RPI * BK));
     }
   };
 
@@ -217,15 +242,23 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   };
 
   if (KT > 0) {
-    stage(0, 0);
-    __syncthreads();   // waits vmcnt(0): the DMA has landed
-    for (int kt = 0; kt < KT; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < KT) stage(cur ^ 1, kt + 1);
-      compute(cur);
-      __syncthreads();
+    {
+#pragma unroll
+      for (int st0 = 0; st0 < NS - 1; ++st0)
+        if (st0 < KT) stage(st0, st0);
+      for (int kt = 0; kt < KT; ++kt) {
+        // k-tile kt landed for this wave (younger tiles may still fly) ...
+        if (kt + NS - 2 < KT) wait_vm<(NS - 2) * INS_MIN>();
+        else wait_vm<0>();
+        // ... and for every wave; everyone is done with tile kt-1's slot
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + NS - 1 < KT) stage((kt + NS - 1) % NS, kt + NS - 1);
+        compute(kt % NS);
+      }
     }
   }
+  __syncthreads();   // all ring reads done before the epilogue reuses LDS
 
   // epilogue: D^T layout -> lane owns channels n..n+3 of output row m
   float s_sum[TN][4], s_sq[TN][4];
@@ -278,7 +311,6 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
         }
       }
     float* red = reinterpret_cast<float*>(lds);   // [WM][BN] sums, then [WM][BN] squares
-    if (KT == 0) __syncthreads();
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -318,29 +350,39 @@ __global__ void __launch_bounds__(256) conv_weight_transpose_kernel(
 }
 
 // ---------------------------------------------------------------- launchers
-// Tile configurations (BM, BN, BK, WM, WN).  Index = the `cfg` id used by the
-// host-side tuner; -1 selects the heuristic default.
-#define DMP_CONV_CONFIGS(X)   \
-  X(0, 256, 64, 64, 4, 1)     \
-  X(1, 256, 64, 32, 4, 2)     \
-  X(2, 128, 64, 64, 2, 2)     \
-  X(3, 128, 64, 32, 2, 2)     \
-  X(4, 64, 64, 64, 2, 2)      \
-  X(5, 64, 64, 32, 2, 2)      \
-  X(6, 256, 128, 64, 2, 2)    \
-  X(7, 256, 128, 32, 4, 2)    \
-  X(8, 128, 128, 64, 2, 2)    \
-  X(9, 128, 128, 32, 2, 4)    \
-  X(10, 64, 128, 64, 1, 4)    \
-  X(11, 128, 64, 32, 4, 2)    \
-  X(12, 256, 64, 64, 4, 2)    \
-  X(13, 128, 128, 64, 2, 4)
+// Tile configurations (BM, BN, BK, WM, WN, NS).  Index = the `cfg` id used by
+// the host-side tuner; -1 selects the heuristic default.
+#define DMP_CONV_CONFIGS(X)      \
+  X(0, 256, 64, 64, 4, 1, 2)     \
+  X(1, 256, 64, 32, 4, 2, 2)     \
+  X(2, 128, 64, 64, 2, 2, 2)     \
+  X(3, 128, 64, 32, 2, 2, 2)     \
+  X(4, 64, 64, 64, 2, 2, 2)      \
+  X(5, 64, 64, 32, 2, 2, 2)      \
+  X(6, 256, 128, 64, 2, 2, 2)    \
+  X(7, 256, 128, 32, 4, 2, 2)    \
+  X(8, 128, 128, 64, 2, 2, 2)    \
+  X(9, 128, 128, 32, 2, 4, 2)    \
+  X(10, 64, 128, 64, 1, 4, 2)    \
+  X(11, 128, 64, 32, 4, 2, 2)    \
+  X(12, 256, 64, 64, 4, 2, 2)    \
+  X(13, 128, 128, 64, 2, 4, 2)   \
+  X(14, 256, 64, 32, 4, 2, 4)    \
+  X(15, 256, 64, 64, 4, 2, 3)    \
+  X(16, 128, 128, 32, 2, 4, 4)   \
+  X(17, 128, 128, 64, 2, 4, 3)   \
+  X(18, 64, 64, 64, 2, 2, 4)     \
+  X(19, 128, 64, 32, 2, 2, 4)    \
+  X(20, 64, 128, 64, 1, 4, 3)    \
+  X(21, 128, 64, 64, 2, 2, 3)    \
+  X(22, 64, 64, 32, 2, 2, 4)     \
+  X(23, 128, 128, 32, 2, 2, 4)
 
-constexpr int kNumConvConfigs = 14;
+constexpr int kNumConvConfigs = 24;
 
 static int config_bm(int cfg) {
   switch (cfg) {
-#define X(id, BM, BN, BK, WM, WN) case id: return BM;
+#define X(id, BM, BN, BK, WM, WN, NS) case id: return BM;
     DMP_CONV_CONFIGS(X)
 #undef X
   }
@@ -351,12 +393,12 @@ int conv_num_configs() { return kNumConvConfigs; }
 
 void conv_config_info(int cfg, int* info) {
   switch (cfg) {
-#define X(id, BM, BN, BK, WM, WN) \
-  case id: info[0] = BM; info[1] = BN; info[2] = BK; info[3] = 64 * WM * WN; return;
+#define X(id, BM, BN, BK, WM, WN, NS) \
+  case id: info[0] = BM; info[1] = BN; info[2] = BK; info[3] = 64 * WM * WN; info[4] = NS; return;
     DMP_CONV_CONFIGS(X)
 #undef X
   }
-  info[0] = info[1] = info[2] = info[3] = 0;
+  info[0] = info[1] = info[2] = info[3] = info[4] = 0;
 }
 
 // heuristic default: widest N tile the channels fill, tallest M tile that
@@ -373,19 +415,19 @@ int conv_default_config(long long M, int CO) {
   return 5;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int MODE, bool STATS>
+template <int BM, int BN, int BK, int WM, int WN, int NS, int MODE, bool STATS>
 static void launch_cfg(const ConvArgs& a, int classes, hipStream_t s) {
   const dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)((a.CO + BN - 1) / BN),
                   (unsigned)classes);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, MODE, STATS>), grid,
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, MODE, STATS, NS>), grid,
                      dim3(64 * WM * WN), 0, s, a);
 }
 
 template <int MODE, bool STATS>
 static void dispatch(const ConvArgs& a, int cfg, int classes, hipStream_t s) {
   switch (cfg) {
-#define X(id, BM, BN, BK, WM, WN) \
-  case id: launch_cfg<BM, BN, BK, WM, WN, MODE, STATS>(a, classes, s); return;
+#define X(id, BM, BN, BK, WM, WN, NS) \
+  case id: launch_cfg<BM, BN, BK, WM, WN, NS, MODE, STATS>(a, classes, s); return;
     DMP_CONV_CONFIGS(X)
 #undef X
   }

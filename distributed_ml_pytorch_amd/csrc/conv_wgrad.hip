@@ -3,8 +3,8 @@
 //   dW[co][k] += sum_p dY[p][co] * X_gather[p][k]     k = (r, s, ci), p = (b, oh, ow)
 //
 // The reduction runs over p, which is the SLOW index of both NHWC operands, so
-// both tiles are staged as [p][*] row-major images (global_load_lds, 16 B per
-// lane, swizzle applied on the source side) and read back transposed with
+// both tiles are staged as [p][*] row-major images (buffer_load ... lds DMA,
+// 16 B per lane, swizzle applied on the source side) and read back transposed with
 // ds_read_b64_tr_b16: a lane receives 8 consecutive p of one column, exactly
 // the v_mfma_f32_16x16x32_bf16 operand layout.  P is split over blocks and each
 // block adds its fp32 tile into the flat fp32 grad arena with atomics (no
@@ -27,7 +27,6 @@ namespace dmp {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
-__device__ __attribute__((aligned(256))) u16 g_wgrad_zero[128];
 
 struct WgradArgs {
   const u16* dy;    // [P][CO]  (P = B*OH*OW)
@@ -43,14 +42,19 @@ __device__ __forceinline__ f32x4 mfma16w(const bf16x8& a, const bf16x8& b, f32x4
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
-// LDS DMA issued from inline asm on purpose: the compiler models the builtin as
-// an LDS store it cannot disambiguate from the ring buffer being read, and
-// inserts s_waitcnt vmcnt(0) in front of the very next ds_read -- serialising
-// every stage's DMA with the MFMA work.  Completion is tracked by hand
-// (wait_vm below), which is the whole point of the multi-stage ring.
-__device__ __forceinline__ void glds16w(const u16* src, u16* lds_wave_base) {
+// LDS DMA (buffer_load_dwordx4 ... lds) issued from inline asm on purpose: the
+// compiler models the builtin as an LDS store it cannot disambiguate from the
+// ring buffer being read, and inserts s_waitcnt vmcnt(0) in front of the very
+// next ds_read -- serialising every stage's DMA with the MFMA work.
+// Completion is tracked by hand (wait_vm below).  32-bit byte offsets into a
+// buffer descriptor; offsets past its bound read zeros (padding taps, rows
+// past the end of P).
+constexpr unsigned kOOBw = 0x80000000u;
+__device__ __forceinline__ void bdma16w(__amdgpu_buffer_rsrc_t rs, unsigned voff,
+                                        u16* lds_wave_base) {
   const unsigned m0 = (unsigned)(size_t)(__attribute__((address_space(3))) void*)lds_wave_base;
-  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(m0));
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+               "{m0}"(m0));
 }
 
 // wait until at most N vector-memory ops (our DMAs) of this wave are outstanding,
@@ -130,28 +134,30 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   // row table for stage `stg`: {pixel base, oh*stride-pad, ow*stride-pad, valid}
   auto fill_rows = [&](int stg) {
     if (tid < BP) {
-      const long long p = p_begin + (long long)stg * BP + tid;
+      const int p = (int)p_begin + stg * BP + tid;
       int4 e = make_int4(0, -(1 << 20), -(1 << 20), 0);
-      if (stg < nsteps && p < p_end) {
-        const int ow = (int)(p % a.OW);
-        const long long t = p / a.OW;
-        const int oh = (int)(t % a.OH);
-        const int b = (int)(t / a.OH);
+      if (stg < nsteps && p < (int)p_end) {
+        const int ow = p % a.OW, t = p / a.OW;
+        const int oh = t % a.OH, b = t / a.OH;
         e = make_int4(b * GH * GW, oh * a.stride - a.pad, ow * a.stride - a.pad, 1);
       }
       rowtab[(stg % NS) * BP + tid] = e;
     }
   };
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.dy, 0, (int)(2 * a.P * a.CO), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, 0, (int)(2LL * a.B * GH * GW * CI), 0x00020000);
   auto stage = [&](int stg) {
     const int buf = stg % NS;
-    const long long pb = p_begin + (long long)stg * BP;
+    const int pb = (int)p_begin + stg * BP;
     u16* As = lds + buf * STAGE;
     u16* Bs = As + A_EL;
 #pragma unroll
     for (int j = 0; j < A_PW; ++j) {
-      const long long p = pb + a_row[j];
-      const u16* src = (stg < nsteps && p < p_end) ? a.dy + p * a.CO + a_col[j] : g_wgrad_zero;
-      glds16w(src, As + (wid + j * NW) * 512);
+      const int p = pb + a_row[j];
+      const bool ok = stg < nsteps && p < (int)p_end;
+      bdma16w(rsA, ok ? 2u * (unsigned)(p * a.CO + a_col[j]) : kOOBw, As + (wid + j * NW) * 512);
     }
     const int4* tb = rowtab + buf * BP;
 #pragma unroll
@@ -159,8 +165,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
       const int4 e = tb[b_row[j]];
       const int ih = e.y + b_r[j], iw = e.z + b_s[j];
       const bool ok = e.w && (unsigned)ih < (unsigned)GH && (unsigned)iw < (unsigned)GW;
-      const u16* src = ok ? a.x + ((long long)e.x + ih * GW + iw) * CI + b_ci[j] : g_wgrad_zero;
-      glds16w(src, Bs + (wid + j * NW) * 512);
+      bdma16w(rsB, ok ? 2u * (unsigned)((e.x + ih * GW + iw) * CI + b_ci[j]) : kOOBw,
+              Bs + (wid + j * NW) * 512);
     }
   };
 

@@ -54,7 +54,7 @@ void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, in
 namespace dmp {
 // conv.hip
 int conv_num_configs();
-void conv_config_info(int cfg, int* info);
+void conv_config_info(int cfg, int* info);   // {BM, BN, BK, threads, stages}
 int conv_default_config(long long M, int CO);
 int conv_fwd_num_mblocks(long long M, int CO, int cfg);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int B, int H,

@@ -43,7 +43,7 @@ def _pair(v):
 def _configs():
     global _CONFIGS
     if _CONFIGS is None:
-        _CONFIGS = [tuple(c) for c in native().conv_configs()]   # (id, BM, BN, BK, threads)
+        _CONFIGS = [tuple(c) for c in native().conv_configs()]   # (id, BM, BN, BK, threads, NS)
     return _CONFIGS
 
 

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--shape", default="256,64,32,32,64,3,1,1")
     ap.add_argument("--repeat", type=int, default=1, help="launches per timed region")
     ap.add_argument("--wgrad-only", action="store_true")
+    ap.add_argument("--no-wgrad", action="store_true")
     a = ap.parse_args()
     B, CI, H, W, CO, k, st, pd = map(int, a.shape.split(","))
     from distributed_ml_pytorch_amd.ops._ext import native
@@ -48,11 +49,11 @@ def main():
         f1 = t(lambda: nat.conv_fwd(x, w, st, pd, True, cid))
         f0 = t(lambda: nat.conv_fwd(x, w, st, pd, False, cid))
         d = t(lambda: nat.conv_dgrad(dy, w, H, W, st, pd, cid))
-        print(f"cfg {cid:2d} {c[1:]}: fwd+stats {f1:.4f} ({fl / f1 / 1e9:6.1f} TF)  fwd {f0:.4f} "
+        print(f"cfg {cid:2d} {tuple(c[1:])}: fwd+stats {f1:.4f} ({fl / f1 / 1e9:6.1f} TF)  fwd {f0:.4f} "
               f"({fl / f0 / 1e9:6.1f})  dgrad {d:.4f} ({fl / d / 1e9:6.1f})")
     from distributed_ml_pytorch_amd.ops.conv import _wgrad_candidates
 
-    for cfg in _wgrad_candidates(CI * k * k):
+    for cfg in ([] if a.no_wgrad else _wgrad_candidates(CI * k * k)):
         ww = t(lambda: nat.conv_wgrad(dy, x, dw, st, pd, cfg))
         print(f"wgrad bnw={64 * (cfg & 3)} bp={32 if cfg & 4 else 64} ns={3 if cfg & 8 else 2} "
               f"chunk={512 * (cfg >> 4)}: {ww:.4f} ({fl / ww / 1e9:6.1f} TF)")
