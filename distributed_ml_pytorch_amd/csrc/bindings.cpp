@@ -38,6 +38,19 @@ T* ptr_or_null(const optional<Tensor>& t) {
   return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
 }
 
+// BatchNorm slot sums [2][kBnSlots][C]: a persistent per-layer buffer (zeroed
+// once, re-zeroed by every finalize) or a fresh zeroed one
+Tensor bn_slots(const optional<Tensor>& slots, int64_t C, const at::TensorOptions& opt) {
+  if (slots.has_value() && slots->defined()) {
+    TORCH_CHECK(slots->is_cuda() && slots->scalar_type() == at::kFloat && slots->is_contiguous() &&
+                    slots->numel() == 2 * dmp::kBnSlots * C,
+                "BN slot buffer must be a contiguous fp32 GPU tensor of 2*", dmp::kBnSlots,
+                "*C elements");
+    return *slots;
+  }
+  return at::zeros({2 * dmp::kBnSlots * C}, opt.dtype(at::kFloat));
+}
+
 // ----------------------------------------------------------------- optimizer
 void asgd_fused_step(Tensor g, Tensor p, optional<Tensor> acc, optional<Tensor> mom,
                      optional<Tensor> w16, double lr, double wd, double momentum,
@@ -170,7 +183,7 @@ void check_nhwc_bf16(const Tensor& x, const char* name) {
 std::vector<Tensor> bn_fwd(Tensor x, optional<Tensor> res, optional<Tensor> gamma,
                            optional<Tensor> beta, optional<Tensor> running_mean,
                            optional<Tensor> running_var, double momentum, double eps,
-                           bool training, bool relu) {
+                           bool training, bool relu, optional<Tensor> slots) {
   check_nhwc_bf16(x, "x");
   const int64_t C = channels_of(x);
   const int64_t M = x.numel() / C;
@@ -190,8 +203,7 @@ std::vector<Tensor> bn_fwd(Tensor x, optional<Tensor> res, optional<Tensor> gamm
   auto y = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
   auto stats = at::empty({4, C}, fopt);
-  const int G = dmp::bn_num_partials(M, (int)C);
-  auto part = at::empty({2 * G * C}, fopt);
+  auto part = bn_slots(slots, C, fopt);
   dmp::launch_bn_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                      res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr,
                      reinterpret_cast<uint16_t*>(y.data_ptr()), ptr_or_null<float>(gamma),
@@ -204,7 +216,7 @@ std::vector<Tensor> bn_fwd(Tensor x, optional<Tensor> res, optional<Tensor> gamm
 
 std::vector<Tensor> bn_bwd(Tensor x, Tensor dy, optional<Tensor> y, optional<Tensor> gamma,
                            Tensor stats, optional<Tensor> dgamma, optional<Tensor> dbeta,
-                           bool relu, bool want_dres) {
+                           bool relu, bool want_dres, optional<Tensor> slots) {
   check_nhwc_bf16(x, "x");
   const int64_t C = channels_of(x);
   const int64_t M = x.numel() / C;
@@ -229,8 +241,7 @@ std::vector<Tensor> bn_bwd(Tensor x, Tensor dy, optional<Tensor> y, optional<Ten
   Tensor dres;
   if (want_dres) dres = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
-  const int G = dmp::bn_num_partials(M, (int)C);
-  auto part = at::empty({2 * G * C}, fopt);
+  auto part = bn_slots(slots, C, fopt);
   auto coef = at::empty({3, C}, fopt);
   dmp::launch_bn_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                      reinterpret_cast<const uint16_t*>(dy.data_ptr()),
@@ -328,7 +339,7 @@ ConvGeom conv_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad
 }
 
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bool want_stats,
-                             int64_t cfg) {
+                             int64_t cfg, optional<Tensor> slots, optional<Tensor> bias) {
   check_nhwc_bf16(x, "x");
   check_gpu(w, "w");
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -336,17 +347,25 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
   auto g = conv_geom(x, w, stride, pad);
   auto y = at::empty({g.B, g.CO, g.OH, g.OW},
                      x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() &&
+                    bias->numel() == g.CO,
+                "conv bias must be a contiguous fp32 [CO] GPU tensor");
+  } else {
+    bias.reset();
+  }
   Tensor part;
   int64_t G = 0;
   if (want_stats) {
-    G = dmp::conv_fwd_num_mblocks((long long)g.B * g.OH * g.OW, g.CO, (int)cfg);
-    part = at::empty({2 * G * g.CO}, x.options().dtype(at::kFloat));
+    G = dmp::kBnSlots;
+    part = bn_slots(slots, g.CO, x.options());
   }
   dmp::launch_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                        reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()),
                        want_stats ? part.data_ptr<float>() : nullptr, g.B, g.H, g.W, g.CI, g.OH,
-                       g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream());
+                       g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream(),
+                       bias ? bias->data_ptr<float>() : nullptr);
   return {y, part, at::scalar_tensor(G, at::kLong)};
 }
 
@@ -443,7 +462,7 @@ SmallGeom small_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t p
 }
 
 std::vector<Tensor> conv_small_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad,
-                                   bool want_stats) {
+                                   bool want_stats, optional<Tensor> slots) {
   check_gpu(w, "w");
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv weight must be bf16 channels_last");
@@ -454,8 +473,8 @@ std::vector<Tensor> conv_small_fwd(Tensor x, Tensor w, int64_t stride, int64_t p
   Tensor part;
   int64_t G = 0;
   if (want_stats) {
-    G = dmp::conv_small_fwd_blocks(P);
-    part = at::empty({2 * G * g.CO}, x.options().dtype(at::kFloat));
+    G = dmp::kBnSlots;
+    part = bn_slots(slots, g.CO, x.options());
   }
   dmp::launch_conv_small_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                              (int)(2 * x.numel()), (int)x.stride(0),
@@ -489,6 +508,71 @@ void conv_small_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pa
                                cur_stream());
 }
 
+// ------------------------------------------------------------------ dropout
+// mode 0: element-wise; 1: per (n, c) plane of an NCHW tensor; 2: per (n, c)
+// of an NHWC (channels_last) tensor.
+std::vector<Tensor> dropout_fwd(Tensor x, double p, int64_t seed, Tensor offset, int64_t mode) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat,
+              "dropout: bf16 or fp32 input");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout: p must be in [0, 1)");
+  TORCH_CHECK(offset.is_cuda() && offset.scalar_type() == at::kLong && offset.numel() >= 1,
+              "dropout: offset must be an int64 GPU tensor");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "dropout: bad mode");
+  long long inner = 1, nmask = x.numel();
+  int C = 1;
+  if (mode != 0) {
+    TORCH_CHECK(x.dim() >= 3, "channel dropout needs [N, C, ...]");
+    C = (int)x.size(1);
+    inner = x.numel() / (x.size(0) * C);
+    nmask = x.size(0) * C;
+    if (mode == 1) {
+      TORCH_CHECK(x.is_contiguous(), "mode 1 needs a contiguous NCHW tensor");
+    } else {
+      TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                  "mode 2 needs a channels_last tensor");
+    }
+  } else {
+    TORCH_CHECK(x.is_contiguous() || x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "dropout: dense input");
+  }
+  auto mask = at::empty({nmask}, x.options().dtype(at::kByte));
+  auto y = at::empty_like(x);
+  const float scale = (float)(1.0 / (1.0 - p));
+  dmp::launch_dropout_mask(mask.data_ptr<uint8_t>(), nmask, (float)p, (unsigned long long)seed,
+                           reinterpret_cast<const long long*>(offset.data_ptr<int64_t>()), cur_stream());
+  if (x.scalar_type() == at::kBFloat16)
+    dmp::launch_dropout_apply_bf16(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                   mask.data_ptr<uint8_t>(), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                   x.numel(), scale, (int)mode, inner, C, cur_stream());
+  else
+    dmp::launch_dropout_apply_f32(x.data_ptr<float>(), mask.data_ptr<uint8_t>(), y.data_ptr<float>(),
+                                  x.numel(), scale, (int)mode, inner, C, cur_stream());
+  return {y, mask};
+}
+
+Tensor dropout_bwd(Tensor dy, Tensor mask, double p, int64_t mode) {
+  check_gpu(dy, "dy");
+  long long inner = 1;
+  int C = 1;
+  if (mode == 2) dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  else if (!(mode == 0 && dy.is_contiguous(at::MemoryFormat::ChannelsLast))) dy = dy.contiguous();
+  if (mode != 0) {
+    C = (int)dy.size(1);
+    inner = dy.numel() / (dy.size(0) * C);
+  }
+  auto dx = at::empty_like(dy);
+  const float scale = (float)(1.0 / (1.0 - p));
+  if (dy.scalar_type() == at::kBFloat16)
+    dmp::launch_dropout_apply_bf16(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                   mask.data_ptr<uint8_t>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                                   dy.numel(), scale, (int)mode, inner, C, cur_stream());
+  else
+    dmp::launch_dropout_apply_f32(dy.data_ptr<float>(), mask.data_ptr<uint8_t>(), dx.data_ptr<float>(),
+                                  dy.numel(), scale, (int)mode, inner, C, cur_stream());
+  return dx;
+}
+
 std::vector<std::vector<int64_t>> conv_configs() {
   std::vector<std::vector<int64_t>> out;
   for (int c = 0; c < dmp::conv_num_configs(); ++c) {
@@ -508,7 +592,9 @@ std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optio
   const int64_t C = channels_of(x);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: bad C");
-  TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() == 2 * G * C, "bad partials");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  G == dmp::kBnSlots && part.numel() == 2 * G * C,
+              "bad BN slot sums");
   if (res) {
     check_nhwc_bf16(*res, "res");
     TORCH_CHECK(res->sizes() == x.sizes(), "res shape mismatch");
@@ -520,7 +606,7 @@ std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optio
                               reinterpret_cast<uint16_t*>(y.data_ptr()), ptr_or_null<float>(gamma),
                               ptr_or_null<float>(beta), ptr_or_null<float>(running_mean),
                               ptr_or_null<float>(running_var), stats.data_ptr<float>(),
-                              part.data_ptr<float>(), (int)G, M, (int)C, (float)momentum,
+                              part.data_ptr<float>(), M, (int)C, (float)momentum,
                               (float)eps, relu, cur_stream());
   return {y, stats};
 }
@@ -530,7 +616,7 @@ std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optio
 PYBIND11_MODULE(_native, m) {
   m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM conv forward (+BN partials)",
         py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
-        py::arg("cfg") = -1);
+        py::arg("cfg") = -1, py::arg("slots") = py::none(), py::arg("bias") = py::none());
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM conv data gradient", py::arg("dy"),
         py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"),
         py::arg("cfg") = -1, py::arg("wt") = py::none());
@@ -542,7 +628,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("conv_configs", &conv_configs, "[(id, BM, BN, BK, threads)] of the compiled conv tiles");
   m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials");
   m.def("conv_small_fwd", &conv_small_fwd, "few-input-channel conv forward (+BN partials)",
-        py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"));
+        py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
+        py::arg("slots") = py::none());
   m.def("conv_small_wgrad", &conv_small_wgrad, "few-input-channel conv weight gradient (fp32 +=)",
         py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"));
   m.doc() = "gfx950 (MI355X) HIP kernels for distributed_ml_pytorch_amd";
@@ -553,8 +640,15 @@ PYBIND11_MODULE(_native, m) {
   m.def("cast_f32_bf16", &cast_f32_bf16, "flat fp32 -> bf16");
   m.def("sumsq", &sumsq, "sum of squares of a flat fp32 buffer");
   m.def("softmax_xent", &softmax_xent, "fused softmax cross entropy fwd+bwd");
-  m.def("bn_fwd", &bn_fwd, "NHWC batchnorm(+residual)(+relu) forward");
-  m.def("bn_bwd", &bn_bwd, "NHWC batchnorm(+residual)(+relu) backward");
+  m.def("bn_fwd", &bn_fwd, "NHWC batchnorm(+residual)(+relu) forward", py::arg("x"),
+        py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("training"),
+        py::arg("relu"), py::arg("slots") = py::none());
+  m.def("bn_bwd", &bn_bwd, "NHWC batchnorm(+residual)(+relu) backward", py::arg("x"),
+        py::arg("dy"), py::arg("y"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"), py::arg("slots") = py::none());
+  m.def("dropout_fwd", &dropout_fwd, "Philox dropout forward -> (y, keep mask)");
+  m.def("dropout_bwd", &dropout_bwd, "dropout backward from the saved keep mask");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pool forward");
   m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC KxK/sK max pool forward");

@@ -4,8 +4,9 @@
 // it is needed by the BASELINE.json models (ResNet-18/50). Layout is [M, C]
 // bf16 with M = N*H*W, every thread owning 8 consecutive channels (16 B).
 //
-// forward  : stats (partial sums per block) -> finalize (mean/invstd, running
-//            stats, folded scale/shift) -> apply  y = relu(x*scale + shift [+ res])
+// forward  : stats (per-block sums added into kBnSlots slot rows) -> finalize
+//            (mean/invstd, running stats, folded scale/shift; re-zeroes the
+//            slots) -> apply  y = relu(x*scale + shift [+ res])
 // backward : reduce (sum dz, sum dz*xhat with dz = dy*[y>0]) -> finalize
 //            (dgamma/dbeta accumulated straight into the fp32 grad arena, folded
 //            dx coefficients) -> apply  dx = A*dz + Cc*x + Bc  [and dres = dz]
@@ -81,15 +82,18 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(
   for (int c = t; c < C; c += 256) {
     float a = 0.f, b = 0.f;
     for (int r = 0; r < rpi; ++r) { a += ls[r * C + c]; b += lq[r * C + c]; }
-    part[(long long)blockIdx.x * C + c] = a;
-    part[(long long)(gridDim.x + blockIdx.x) * C + c] = b;
+    const int slot = blockIdx.x % kBnSlots;
+    atomicAdd(part + (long long)slot * C + c, a);
+    atomicAdd(part + (long long)(kBnSlots + slot) * C + c, b);
   }
 }
 
 // -------- forward finalize: stats = [mean | invstd | scale | shift] -------
 // Block = 64 channels x 16 partial-slices (1024 threads): coalesced loads of
 // the [G][C] partial arrays, LDS tree over the slices.
-__device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int G, int C,
+// Reads the [2][G][C] slot sums of channel c and zeroes them (the slots are
+// persistent and accumulated into by the next producer).
+__device__ __forceinline__ void reduce_partials(float* __restrict__ part, int G, int C,
                                                 int c, float& S, float& Q) {
   __shared__ float rs[16][64], rq[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -97,8 +101,8 @@ __device__ __forceinline__ void reduce_partials(const float* __restrict__ part, 
   // partial arrays come from conv epilogues with up to a few thousand blocks)
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
   if (c < C) {
-    const float* ps = part + c;
-    const float* pq = part + (long long)G * C + c;
+    float* ps = part + c;
+    float* pq = part + (long long)G * C + c;
     int g = ty;
     for (; g + 48 < G; g += 64) {
       a0 += ps[(long long)g * C];        b0 += pq[(long long)g * C];
@@ -107,6 +111,7 @@ __device__ __forceinline__ void reduce_partials(const float* __restrict__ part, 
       a3 += ps[(long long)(g + 48) * C]; b3 += pq[(long long)(g + 48) * C];
     }
     for (; g < G; g += 16) { a0 += ps[(long long)g * C]; b0 += pq[(long long)g * C]; }
+    for (g = ty; g < G; g += 16) { ps[(long long)g * C] = 0.f; pq[(long long)g * C] = 0.f; }
   }
   const float a = (a0 + a1) + (a2 + a3), b = (b0 + b1) + (b2 + b3);
   rs[ty][tx] = a;
@@ -122,7 +127,7 @@ __device__ __forceinline__ void reduce_partials(const float* __restrict__ part, 
 }
 
 __global__ void __launch_bounds__(1024) bn_fwd_finalize_kernel(
-    const float* __restrict__ part, int G, long long M, int C, const float* __restrict__ gamma,
+    float* __restrict__ part, int G, long long M, int C, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ running_mean,
     float* __restrict__ running_var, float momentum, float eps, float* __restrict__ stats,
     int use_running) {
@@ -185,7 +190,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(
 
 // -------- backward finalize: coef = [A | Bc | Cc] -----------------------------
 __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(
-    const float* __restrict__ part, int G, long long M, int C, const float* __restrict__ gamma,
+    float* __restrict__ part, int G, long long M, int C, const float* __restrict__ gamma,
     const float* __restrict__ stats, float* __restrict__ dgamma, float* __restrict__ dbeta,
     float* __restrict__ coef) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -254,9 +259,9 @@ void launch_bn_fwd(const u16* x, const u16* res, u16* y, const float* gamma, con
     hipLaunchKernelGGL((bn_partial_kernel<0, false>), dim3(G), dim3(256), lds, s, x, nullptr,
                        nullptr, nullptr, part, M, C);
   }
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, G, M,
-                     C, gamma, beta, running_mean, running_var, momentum, eps, stats,
-                     training ? 0 : 1);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part,
+                     kBnSlots, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                     stats, training ? 0 : 1);
   const long long nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, 256));
   if (relu) {
@@ -278,8 +283,8 @@ void launch_bn_bwd(const u16* x, const u16* dy, const u16* y, const float* gamma
     hipLaunchKernelGGL((bn_partial_kernel<1, true>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, M, C);
   else
     hipLaunchKernelGGL((bn_partial_kernel<1, false>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, M, C);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, G, M,
-                     C, gamma, stats, dgamma, dbeta, coef);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part,
+                     kBnSlots, M, C, gamma, stats, dgamma, dbeta, coef);
   const long long nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, 256));
   if (relu) {
@@ -298,10 +303,11 @@ namespace dmp {
 // conv's epilogue (conv.hip STATS): finalize + apply only, no stats pass over x.
 void launch_bn_fwd_partials(const u16* x, const u16* res, u16* y, const float* gamma,
                             const float* beta, float* running_mean, float* running_var,
-                            float* stats, const float* part, int G, long long M, int C,
+                            float* stats, float* part, long long M, int C,
                             float momentum, float eps, bool relu, hipStream_t s) {
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, G, M,
-                     C, gamma, beta, running_mean, running_var, momentum, eps, stats, 0);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part,
+                     kBnSlots, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                     stats, 0);
   const long long nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, 256));
   if (relu) {

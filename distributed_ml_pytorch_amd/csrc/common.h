@@ -9,6 +9,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include "bn_slots.h"
 #include <stdint.h>
 
 namespace dmp {
@@ -17,6 +19,7 @@ constexpr int kWave = 64;
 
 using u16 = uint16_t;
 using u32 = uint32_t;
+using u8 = uint8_t;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

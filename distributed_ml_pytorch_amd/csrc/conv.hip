@@ -42,9 +42,10 @@ struct ConvArgs {
   const u16* x;     // gathered operand NHWC [B][GH][GW][CI]   (fwd: X, dgrad: dY)
   const u16* w;     // [CO][R][S][CI]                           (fwd: W, dgrad: Wt)
   u16* y;           // output NHWC [B][OH][OW][CO]              (fwd: Y, dgrad: dX)
-  float* part;      // optional BN partials [2][gridDim.x][CO]
+  float* part;      // optional BN slot sums [2][kBnSlots][CO] (atomically accumulated)
   int B, GH, GW, CI, OH, OW, CO, R, S, stride, pad;
   long long M;      // fwd: B*OH*OW; dgrad: rows of the largest parity class
+  const float* bias;   // optional fp32 [CO] added in the fwd epilogue
 };
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -285,7 +286,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
       const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
       bf16x4 o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o.v[r] = f2bf(acc[i][j][r]);
+      for (int r = 0; r < 4; ++r)
+        o.v[r] = f2bf(acc[i][j][r] + ((MODE == 0 && a.bias && n + r < a.CO) ? a.bias[n + r] : 0.f));
       if (m < Mc && n < a.CO) {
         *reinterpret_cast<bf16x4*>(a.y + pix * a.CO + n) = o;
         if (STATS) {
@@ -328,8 +330,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
         float ss = 0.f, qq = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { ss += red[w * BN + nl]; qq += red[WM * BN + w * BN + nl]; }
-        a.part[(long long)blockIdx.x * a.CO + n] = ss;
-        a.part[(long long)(gridDim.x + blockIdx.x) * a.CO + n] = qq;
+        const int slot = blockIdx.x % kBnSlots;
+        atomicAdd(a.part + (long long)slot * a.CO + n, ss);
+        atomicAdd(a.part + (long long)(kBnSlots + slot) * a.CO + n, qq);
       }
     }
   }
@@ -441,9 +444,9 @@ int conv_fwd_num_mblocks(long long M, int CO, int cfg) {
 
 void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int H, int W,
                      int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                     hipStream_t s) {
+                     hipStream_t s, const float* bias) {
   ConvArgs a{x, w, y, part, B, H, W, CI, OH, OW, CO, R, S, stride, pad,
-             (long long)B * OH * OW};
+             (long long)B * OH * OW, bias};
   if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(a.M, CO);
   if (part) dispatch<0, true>(a, cfg, 1, s);
   else dispatch<0, false>(a, cfg, 1, s);
@@ -454,7 +457,7 @@ void launch_conv_dgrad(const u16* dy, const u16* wt, u16* dx, int B, int H, int 
                        int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s) {
   const long long rows = (long long)B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
-  ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad, rows};
+  ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad, rows, nullptr};
   if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(rows * stride * stride, CI);
   dispatch<1, false>(a, cfg, stride * stride, s);
 }

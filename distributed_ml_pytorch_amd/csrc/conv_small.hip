@@ -13,8 +13,8 @@
 //            taps are gathered 8 at a time through an LDS tap table (no integer
 //            division in the loop).  Epilogue: bf16 NHWC store + per-channel BN
 //            partial sums (recursive-halving butterfly over the lanes, lane l
-//            ends up owning channel l & 15), same [2][G][CO] layout as the
-//            implicit-GEMM epilogue (conv.hip).
+//            ends up owning channel l & 15), added into the same
+//            [2][kBnSlots][CO] slot sums as the implicit-GEMM epilogue.
 //   wgrad    dW[co][k] = sum_p dY[p][co] * patch_p[k]: a block owns a chunk of
 //            P, a 64-channel x 32-tap output tile; 64-pixel slabs of dY and of
 //            the patches are staged to LDS as fp32, each lane accumulates a 4 x 8
@@ -31,7 +31,7 @@ struct SmallConvArgs {
   const u16* w;     // [CO][R][S][CI] bf16
   const u16* dy;    // [P][CO] bf16 (wgrad)
   u16* y;           // [P][CO] bf16 (forward)
-  float* part;      // [2][G][CO] BN partials (forward, optional)
+  float* part;      // [2][kBnSlots][CO] BN slot sums (forward, optional, accumulated)
   float* dw;        // [CO][R][S][CI] fp32 (wgrad, accumulated)
   float* ws;        // wgrad: [G][CO][K] per-block partial tiles
   int sb, sh, sw, sc;           // input strides in elements (input < 2^30 elements)
@@ -177,8 +177,9 @@ __global__ void __launch_bounds__(256) conv_small_fwd_kernel(SmallConvArgs a) {
   t1 += __shfl_xor(t1, 32, 64); t2 += __shfl_xor(t2, 32, 64);
   if (lane < 16) {
     const int c = co0 + wid * 16 + lane;
-    a.part[(long long)blockIdx.x * a.CO + c] = t1;
-    a.part[(long long)(gridDim.x + blockIdx.x) * a.CO + c] = t2;
+    const int slot = blockIdx.x % kBnSlots;
+    atomicAdd(a.part + (long long)slot * a.CO + c, t1);
+    atomicAdd(a.part + (long long)(kBnSlots + slot) * a.CO + c, t2);
   }
 }
 

@@ -1,6 +1,8 @@
 // Host-side launch entry points of the gfx950 kernels (raw pointers + stream).
 #pragma once
 #include <hip/hip_runtime_api.h>
+
+#include "bn_slots.h"
 #include <stdint.h>
 
 namespace dmp {
@@ -49,6 +51,14 @@ void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int
 void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W,
                         int C, int K, hipStream_t s);
 
+
+// dropout.hip: Philox4x32-10 dropout
+void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
+                         const long long* offset, hipStream_t s);
+void launch_dropout_apply_bf16(const uint16_t* x, const uint8_t* mask, uint16_t* y, long long n,
+                               float scale, int mode, long long inner, int C, hipStream_t s);
+void launch_dropout_apply_f32(const float* x, const uint8_t* mask, float* y, long long n,
+                              float scale, int mode, long long inner, int C, hipStream_t s);
 }  // namespace dmp
 
 namespace dmp {
@@ -59,7 +69,7 @@ int conv_default_config(long long M, int CO);
 int conv_fwd_num_mblocks(long long M, int CO, int cfg);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int B, int H,
                      int W, int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
-                     int cfg, hipStream_t s);
+                     int cfg, hipStream_t s, const float* bias = nullptr);
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int B, int H, int W,
                        int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s);
@@ -80,17 +90,41 @@ int conv_small_wgrad_blocks(long long P, int CO, int R, int S, int CI);
 void launch_conv_small_wgrad(const uint16_t* dy, const uint16_t* x, int xbytes, int sb, int sh, int sw, int sc,
                              float* dw, float* ws, int B, int H, int W, int CI, int OH, int OW,
                              int CO, int R, int S, int stride, int pad, hipStream_t s);
+
+// dropout.hip: Philox4x32-10 dropout
+void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
+                         const long long* offset, hipStream_t s);
+void launch_dropout_apply_bf16(const uint16_t* x, const uint8_t* mask, uint16_t* y, long long n,
+                               float scale, int mode, long long inner, int C, hipStream_t s);
+void launch_dropout_apply_f32(const float* x, const uint8_t* mask, float* y, long long n,
+                              float scale, int mode, long long inner, int C, hipStream_t s);
 }  // namespace dmp
 
 namespace dmp {
 void launch_bn_fwd_partials(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma,
                             const float* beta, float* running_mean, float* running_var,
-                            float* stats, const float* part, int G, long long M, int C,
+                            float* stats, float* part, long long M, int C,
                             float momentum, float eps, bool relu, hipStream_t s);
+
+// dropout.hip: Philox4x32-10 dropout
+void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
+                         const long long* offset, hipStream_t s);
+void launch_dropout_apply_bf16(const uint16_t* x, const uint8_t* mask, uint16_t* y, long long n,
+                               float scale, int mode, long long inner, int C, hipStream_t s);
+void launch_dropout_apply_f32(const float* x, const uint8_t* mask, float* y, long long n,
+                              float scale, int mode, long long inner, int C, hipStream_t s);
 }  // namespace dmp
 
 namespace dmp {
 void launch_conv_weight_transpose_batched(const uint16_t* src, uint16_t* dst,
                                           const long long* table, int n, long long max_elems,
                                           hipStream_t s);
+
+// dropout.hip: Philox4x32-10 dropout
+void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
+                         const long long* offset, hipStream_t s);
+void launch_dropout_apply_bf16(const uint16_t* x, const uint8_t* mask, uint16_t* y, long long n,
+                               float scale, int mode, long long inner, int C, hipStream_t s);
+void launch_dropout_apply_f32(const float* x, const uint8_t* mask, float* y, long long n,
+                              float scale, int mode, long long inner, int C, hipStream_t s);
 }  // namespace dmp

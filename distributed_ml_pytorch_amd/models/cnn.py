@@ -23,7 +23,8 @@ class LeNet(nn.Module):
         super().__init__()
         self.conv1 = L.Conv2d(3, 6, kernel_size=5)
         self.conv2 = L.Conv2d(6, 16, kernel_size=5)
-        self.conv2_drop = nn.Dropout2d()
+        self.conv2_drop = L.Dropout2d()
+        self.fc1_drop = L.Dropout()
         self.fc1 = L.Linear(16 * 5 * 5, 120)
         self.fc2 = L.Linear(120, 84)
         self.fc3 = L.Linear(84, num_classes)
@@ -32,7 +33,7 @@ class LeNet(nn.Module):
         h = F.relu(F.max_pool2d(self.conv1(x), 2))
         h = F.relu(F.max_pool2d(self.conv2_drop(self.conv2(h)), 2))
         h = torch.flatten(h.contiguous(), 1)
-        h = F.dropout(F.relu(self.fc1(h)), training=self.training)
+        h = self.fc1_drop(F.relu(self.fc1(h)))
         h = F.relu(self.fc2(h))
         return self.fc3(h)
 

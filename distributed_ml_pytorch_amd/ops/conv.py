@@ -2,7 +2,8 @@
 
 Native path (``csrc/conv.hip``): NHWC bf16 implicit GEMM on MFMA for
 ``groups == 1, dilation == 1, CI % 64 == 0, CO % 64 == 0`` (every ResNet conv
-except the 3-channel stem, AlexNet conv2-5).  The weight operand is the
+except the 3-channel stem, AlexNet conv2-5), optional fp32 bias added in the
+epilogue (AlexNet; reference convs carry biases, /root/reference/example/models.py:28-38).  The weight operand is the
 arena's bf16 shadow (no per-step cast) and the weight gradient is accumulated
 in fp32 straight into the arena grad view (no AccumulateGrad, no cast
 kernels).  When the conv feeds a BatchNorm (``emit_bn_stats``) its epilogue
@@ -19,6 +20,8 @@ Everything else goes to ``F.conv2d`` (MIOpen) in channels_last.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch.autograd import Function
@@ -29,6 +32,46 @@ from .tuner import TUNER
 _NATIVE_ENABLED = True
 _CONFIGS = None
 _SMALL_MAX_K = 32
+
+# Weight gradients on a side HIP stream.  A layer's wgrad depends only on its
+# dY and X, and nothing in the rest of the backward depends on it (it lands in
+# the fp32 grad arena), so it runs concurrently with the dgrad -> BN-backward
+# chain of the layers below: the MFMA-bound wgrad fills the CUs that the
+# latency-bound BN reductions / finalizes and the small-grid layer-4 convs
+# leave idle.  The side stream is joined back (current stream waits on it) by
+# an autograd end-of-backward callback, so callers -- including hipGraph
+# capture -- see an ordinary single-stream backward.  Disabled for parameters
+# with a grad-ready hook (sync-DP bucket all-reduce orders on the current
+# stream).  Opt-in (DMP_WGRAD_STREAM=1): measured on ResNet-18/CIFAR bs256 the
+# concurrent wgrad grids delay the single-block BN finalize kernels on the
+# critical path (bwd finalize 96 -> 244 us/step) and the step got 3.6% slower
+# (profiles/bench_steady_state_wgrad_stream_r1.txt).
+_WG_STREAM_ENABLED = os.environ.get("DMP_WGRAD_STREAM", "0") == "1"
+_WG_STREAMS: dict = {}
+_WG_KEEP: list = []          # operands kept alive until the join
+_WG_JOIN_QUEUED = [False]
+
+
+def _wg_join():
+    _WG_JOIN_QUEUED[0] = False
+    cur = torch.cuda.current_stream()
+    for side in _WG_STREAMS.values():
+        cur.wait_stream(side)
+    _WG_KEEP.clear()
+
+
+def _side_wgrad(dev, fn, *keep):
+    """Run ``fn()`` on the device's wgrad stream (ordered after the current stream)."""
+    side = _WG_STREAMS.get(dev)
+    if side is None:
+        side = _WG_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        fn()
+    _WG_KEEP.append(keep)
+    if not _WG_JOIN_QUEUED[0]:
+        _WG_JOIN_QUEUED[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(_wg_join)
 
 
 def set_native_conv(enabled: bool):
@@ -89,12 +132,18 @@ def _wgrad_cfg(dy, x, shape, stride, pad):
 
 class _NativeConv(Function):
     @staticmethod
-    def forward(ctx, x, w16, master, stride, pad, want_stats):
+    def forward(ctx, x, w16, master, stride, pad, want_stats, slots=None, bias=None):
         # the BN-partials output never receives a gradient: do not let autograd
         # materialise (zero-fill) one for it every backward
         ctx.set_materialize_grads(False)
         cfg = _fwd_cfg(x, w16, stride, pad)
-        y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats, cfg)
+        b32 = None
+        if bias is not None:
+            b32 = bias.detach()
+            if b32.dtype != torch.float32 or not b32.is_contiguous():
+                b32 = b32.float().contiguous()
+        ctx.bias = bias
+        y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats, cfg, slots, b32)
         ctx.save_for_backward(x, w16)
         ctx.master = master
         ctx.geom = (x.shape[2], x.shape[3], stride, pad)
@@ -106,7 +155,7 @@ class _NativeConv(Function):
     @staticmethod
     def backward(ctx, dy, _dpart):
         if dy is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         x, w16 = ctx.saved_tensors
         H, W, stride, pad = ctx.geom
         dy = dy.contiguous(memory_format=torch.channels_last)
@@ -126,25 +175,40 @@ class _NativeConv(Function):
             wcfg = _wgrad_cfg(dy, x, tuple(master.shape), stride, pad)
             g = master.grad if getattr(master, "_dmp_arena", False) else None
             if g is not None and g.is_contiguous(memory_format=torch.channels_last):
-                native().conv_wgrad(dy, x, g, stride, pad, wcfg)
                 cb = getattr(master, "_dmp_grad_ready", None)
-                if cb is not None:
-                    cb(master)
+                if cb is None and _WG_STREAM_ENABLED:
+                    _side_wgrad(x.device, lambda: native().conv_wgrad(dy, x, g, stride, pad, wcfg),
+                                dy, x)
+                else:
+                    native().conv_wgrad(dy, x, g, stride, pad, wcfg)
+                    if cb is not None:
+                        cb(master)
             else:
                 gw = torch.zeros(tuple(master.shape), dtype=torch.float32, device=x.device)
                 gw = gw.contiguous(memory_format=torch.channels_last)
                 native().conv_wgrad(dy, x, gw, stride, pad, wcfg)
                 gw = gw.to(master.dtype)
-        return dx, None, gw, None, None, None
+        gb = None
+        bias = ctx.bias
+        if bias is not None and bias.requires_grad:
+            col = dy.sum(dim=(0, 2, 3), dtype=torch.float32)
+            if getattr(bias, "_dmp_arena", False) and bias.grad is not None:
+                bias.grad.add_(col)
+                cb = getattr(bias, "_dmp_grad_ready", None)
+                if cb is not None:
+                    cb(bias)
+            else:
+                gb = col.to(bias.dtype)
+        return dx, None, gw, None, None, None, None, gb
 
 
 class _SmallConv(Function):
     """Stem conv: forward + weight gradient only (the input is data)."""
 
     @staticmethod
-    def forward(ctx, x, w16, master, stride, pad, want_stats):
+    def forward(ctx, x, w16, master, stride, pad, want_stats, slots=None):
         ctx.set_materialize_grads(False)
-        y, part, _ = native().conv_small_fwd(x, w16, stride, pad, want_stats)
+        y, part, _ = native().conv_small_fwd(x, w16, stride, pad, want_stats, slots)
         ctx.save_for_backward(x)
         ctx.master = master
         ctx.geom = (stride, pad)
@@ -156,7 +220,7 @@ class _SmallConv(Function):
     @staticmethod
     def backward(ctx, dy, _dpart):
         if dy is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         (x,) = ctx.saved_tensors
         stride, pad = ctx.geom
         master = ctx.master
@@ -173,7 +237,7 @@ class _SmallConv(Function):
                                  memory_format=torch.channels_last).zero_()
                 native().conv_small_wgrad(dy, x, gw, stride, pad)
                 gw = gw.to(master.dtype)
-        return None, None, gw, None, None, None
+        return None, None, gw, None, None, None, None
 
 
 def small_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
@@ -190,6 +254,18 @@ def small_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
     return co % 64 == 0 and r * s * ci <= _SMALL_MAX_K
 
 
+BN_SLOTS = 64   # csrc/bn_slots.h kBnSlots
+
+
+def bn_slot_buffer(owner, attr: str, channels: int, device):
+    """Persistent zeroed ``[2][BN_SLOTS][channels]`` fp32 slot buffer cached on ``owner``."""
+    buf = getattr(owner, attr, None)
+    if buf is None or buf.device != device or buf.numel() != 2 * BN_SLOTS * channels:
+        buf = torch.zeros(2 * BN_SLOTS * channels, dtype=torch.float32, device=device)
+        object.__setattr__(owner, attr, buf)
+    return buf
+
+
 def native_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
     if not (_NATIVE_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
         return False
@@ -202,18 +278,23 @@ def native_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
     return ci % 64 == 0 and co % 64 == 0
 
 
-def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=False):
-    """Returns ``y`` (with BN partials attached as ``y._dmp_bn_part`` when ``want_stats``)."""
+def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=False,
+           slots=None):
+    """Returns ``y`` (with BN slot sums attached as ``y._dmp_bn_part`` when ``want_stats``).
+
+    ``slots``: the layer's persistent ``[2][64][CO]`` fp32 BN slot buffer (zeroed;
+    the consuming BatchNorm's finalize re-zeroes it); a fresh one when None.
+    """
     if x.is_cuda and x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
-        if master is not None and b is None and native_conv_supported(
+        if master is not None and native_conv_supported(
                 x, master, stride, padding, dilation, groups):
             w16 = getattr(master, "_dmp_w16", None)
             if w16 is None or not w16.is_contiguous(memory_format=torch.channels_last):
                 w16 = master.detach().to(torch.bfloat16).contiguous(
                     memory_format=torch.channels_last)
             y, part = _NativeConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
-                                        bool(want_stats))
+                                        bool(want_stats), slots if want_stats else None, b)
             if part is not None:
                 y._dmp_bn_part = part
             return y
@@ -224,7 +305,7 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
                 w16 = master.detach().to(torch.bfloat16).contiguous(
                     memory_format=torch.channels_last)
             y, part = _SmallConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
-                                       bool(want_stats))
+                                       bool(want_stats), slots if want_stats else None)
             if part is not None:
                 y._dmp_bn_part = part
             return y

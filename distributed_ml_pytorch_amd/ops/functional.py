@@ -111,7 +111,7 @@ def softmax_cross_entropy(logits, labels, label_smoothing: float = 0.0, ignore_i
 class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
-                relu, part=None):
+                relu, part=None, slots=None):
         if x.dim() == 4:
             x = x.contiguous(memory_format=CL)
             if residual is not None:
@@ -124,7 +124,9 @@ class _BNAct(Function):
                 running_var, float(momentum), float(eps), bool(relu))
         else:
             y, stats = native().bn_fwd(x, residual, gamma, beta, running_mean, running_var,
-                                       float(momentum), float(eps), bool(training), bool(relu))
+                                       float(momentum), float(eps), bool(training), bool(relu),
+                                       slots[0] if slots is not None else None)
+        ctx.bslots = slots[1] if slots is not None else None
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.gamma, ctx.beta = gamma, beta
@@ -146,24 +148,29 @@ class _BNAct(Function):
             dy = dy.contiguous(memory_format=CL)
         else:
             dy = dy.contiguous()
-        dx, dres = native().bn_bwd(x, dy, y, gamma, stats, dg, db, ctx.relu, ctx.has_res)
+        dx, dres = native().bn_bwd(x, dy, y, gamma, stats, dg, db, ctx.relu, ctx.has_res,
+                                   ctx.bslots)
         if dg_arena is not None or db_arena is not None:
             _notify(gamma, beta)
         ret_g = None if (dg_arena is not None or not need_g) else dg
         ret_b = None if (db_arena is not None or not need_b) else db
         return (dx, ret_g, ret_b, (dres if ctx.has_res else None), None, None, None, None, None,
-                None, None)
+                None, None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float,
-                   eps: float, relu: bool = False, residual=None):
-    """``relu?(batch_norm(x) [+ residual])`` in one fused kernel pair (NHWC bf16 on GPU)."""
+                   eps: float, relu: bool = False, residual=None, slots=None):
+    """``relu?(batch_norm(x) [+ residual])`` in one fused kernel pair (NHWC bf16 on GPU).
+
+    ``slots``: optional persistent (forward, backward) BN slot-sum buffers of the
+    layer (see ``ops.conv.bn_slot_buffer``); fresh zeroed ones when None.
+    """
     if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0 and x.shape[1] <= 2048:
         if not training and (running_mean is None or running_var is None):
             training = True
         part = getattr(x, "_dmp_bn_part", None) if training else None
         return _BNAct.apply(x, weight, bias, residual, running_mean, running_var, training,
-                            momentum, eps, relu, part)
+                            momentum, eps, relu, part, slots)
     if x.is_cuda:
         raise RuntimeError(
             f"batch_norm_act: unsupported GPU input (dtype={x.dtype}, C={x.shape[1]}); "
@@ -218,3 +225,45 @@ def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0)
             and x.shape[1] % 8 == 0 and x.shape[2] >= kernel_size and x.shape[3] >= kernel_size):
         return _MaxPool.apply(x, int(kernel_size))
     return F.max_pool2d(x, kernel_size, stride, padding)
+
+
+# -------------------------------------------------------------------- dropout
+class _Dropout(Function):
+    @staticmethod
+    def forward(ctx, x, p, seed, offset, mode):
+        y, mask = native().dropout_fwd(x, float(p), int(seed), offset, int(mode))
+        # advance the layer's device-side Philox offset in-stream: a captured
+        # hipGraph replays this add, so every replay draws a fresh mask
+        offset.add_(1)
+        ctx.save_for_backward(mask)
+        ctx.p, ctx.mode = p, mode
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (mask,) = ctx.saved_tensors
+        return native().dropout_bwd(dy, mask, float(ctx.p), int(ctx.mode)), None, None, None, None
+
+
+def dropout(x, p: float, training: bool, channelwise: bool = False, state=None, seed: int = 0):
+    """Dropout (``channelwise``: Dropout2d, one draw per (n, c) plane).
+
+    GPU: Philox4x32-10 kernel (``csrc/dropout.hip``) keyed by ``seed`` and the
+    device int64 counter ``state`` (advanced in-stream after each call).
+    Reference: ``nn.Dropout2d`` / ``F.dropout`` in LeNet
+    (/root/reference/example/models.py:10,17,20).
+    """
+    if not training or p == 0.0:
+        return x
+    if x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and state is not None:
+        mode = 0
+        if channelwise:
+            if x.dim() == 4 and x.is_contiguous(memory_format=CL) and not x.is_contiguous():
+                mode = 2
+            else:
+                x = x.contiguous()
+                mode = 1
+        return _Dropout.apply(x, p, seed, state, mode)
+    if channelwise:
+        return F.dropout2d(x, p, True)
+    return F.dropout(x, p, True)

@@ -12,7 +12,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import functional as DF
-from .conv import conv2d as _conv2d, native_conv_supported, small_conv_supported
+from .conv import bn_slot_buffer, conv2d as _conv2d, native_conv_supported, small_conv_supported
 from .linear import arena_linear_ok, linear as _arena_linear
 
 
@@ -26,14 +26,16 @@ class Conv2d(nn.Conv2d):
     emit_bn_stats = False
 
     def forward(self, x):
-        if (x.is_cuda and self.bias is None
+        if (x.is_cuda and (self.bias is None or native_conv_supported(
+                x, self.weight, self.stride, self.padding, self.dilation, self.groups))
                 and (native_conv_supported(x, self.weight, self.stride, self.padding,
                                            self.dilation, self.groups)
                      or small_conv_supported(x, self.weight, self.stride, self.padding,
                                              self.dilation, self.groups))):
-            return _conv2d(x, None, None, self.stride, self.padding, self.dilation, self.groups,
-                           master=self.weight,
-                           want_stats=self.emit_bn_stats and self.training)
+            want = self.emit_bn_stats and self.training
+            slots = bn_slot_buffer(self, "_dmp_slots", self.out_channels, x.device) if want else None
+            return _conv2d(x, None, self.bias, self.stride, self.padding, self.dilation,
+                           self.groups, master=self.weight, want_stats=want, slots=slots)
         w = DF.compute_weight(self.weight, x.dtype)
         b = DF.compute_weight(self.bias, x.dtype)
         return _conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups)
@@ -48,9 +50,18 @@ class Linear(nn.Linear):
         return F.linear(x, w, b)
 
 
+def _bn_slots(mod, x):
+    if not x.is_cuda:
+        return None
+    return (bn_slot_buffer(mod, "_dmp_fslots", mod.num_features, x.device),
+            bn_slot_buffer(mod, "_dmp_bslots", mod.num_features, x.device))
+
+
 class BatchNorm2d(nn.BatchNorm2d):
     """BatchNorm with optional fused residual-add and ReLU epilogue."""
 
+    _slots = _bn_slots
+
     def __init__(self, num_features, eps=1e-5, momentum=0.1, relu: bool = False, **kw):
         super().__init__(num_features, eps=eps, momentum=momentum, **kw)
         self.relu = relu
@@ -62,10 +73,12 @@ class BatchNorm2d(nn.BatchNorm2d):
             self.running_mean if self.track_running_stats else None,
             self.running_var if self.track_running_stats else None,
             use_batch, 0.1 if self.momentum is None else self.momentum, self.eps,
-            relu=self.relu, residual=residual)
+            relu=self.relu, residual=residual, slots=self._slots(x))
 
 
 class BatchNorm1d(nn.BatchNorm1d):
+    _slots = _bn_slots
+
     def __init__(self, num_features, eps=1e-5, momentum=0.1, relu: bool = False, **kw):
         super().__init__(num_features, eps=eps, momentum=momentum, **kw)
         self.relu = relu
@@ -77,7 +90,7 @@ class BatchNorm1d(nn.BatchNorm1d):
             self.running_mean if self.track_running_stats else None,
             self.running_var if self.track_running_stats else None,
             use_batch, 0.1 if self.momentum is None else self.momentum, self.eps,
-            relu=self.relu, residual=residual)
+            relu=self.relu, residual=residual, slots=self._slots(x))
 
 
 class MaxPool2d(nn.MaxPool2d):
@@ -97,3 +110,37 @@ class GlobalAvgPool(nn.Module):
 
 class ReLU(nn.ReLU):
     pass
+
+
+class _DropoutBase(nn.Module):
+    channelwise = False
+
+    def __init__(self, p: float = 0.5, seed: int | None = None):
+        super().__init__()
+        if not 0.0 <= p < 1.0:
+            raise ValueError(f"dropout probability must be in [0, 1), got {p}")
+        self.p = p
+        self.seed = int(torch.randint(0, 2**62, (1,)).item()) if seed is None else int(seed)
+        self._state = None
+
+    def forward(self, x):
+        state = None
+        if x.is_cuda:
+            if self._state is None or self._state.device != x.device:
+                self._state = torch.zeros(1, dtype=torch.int64, device=x.device)
+            state = self._state
+        return DF.dropout(x, self.p, self.training, self.channelwise, state, self.seed)
+
+    def extra_repr(self):
+        return f"p={self.p}"
+
+
+class Dropout(_DropoutBase):
+    """Element-wise dropout on the Philox kernel (``csrc/dropout.hip``)."""
+
+
+class Dropout2d(_DropoutBase):
+    """Channel (plane) dropout on the Philox kernel."""
+
+    channelwise = True
+

@@ -179,3 +179,29 @@ def test_weight_transpose_batched():
         w = src[o:o + n].view(co, r, k, ci)
         wt = dst[o:o + n].view(ci, r, k, co)
         assert torch.equal(wt, w.permute(3, 1, 2, 0))
+
+
+def test_conv_layer_bias_native():
+    """AlexNet-style conv with bias on the native path: output and all grads vs fp32."""
+    from distributed_ml_pytorch_amd.ops import layers as L
+    from distributed_ml_pytorch_amd.parallel.arena import FlatArena
+
+    torch.manual_seed(2)
+    conv = L.Conv2d(64, 192, 5, padding=2, bias=True).cuda()
+    with torch.no_grad():
+        conv.bias.uniform_(-0.5, 0.5)
+    FlatArena(conv, device="cuda")
+    x = torch.randn(4, 64, 8, 8, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    x.requires_grad_(True)
+    y = conv(x)
+    w = conv.weight._dmp_w16.float().detach().requires_grad_(True)
+    b = conv.bias.detach().clone().requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, w, b, 1, 2)
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(torch.bfloat16))
+    yr.backward(dy.to(torch.bfloat16).float())
+    assert _rel(conv.weight.grad, w.grad) < 1e-2
+    assert _rel(conv.bias.grad, b.grad) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2

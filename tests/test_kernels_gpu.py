@@ -198,3 +198,35 @@ def test_max_pool(shape, k):
     (y.float() * dy).sum().backward()
     (yr * dy).sum().backward()
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("mode", ["elem", "nchw", "nhwc"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_dropout_kernel(mode, dtype):
+    from distributed_ml_pytorch_amd.ops import layers as L
+
+    torch.manual_seed(0)
+    x = torch.randn(8, 32, 9, 9, device="cuda").to(dtype)
+    if mode == "nhwc":
+        x = x.contiguous(memory_format=torch.channels_last)
+    layer = (L.Dropout(0.3, seed=7) if mode == "elem" else L.Dropout2d(0.3, seed=7)).cuda()
+    x.requires_grad_(True)
+    y = layer(x)
+    keep = y.float() != 0
+    frac = keep.float().mean().item()
+    assert abs(frac - 0.7) < 0.03
+    scale = 1.0 / 0.7
+    torch.testing.assert_close(y.float()[keep], (x.detach().float() * scale)[keep],
+                               rtol=1e-2, atol=1e-2)
+    if mode != "elem":   # one draw per (n, c) plane
+        per_plane = keep.float().mean(dim=(2, 3))
+        assert bool(((per_plane == 0) | (per_plane == 1)).all())
+    g = torch.randn_like(y)
+    y.backward(g)
+    torch.testing.assert_close(x.grad.float(), (g.float() * keep.float() * scale),
+                               rtol=1e-2, atol=1e-2)
+    # the device offset advances: a second call draws a different mask
+    y2 = layer(x.detach())
+    assert not torch.equal(y2 != 0, y != 0)
+    layer.eval()
+    assert layer(x) is x
