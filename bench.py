@@ -51,7 +51,51 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="capture fwd+bwd+update in a hipGraph")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra steps after timing, for rocprofv3 windows")
+    ap.add_argument("--ttl-target", type=float, default=0.5,
+                    help="after the throughput run: train a FRESH model on learnable synthetic "
+                         "data until the mean loss of 10 steps <= target and report the "
+                         "wall time (the metric's time-to-target-loss half); 0 skips")
+    ap.add_argument("--ttl-max-steps", type=int, default=1500)
     return ap.parse_args()
+
+
+def time_to_target(a, cfg, info):
+    """Wall time for a freshly initialised model (same engine, same config) to
+    bring the mean training loss over 10 steps down to ``--ttl-target`` on
+    class-template synthetic images (learnable, unlike the noise batches of the
+    throughput run).  Includes graph capture and the first (tuning) step."""
+    from distributed_ml_pytorch_amd.runtime.dist import barrier
+    from distributed_ml_pytorch_amd.runtime.trainer import Worker
+    from distributed_ml_pytorch_amd.utils.data import DeviceBatchPool
+
+    torch.manual_seed(1000 + info.rank)
+    w = Worker(cfg, info)
+    if a.mode != "sync":
+        w.enable_graph(bool(a.graph))
+    pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device, n_batches=32,
+                           dtype=w.compute_dtype, seed=100 + info.rank, learnable=True)
+    barrier(info)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    steps, reached, window = 0, False, []
+    while steps < a.ttl_max_steps:
+        x, y = pool.next()
+        loss, _ = w.train_step(x, y)
+        window.append(loss.detach().float())
+        steps += 1
+        if steps % 10 == 0:
+            mean = float(torch.stack(window).mean().item())
+            window.clear()
+            if mean <= a.ttl_target:
+                reached = True
+                break
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    w.finish()
+    return {"time_to_target_s": round(t, 3), "ttl_target_loss": a.ttl_target,
+            "ttl_steps": steps, "ttl_reached": reached,
+            "ttl_data": "synthetic class-template images (signal 0.5 + N(0,1) noise), "
+                        "32 distinct batches per rank"}
 
 
 def main():
@@ -93,7 +137,9 @@ def main():
         x, y = pool.next()
         w.train_step(x, y)
     torch.cuda.synchronize()
+    in_shape = tuple(w.input_shape)
     w.finish()
+    ttl = time_to_target(a, cfg, info) if a.ttl_target > 0 else None
     if info.rank == 0:
         global_batch = a.batch * world
         value = global_batch * a.steps / elapsed
@@ -111,17 +157,19 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": a.dtype,
-            "data": "synthetic (CIFAR-10-shaped 3x32x32, random labels, HBM-resident); "
-                    "random-init weights",
+            "data": f"synthetic ({'x'.join(map(str, in_shape))} images, random labels, "
+                    "HBM-resident); random-init weights",
             "config": {"model": f"{a.model} (CIFAR stem)" if a.model.startswith("resnet")
                        else a.model,
                        "global_batch": global_batch, "per_gpu_batch": a.batch,
-                       "seq_len": None, "image": "3x32x32",
+                       "seq_len": None, "image": "x".join(map(str, in_shape)),
                        "parallelism": par, "n_push": a.n_push, "n_pull": a.n_pull,
                        "staleness": a.staleness, "lr": a.lr, "hip_graph": bool(graphed),
                        "master_dtype": "fp32"},
             "final_loss": round(final_loss, 4),
         }
+        if ttl is not None:
+            out.update(ttl)
         print(json.dumps(out), flush=True)
     shutdown()
 

@@ -508,6 +508,103 @@ void conv_small_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pa
                                cur_stream());
 }
 
+// ------------------------------------------------------------- transformer
+void check_rows_bf16(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.is_contiguous(), name,
+              " must be a contiguous bf16 tensor");
+}
+
+std::vector<Tensor> layernorm_fwd(Tensor x, optional<Tensor> gamma, optional<Tensor> beta,
+                                  double eps) {
+  check_rows_bf16(x, "x");
+  const int64_t D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= dmp::layernorm_max_dim(), "layernorm: D % 8 == 0, D <= ",
+              dmp::layernorm_max_dim());
+  for (auto* t : {&gamma, &beta})
+    if (t->has_value())
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == D &&
+                      (*t)->is_contiguous(), "layernorm affine params must be fp32 [D]");
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({rows}, fopt), rstd = at::empty({rows}, fopt);
+  dmp::launch_layernorm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                            ptr_or_null<float>(gamma), ptr_or_null<float>(beta),
+                            reinterpret_cast<uint16_t*>(y.data_ptr()), mean.data_ptr<float>(),
+                            rstd.data_ptr<float>(), rows, (int)D, (float)eps, cur_stream());
+  return {y, mean, rstd};
+}
+
+Tensor layernorm_bwd(Tensor x, Tensor dy, optional<Tensor> gamma, Tensor mean, Tensor rstd,
+                     optional<Tensor> dgamma, optional<Tensor> dbeta) {
+  check_rows_bf16(x, "x");
+  dy = dy.contiguous();
+  check_rows_bf16(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "layernorm_bwd: dy shape mismatch");
+  const int64_t D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_bwd: stats mismatch");
+  for (auto* t : {&gamma, &dgamma, &dbeta})
+    if (t->has_value())
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == D &&
+                      (*t)->is_contiguous(), "layernorm gamma/dgamma/dbeta must be fp32 [D]");
+  auto dx = at::empty_like(x);
+  dmp::launch_layernorm_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                            reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                            ptr_or_null<float>(gamma), mean.data_ptr<float>(),
+                            rstd.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                            ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta), rows, (int)D,
+                            cur_stream());
+  return dx;
+}
+
+Tensor gelu_fwd(Tensor x) {
+  check_rows_bf16(x, "x");
+  TORCH_CHECK(x.numel() % 8 == 0, "gelu: numel % 8 == 0");
+  auto y = at::empty_like(x);
+  dmp::launch_gelu_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                       reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), cur_stream());
+  return y;
+}
+
+Tensor gelu_bwd(Tensor x, Tensor dy) {
+  check_rows_bf16(x, "x");
+  dy = dy.contiguous();
+  check_rows_bf16(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes() && x.numel() % 8 == 0, "gelu_bwd: shape");
+  auto dx = at::empty_like(x);
+  dmp::launch_gelu_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                       reinterpret_cast<uint16_t*>(dx.data_ptr()), x.numel(), cur_stream());
+  return dx;
+}
+
+Tensor softmax_fwd(Tensor sc, double scale) {
+  check_rows_bf16(sc, "scores");
+  const int64_t L = sc.size(-1);
+  TORCH_CHECK(L <= dmp::softmax_max_len(), "softmax: row length <= ", dmp::softmax_max_len());
+  auto p = at::empty_like(sc);
+  dmp::launch_softmax_fwd(reinterpret_cast<const uint16_t*>(sc.data_ptr()),
+                          reinterpret_cast<uint16_t*>(p.data_ptr()), sc.numel() / L, (int)L,
+                          (float)scale, cur_stream());
+  return p;
+}
+
+Tensor softmax_bwd(Tensor p, Tensor dp, double scale) {
+  check_rows_bf16(p, "p");
+  dp = dp.contiguous();
+  check_rows_bf16(dp, "dp");
+  TORCH_CHECK(dp.sizes() == p.sizes(), "softmax_bwd: shape mismatch");
+  const int64_t L = p.size(-1);
+  auto ds = at::empty_like(p);
+  dmp::launch_softmax_bwd(reinterpret_cast<const uint16_t*>(p.data_ptr()),
+                          reinterpret_cast<const uint16_t*>(dp.data_ptr()),
+                          reinterpret_cast<uint16_t*>(ds.data_ptr()), p.numel() / L, (int)L,
+                          (float)scale, cur_stream());
+  return ds;
+}
+
 // ------------------------------------------------------------------ dropout
 // mode 0: element-wise; 1: per (n, c) plane of an NCHW tensor; 2: per (n, c)
 // of an NHWC (channels_last) tensor.
@@ -647,6 +744,12 @@ PYBIND11_MODULE(_native, m) {
   m.def("bn_bwd", &bn_bwd, "NHWC batchnorm(+residual)(+relu) backward", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"), py::arg("slots") = py::none());
+  m.def("layernorm_fwd", &layernorm_fwd, "row LayerNorm forward -> (y, mean, rstd)");
+  m.def("layernorm_bwd", &layernorm_bwd, "row LayerNorm backward (dgamma/dbeta accumulated)");
+  m.def("gelu_fwd", &gelu_fwd, "tanh-GELU forward");
+  m.def("gelu_bwd", &gelu_bwd, "tanh-GELU backward");
+  m.def("softmax_fwd", &softmax_fwd, "scaled row softmax forward");
+  m.def("softmax_bwd", &softmax_bwd, "scaled row softmax backward");
   m.def("dropout_fwd", &dropout_fwd, "Philox dropout forward -> (y, keep mask)");
   m.def("dropout_bwd", &dropout_bwd, "dropout backward from the saved keep mask");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pool forward");

@@ -52,6 +52,23 @@ void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, in
                         int C, int K, hipStream_t s);
 
 
+// transformer.hip: LayerNorm / GELU / softmax (ViT)
+int layernorm_max_dim();
+void launch_layernorm_fwd(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
+                          float* mean, float* rstd, long long rows, int D, float eps,
+                          hipStream_t s);
+void launch_layernorm_bwd(const uint16_t* x, const uint16_t* dy, const float* gamma,
+                          const float* mean, const float* rstd, uint16_t* dx, float* dgamma,
+                          float* dbeta, long long rows, int D, hipStream_t s);
+void launch_gelu_fwd(const uint16_t* x, uint16_t* y, long long n, hipStream_t s);
+void launch_gelu_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, long long n,
+                     hipStream_t s);
+int softmax_max_len();
+void launch_softmax_fwd(const uint16_t* sc, uint16_t* p, long long rows, int L, float scale,
+                        hipStream_t s);
+void launch_softmax_bwd(const uint16_t* p, const uint16_t* dp, uint16_t* ds, long long rows, int L,
+                        float scale, hipStream_t s);
+
 // dropout.hip: Philox4x32-10 dropout
 void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
                          const long long* offset, hipStream_t s);
@@ -91,6 +108,23 @@ void launch_conv_small_wgrad(const uint16_t* dy, const uint16_t* x, int xbytes, 
                              float* dw, float* ws, int B, int H, int W, int CI, int OH, int OW,
                              int CO, int R, int S, int stride, int pad, hipStream_t s);
 
+// transformer.hip: LayerNorm / GELU / softmax (ViT)
+int layernorm_max_dim();
+void launch_layernorm_fwd(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
+                          float* mean, float* rstd, long long rows, int D, float eps,
+                          hipStream_t s);
+void launch_layernorm_bwd(const uint16_t* x, const uint16_t* dy, const float* gamma,
+                          const float* mean, const float* rstd, uint16_t* dx, float* dgamma,
+                          float* dbeta, long long rows, int D, hipStream_t s);
+void launch_gelu_fwd(const uint16_t* x, uint16_t* y, long long n, hipStream_t s);
+void launch_gelu_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, long long n,
+                     hipStream_t s);
+int softmax_max_len();
+void launch_softmax_fwd(const uint16_t* sc, uint16_t* p, long long rows, int L, float scale,
+                        hipStream_t s);
+void launch_softmax_bwd(const uint16_t* p, const uint16_t* dp, uint16_t* ds, long long rows, int L,
+                        float scale, hipStream_t s);
+
 // dropout.hip: Philox4x32-10 dropout
 void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
                          const long long* offset, hipStream_t s);
@@ -106,6 +140,23 @@ void launch_bn_fwd_partials(const uint16_t* x, const uint16_t* res, uint16_t* y,
                             float* stats, float* part, long long M, int C,
                             float momentum, float eps, bool relu, hipStream_t s);
 
+// transformer.hip: LayerNorm / GELU / softmax (ViT)
+int layernorm_max_dim();
+void launch_layernorm_fwd(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
+                          float* mean, float* rstd, long long rows, int D, float eps,
+                          hipStream_t s);
+void launch_layernorm_bwd(const uint16_t* x, const uint16_t* dy, const float* gamma,
+                          const float* mean, const float* rstd, uint16_t* dx, float* dgamma,
+                          float* dbeta, long long rows, int D, hipStream_t s);
+void launch_gelu_fwd(const uint16_t* x, uint16_t* y, long long n, hipStream_t s);
+void launch_gelu_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, long long n,
+                     hipStream_t s);
+int softmax_max_len();
+void launch_softmax_fwd(const uint16_t* sc, uint16_t* p, long long rows, int L, float scale,
+                        hipStream_t s);
+void launch_softmax_bwd(const uint16_t* p, const uint16_t* dp, uint16_t* ds, long long rows, int L,
+                        float scale, hipStream_t s);
+
 // dropout.hip: Philox4x32-10 dropout
 void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
                          const long long* offset, hipStream_t s);
@@ -119,6 +170,23 @@ namespace dmp {
 void launch_conv_weight_transpose_batched(const uint16_t* src, uint16_t* dst,
                                           const long long* table, int n, long long max_elems,
                                           hipStream_t s);
+
+// transformer.hip: LayerNorm / GELU / softmax (ViT)
+int layernorm_max_dim();
+void launch_layernorm_fwd(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
+                          float* mean, float* rstd, long long rows, int D, float eps,
+                          hipStream_t s);
+void launch_layernorm_bwd(const uint16_t* x, const uint16_t* dy, const float* gamma,
+                          const float* mean, const float* rstd, uint16_t* dx, float* dgamma,
+                          float* dbeta, long long rows, int D, hipStream_t s);
+void launch_gelu_fwd(const uint16_t* x, uint16_t* y, long long n, hipStream_t s);
+void launch_gelu_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, long long n,
+                     hipStream_t s);
+int softmax_max_len();
+void launch_softmax_fwd(const uint16_t* sc, uint16_t* p, long long rows, int L, float scale,
+                        hipStream_t s);
+void launch_softmax_bwd(const uint16_t* p, const uint16_t* dp, uint16_t* ds, long long rows, int L,
+                        float scale, hipStream_t s);
 
 // dropout.hip: Philox4x32-10 dropout
 void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,

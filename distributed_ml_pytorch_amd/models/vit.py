@@ -2,9 +2,11 @@
 
 Not in the reference (no sequence models there).  ViT-B/16 at
 224x224 = 197 tokens, D=768, 12 heads, MLP 3072, 86,567,656 parameters with a
-1000-class head.  Patch embedding is a stride-16 conv (an implicit GEMM);
-attention uses PyTorch-ROCm's fused SDPA kernel; the projection GEMMs run on
-hipBLASLt through ``F.linear`` (plain library GEMMs).
+1000-class head.  LayerNorm, tanh-GELU and the attention softmax are native
+kernels (``csrc/transformer.hip``); the projection / attention GEMMs are plain
+library GEMMs (hipBLASLt through ``F.linear`` / ``torch.matmul``) whose weight
+gradients accumulate in fp32 straight into the grad arena (``ops.linear``).
+Patch embedding is a stride-16 conv.
 """
 from __future__ import annotations
 
@@ -15,13 +17,13 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import layers as L
+from ..ops import functional as DF
 from ..ops.functional import compute_weight
 
 
 class LayerNorm(nn.LayerNorm):
     def forward(self, x):
-        return F.layer_norm(x, self.normalized_shape, compute_weight(self.weight, x.dtype),
-                            compute_weight(self.bias, x.dtype), self.eps)
+        return DF.layer_norm(x, self.weight, self.bias, self.eps)
 
 
 class Attention(nn.Module):
@@ -35,7 +37,7 @@ class Attention(nn.Module):
         B, N, D = x.shape
         qkv = self.qkv(x).view(B, N, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
-        o = F.scaled_dot_product_attention(q, k, v)
+        o = DF.attention(q, k, v)
         return self.proj(o.transpose(1, 2).reshape(B, N, D))
 
 
@@ -51,7 +53,7 @@ class Block(nn.Module):
 
     def forward(self, x):
         x = x + self.attn(self.norm1(x))
-        return x + self.fc2(F.gelu(self.fc1(self.norm2(x)), approximate="tanh"))
+        return x + self.fc2(DF.gelu(self.fc1(self.norm2(x))))
 
 
 class VisionTransformer(nn.Module):

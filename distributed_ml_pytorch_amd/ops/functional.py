@@ -267,3 +267,99 @@ def dropout(x, p: float, training: bool, channelwise: bool = False, state=None, 
     if channelwise:
         return F.dropout2d(x, p, True)
     return F.dropout(x, p, True)
+
+
+# ----------------------------------------------------------------- layernorm
+class _LayerNorm(Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        x = x.contiguous()
+        g32 = gamma.detach() if gamma is not None else None
+        b32 = beta.detach() if beta is not None else None
+        y, mean, rstd = native().layernorm_fwd(x, g32, b32, float(eps))
+        ctx.save_for_backward(x, mean, rstd)
+        ctx.gamma, ctx.beta = gamma, beta
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd = ctx.saved_tensors
+        gamma, beta = ctx.gamma, ctx.beta
+        dg_arena, db_arena = _arena_grad(gamma), _arena_grad(beta)
+        need_g = gamma is not None and ctx.needs_input_grad[1]
+        need_b = beta is not None and ctx.needs_input_grad[2]
+        dg = dg_arena if dg_arena is not None else (
+            torch.zeros_like(gamma, dtype=torch.float32) if need_g else None)
+        db = db_arena if db_arena is not None else (
+            torch.zeros_like(beta, dtype=torch.float32) if need_b else None)
+        g32 = gamma.detach() if gamma is not None else None
+        dx = native().layernorm_bwd(x, dy, g32, mean, rstd, dg, db)
+        if dg_arena is not None or db_arena is not None:
+            _notify(gamma, beta)
+        ret_g = None if (dg_arena is not None or not need_g) else dg.to(gamma.dtype)
+        ret_b = None if (db_arena is not None or not need_b) else db.to(beta.dtype)
+        return dx, ret_g, ret_b, None
+
+
+def layer_norm(x, weight, bias, eps: float):
+    """LayerNorm over the last dim: native row kernel for bf16 GPU input with fp32
+    affine params (``csrc/transformer.hip``), PyTorch otherwise."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0 and x.shape[-1] <= 4096
+            and (weight is None or weight.dtype == torch.float32)
+            and (bias is None or bias.dtype == torch.float32)):
+        return _LayerNorm.apply(x, weight, bias, eps)
+    w = compute_weight(weight, x.dtype)
+    b = compute_weight(bias, x.dtype)
+    return F.layer_norm(x, (x.shape[-1],), w, b, eps)
+
+
+# ---------------------------------------------------------------------- GELU
+class _GELU(Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        ctx.save_for_backward(x)
+        return native().gelu_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return native().gelu_bwd(x, dy)
+
+
+def gelu(x):
+    """tanh-approximate GELU (native bf16 kernel on GPU)."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.numel() % 8 == 0:
+        return _GELU.apply(x)
+    return F.gelu(x, approximate="tanh")
+
+
+# ------------------------------------------------------------------ attention
+class _ScaledSoftmax(Function):
+    @staticmethod
+    def forward(ctx, s, scale):
+        p = native().softmax_fwd(s.contiguous(), float(scale))
+        ctx.save_for_backward(p)
+        ctx.scale = scale
+        return p
+
+    @staticmethod
+    def backward(ctx, dp):
+        (p,) = ctx.saved_tensors
+        return native().softmax_bwd(p, dp, float(ctx.scale)), None
+
+
+def attention(q, k, v):
+    """softmax(q k^T / sqrt(d)) v over [B, H, N, d] bf16.
+
+    The two batched GEMMs are plain library GEMMs (hipBLASLt via
+    ``torch.matmul``); the scaled row softmax and its backward are native
+    kernels.  At ViT-B/16's 197 tokens the score tensor is small
+    (B*H*197^2 bf16), so it is materialised rather than tiled.
+    """
+    scale = q.shape[-1] ** -0.5
+    if q.is_cuda and q.dtype == torch.bfloat16 and k.shape[-2] <= 1024:
+        s = torch.matmul(q, k.transpose(-1, -2))
+        p = _ScaledSoftmax.apply(s, scale)
+        return torch.matmul(p, v)
+    return F.scaled_dot_product_attention(q, k, v)

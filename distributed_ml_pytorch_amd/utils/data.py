@@ -135,14 +135,25 @@ class DeviceBatchPool:
     """``n_batches`` synthetic batches resident on the device, served round-robin."""
 
     def __init__(self, batch: int, shape, num_classes: int, device, n_batches: int = 8,
-                 dtype=torch.bfloat16, seed: int = 0, channels_last: bool = True):
+                 dtype=torch.bfloat16, seed: int = 0, channels_last: bool = True,
+                 learnable: bool = False, signal: float = 0.5):
+        """``learnable``: images are ``signal * template[label] + N(0, 1)`` with
+        fixed per-class templates (as :class:`SyntheticImages`), so the loss can
+        reach a target; otherwise pure noise with random labels."""
         g = torch.Generator(device="cpu").manual_seed(seed)
         self.x, self.y = [], []
         mf = torch.channels_last if (channels_last and len(shape) == 3) else torch.contiguous_format
+        templates = None
+        if learnable:
+            templates = torch.randn(num_classes, *shape,
+                                    generator=torch.Generator().manual_seed(1234))
         for _ in range(n_batches):
-            x = torch.randn(batch, *shape, generator=g).to(device=device, dtype=dtype)
-            self.x.append(x.contiguous(memory_format=mf))
-            self.y.append(torch.randint(0, num_classes, (batch,), generator=g).to(device))
+            y = torch.randint(0, num_classes, (batch,), generator=g)
+            x = torch.randn(batch, *shape, generator=g)
+            if templates is not None:
+                x += signal * templates[y]
+            self.x.append(x.to(device=device, dtype=dtype).contiguous(memory_format=mf))
+            self.y.append(y.to(device))
         self.i = 0
 
     def next(self):

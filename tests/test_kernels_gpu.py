@@ -230,3 +230,59 @@ def test_dropout_kernel(mode, dtype):
     assert not torch.equal(y2 != 0, y != 0)
     layer.eval()
     assert layer(x) is x
+
+
+@pytest.mark.parametrize("D", [768, 192, 4096])
+def test_layernorm_kernel(D):
+    from distributed_ml_pytorch_amd.ops.functional import layer_norm
+
+    torch.manual_seed(0)
+    x = (torch.randn(3, 37, D, device="cuda") * 2 + 0.5).to(torch.bfloat16).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(D, device="cuda")).requires_grad_(True)
+    b = (0.1 * torch.randn(D, device="cuda")).requires_grad_(True)
+    y = layer_norm(x, w, b, 1e-6)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (D,), wr, br, 1e-6)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g.to(torch.bfloat16).float())
+    rel = lambda a, r: float((a.float() - r).norm() / r.norm())
+    assert rel(x.grad, xr.grad) < 1e-2
+    assert rel(w.grad, wr.grad) < 1e-2
+    assert rel(b.grad, br.grad) < 1e-2
+
+
+def test_gelu_kernel():
+    from distributed_ml_pytorch_amd.ops.functional import gelu
+
+    x = (torch.randn(64, 3072, device="cuda") * 3).to(torch.bfloat16).requires_grad_(True)
+    y = gelu(x)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.gelu(xr, approximate="tanh")
+    torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("N", [197, 65, 1000])
+def test_attention_softmax(N):
+    from distributed_ml_pytorch_amd.ops.functional import attention
+
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(2, 3, N, 64, device="cuda").to(torch.bfloat16).requires_grad_(True)
+               for _ in range(3))
+    o = attention(q, k, v)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    orf = F.scaled_dot_product_attention(qr, kr, vr)
+    rel = lambda a, r: float((a.float() - r).norm() / r.norm())
+    assert rel(o, orf) < 2e-2
+    g = torch.randn_like(orf)
+    o.backward(g.to(torch.bfloat16))
+    orf.backward(g.to(torch.bfloat16).float())
+    for a, r in ((q, qr), (k, kr), (v, vr)):
+        assert rel(a.grad, r.grad) < 3e-2
