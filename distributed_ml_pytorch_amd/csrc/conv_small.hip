@@ -85,12 +85,14 @@ __device__ __forceinline__ void halve(float* v, int lane) {
 }
 // forward: lane = 4 consecutive output pixels, wave = 16 output channels of the
 // 64-channel tile -> each broadcast weight read (4 x ds_read_b128) feeds 64 FMAs
+constexpr int kOutPitch = 72;   // bf16 per staged output row (144 B: 16-B aligned, odd x 16 B)
 __global__ void __launch_bounds__(256) conv_small_fwd_kernel(SmallConvArgs a) {
   constexpr int TC = 8;                          // taps gathered per pass
   extern __shared__ float smem[];
   float* wl = smem;                              // [K][64] fp32
   const int K = a.K, Kp = (K + TC - 1) / TC * TC;
   int* taps = reinterpret_cast<int*>(smem + K * 64);   // [Kp]
+  u16* ot = reinterpret_cast<u16*>(smem + ((K * 64 + Kp + 3) & ~3));   // [256][kOutPitch]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int co0 = blockIdx.y * 64;
@@ -161,11 +163,22 @@ __global__ void __launch_bounds__(256) conv_small_fwd_kernel(SmallConvArgs a) {
         s1[c + 1] += fhi; s2[c + 1] += fhi * fhi;
       }
     }
-    if (pv_ok[i]) {
-      uint4* dst = reinterpret_cast<uint4*>(a.y + (long long)(pbase + i) * a.CO + co0 + wid * 16);
-      dst[0] = make_uint4(packed[0], packed[1], packed[2], packed[3]);
-      dst[1] = make_uint4(packed[4], packed[5], packed[6], packed[7]);
-    }
+    // stage the block's [256 px][64 ch] bf16 tile in LDS: a lane's own pixels are
+    // 4 rows apart in the output, so direct 16-B stores would scatter
+    uint4* t = reinterpret_cast<uint4*>(ot + (lane * 4 + i) * kOutPitch + wid * 16);
+    t[0] = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+    t[1] = make_uint4(packed[4], packed[5], packed[6], packed[7]);
+  }
+  __syncthreads();
+  // coalesced write-out: 8 threads per 128-B pixel row
+#pragma unroll
+  for (int pass = 0; pass < 8; ++pass) {
+    const int idx = pass * 256 + tid;
+    const int row = idx >> 3, ch = idx & 7;
+    const int p = blockIdx.x * 256 + row;
+    if (p < a.P)
+      *reinterpret_cast<uint4*>(a.y + (long long)p * a.CO + co0 + ch * 8) =
+          *reinterpret_cast<const uint4*>(ot + row * kOutPitch + ch * 8);
   }
   if (a.part == nullptr) return;
   // 16 channels x 64 lanes: halve over lane bits 3..0 (lane ends up owning
@@ -197,7 +210,7 @@ __global__ void __launch_bounds__(256) conv_small_wgrad_kernel(SmallConvArgs a) 
   __shared__ __attribute__((aligned(16))) float smem[SLAB * 64 + SLAB * KT];
   static_assert(3 * 64 * KT == SLAB * 64 + SLAB * KT, "reduction tile reuses the slabs");
   __shared__ int taps[KT];
-  __shared__ int4 rows[SLAB];
+  __shared__ int4 rows[2][SLAB];   // pixel decode of slab s in rows[s & 1]
   float* dyl = smem;
   float* pl = smem + SLAB * 64;
   float* red = smem;
@@ -205,53 +218,67 @@ __global__ void __launch_bounds__(256) conv_small_wgrad_kernel(SmallConvArgs a) 
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int co0 = blockIdx.y * 64, k0 = blockIdx.z * KT;
   const int cq = lane & 15, ko = lane >> 4;
-  if (tid < KT) taps[tid] = tap_of(a, k0 + tid);
   const __amdgpu_buffer_rsrc_t rs = image_rsrc(a);
   const int p_begin = blockIdx.x * a.chunk;
   const int p_end = min((int)a.P, p_begin + a.chunk);
+  const int nslab = (p_end - p_begin + SLAB - 1) / SLAB;
+  auto fill_rows = [&](int sl) {       // threads 0..63, slab sl
+    const int p = p_begin + sl * SLAB + tid;
+    const bool ok = sl < nslab && p < p_end;
+    const int3 d = decode_pixel(a, ok ? p : p_begin);
+    rows[sl & 1][tid] = make_int4(d.x, d.y, d.z, ok);
+  };
+  // slab operands in registers: this thread's 16 dY values and 8 patch taps
+  uint4 rdy0, rdy1;
+  float rg[SLAB * KT / 256];
+  auto load_slab = [&](int sl) {
+    {
+      const int r = tid >> 2, c = (tid & 3) * 16;
+      const int p = p_begin + sl * SLAB + r;
+      if (sl < nslab && p < p_end) {
+        const uint4* src = reinterpret_cast<const uint4*>(a.dy + (long long)p * a.CO + co0 + c);
+        rdy0 = src[0];
+        rdy1 = src[1];
+      } else {
+        rdy0 = rdy1 = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < SLAB * KT / 256; ++it) {
+      const int i = it * 256 + tid;
+      const int r = i / KT, k = i % KT;
+      const int4 e = rows[sl & 1][r];
+      rg[it] = load_tap(a, rs, e.w ? taps[k] : -1, e.x, e.y, e.z);
+    }
+  };
+  auto store_slab = [&]() {
+    const int r = tid >> 2, c = (tid & 3) * 16;
+    float4* d = reinterpret_cast<float4*>(dyl + r * 64 + c);
+    const u32 u[8] = {rdy0.x, rdy0.y, rdy0.z, rdy0.w, rdy1.x, rdy1.y, rdy1.z, rdy1.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      d[q] = make_float4(bf2f((u16)(u[2 * q] & 0xffff)), bf2f((u16)(u[2 * q] >> 16)),
+                         bf2f((u16)(u[2 * q + 1] & 0xffff)), bf2f((u16)(u[2 * q + 1] >> 16)));
+#pragma unroll
+    for (int it = 0; it < SLAB * KT / 256; ++it) pl[it * 256 + tid] = rg[it];
+  };
+
   float acc[4][8];
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
-  for (int p0 = p_begin; p0 < p_end; p0 += SLAB) {
-    __syncthreads();   // previous slab consumed
-    if (tid < SLAB) {
-      const int p = p0 + tid;
-      const int3 d = decode_pixel(a, p < p_end ? p : p_begin);
-      rows[tid] = make_int4(d.x, d.y, d.z, p < p_end);
-    }
-    {
-      const int r = tid >> 2, c = (tid & 3) * 16;
-      const int p = p0 + r;
-      float4* d = reinterpret_cast<float4*>(dyl + r * 64 + c);
-      if (p < p_end) {
-        const uint4* src = reinterpret_cast<const uint4*>(a.dy + (long long)p * a.CO + co0 + c);
-        const uint4 v0 = src[0], v1 = src[1];
-        const u32 u[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          d[q] = make_float4(bf2f((u16)(u[2 * q] & 0xffff)), bf2f((u16)(u[2 * q] >> 16)),
-                             bf2f((u16)(u[2 * q + 1] & 0xffff)), bf2f((u16)(u[2 * q + 1] >> 16)));
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) d[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
-    __syncthreads();   // row table visible
-    // all gathers first, then the LDS stores (a store between them would
-    // order every later table read behind it and serialise the loads)
-    float g[SLAB * KT / 256];
-#pragma unroll
-    for (int it = 0; it < SLAB * KT / 256; ++it) {
-      const int i = it * 256 + tid;
-      const int r = i / KT, k = i % KT;
-      const int4 e = rows[r];
-      g[it] = load_tap(a, rs, e.w ? taps[k] : -1, e.x, e.y, e.z);
-    }
-#pragma unroll
-    for (int it = 0; it < SLAB * KT / 256; ++it) pl[it * 256 + tid] = g[it];
-    __syncthreads();
+  // prologue: tables for slabs 0 and 1, slab 0 staged
+  if (tid < KT) taps[tid] = tap_of(a, k0 + tid);
+  if (tid < SLAB) fill_rows(0);
+  __syncthreads();
+  load_slab(0);
+  store_slab();
+  if (tid < SLAB) fill_rows(1);
+  __syncthreads();
+  for (int sl = 0; sl < nslab; ++sl) {
+    // next slab's global loads fly while this one is consumed from LDS
+    if (sl + 1 < nslab) load_slab(sl + 1);
 #pragma unroll 4
     for (int rr = 0; rr < SLAB / 4; ++rr) {
       const int r = rr * 4 + wid;
@@ -265,6 +292,12 @@ __global__ void __launch_bounds__(256) conv_small_wgrad_kernel(SmallConvArgs a) 
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[c][j] += dv[c] * pv[j];
     }
+    __syncthreads();   // slab sl consumed; its row table slot is free
+    if (sl + 1 < nslab) {
+      store_slab();
+      if (tid < SLAB) fill_rows(sl + 2);
+    }
+    __syncthreads();
   }
   // sum the 4 waves: waves 1..3 park their tiles, wave 0 adds and stores
   __syncthreads();
@@ -292,19 +325,30 @@ __global__ void __launch_bounds__(256) conv_small_wgrad_kernel(SmallConvArgs a) 
   }
 }
 
-// dw[i] += sum_g ws[g][i]: one wave per 64 consecutive outputs, lanes stride G
+// dw[i] += sum_g ws[g][i]: block (x, y) sums outputs [64x, 64x+64) over the
+// y-th 1/16 of the G tiles (4 waves split it), one fp32 atomic per output
 __global__ void __launch_bounds__(256) conv_small_wgrad_reduce(const float* __restrict__ ws,
                                                                float* __restrict__ dw, int n,
                                                                int G) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int part = threadIdx.x >> 6;   // 4 waves split G
+  const int w = threadIdx.x >> 6;
+  const int g0 = (int)((long long)G * blockIdx.y / gridDim.y);
+  const int g1 = (int)((long long)G * (blockIdx.y + 1) / gridDim.y);
   __shared__ float red[4][64];
-  float v = 0.f;
-  if (i < n)
-    for (int g = part; g < G; g += 4) v += ws[(long long)g * n + i];
-  red[part][threadIdx.x & 63] = v;
+  float v0 = 0.f, v1 = 0.f;
+  if (i < n) {
+    int g = g0 + w;
+    for (; g + 4 < g1; g += 8) {
+      v0 += ws[(long long)g * n + i];
+      v1 += ws[(long long)(g + 4) * n + i];
+    }
+    for (; g < g1; g += 4) v0 += ws[(long long)g * n + i];
+  }
+  red[w][threadIdx.x & 63] = v0 + v1;
   __syncthreads();
-  if (threadIdx.x < 64 && i < n) dw[i] += red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  if (threadIdx.x < 64 && i < n)
+    atomicAdd(dw + i, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                          red[3][threadIdx.x]);
 }
 
 static SmallConvArgs small_args(const u16* x, int xbytes, int sb, int sh, int sw, int sc, int B, int H, int W, int CI, int OH, int OW, int CO,
@@ -331,15 +375,16 @@ void launch_conv_small_fwd(const u16* x, int xbytes, int sb, int sh, int sw, int
   a.y = y;
   a.part = part;
   const int Kp = (a.K + 7) / 8 * 8;
-  const size_t lds = (size_t)a.K * 64 * 4 + (size_t)Kp * 4;
+  const size_t lds = (size_t)((a.K * 64 + Kp + 3) & ~3) * 4 + 256 * kOutPitch * 2;
   const dim3 grid((unsigned)conv_small_fwd_blocks(a.P), (unsigned)(CO / 64));
   hipLaunchKernelGGL(conv_small_fwd_kernel, grid, dim3(256), lds, s, a);
 }
 
 int conv_small_wgrad_blocks(long long P, int CO, int R, int S, int CI) {
   (void)CO; (void)R; (void)S; (void)CI;
-  // one pixel chunk per CU; whole 64-pixel slabs
-  long long chunk = (P + 255) / 256;
+  // ~4 blocks (16 waves) per CU: one 4-wave block per CU leaves every SIMD a
+  // single wave and the LDS -> FMA chains unhidden; whole 64-pixel slabs
+  long long chunk = (P + 1023) / 1024;
   chunk = (chunk + 63) / 64 * 64;
   if (chunk < 256) chunk = 256;
   return (int)((P + chunk - 1) / chunk);
@@ -358,7 +403,8 @@ void launch_conv_small_wgrad(const u16* dy, const u16* x, int xbytes, int sb, in
   const dim3 grid((unsigned)G, (unsigned)(CO / 64), (unsigned)((a.K + 31) / 32));
   hipLaunchKernelGGL(conv_small_wgrad_kernel, grid, dim3(256), 0, s, a);
   const int n = CO * a.K;
-  hipLaunchKernelGGL(conv_small_wgrad_reduce, dim3((n + 63) / 64), dim3(256), 0, s, ws, dw, n, G);
+  hipLaunchKernelGGL(conv_small_wgrad_reduce, dim3((n + 63) / 64, 16), dim3(256), 0, s, ws, dw, n,
+                     G);
 }
 
 }  // namespace dmp
