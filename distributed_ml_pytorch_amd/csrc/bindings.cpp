@@ -43,12 +43,12 @@ T* ptr_or_null(const optional<Tensor>& t) {
 Tensor bn_slots(const optional<Tensor>& slots, int64_t C, const at::TensorOptions& opt) {
   if (slots.has_value() && slots->defined()) {
     TORCH_CHECK(slots->is_cuda() && slots->scalar_type() == at::kFloat && slots->is_contiguous() &&
-                    slots->numel() == 2 * dmp::kBnSlots * C,
+                    slots->numel() == 2 * dmp::kBnSlots * C + dmp::kBnTail,
                 "BN slot buffer must be a contiguous fp32 GPU tensor of 2*", dmp::kBnSlots,
-                "*C elements");
+                "*C+", dmp::kBnTail, " elements");
     return *slots;
   }
-  return at::zeros({2 * dmp::kBnSlots * C}, opt.dtype(at::kFloat));
+  return at::zeros({2 * dmp::kBnSlots * C + dmp::kBnTail}, opt.dtype(at::kFloat));
 }
 
 // ----------------------------------------------------------------- optimizer
@@ -690,7 +690,7 @@ std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optio
   const int64_t M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: bad C");
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
-                  G == dmp::kBnSlots && part.numel() == 2 * G * C,
+                  G == dmp::kBnSlots && part.numel() == 2 * G * C + dmp::kBnTail,
               "bad BN slot sums");
   if (res) {
     check_nhwc_bf16(*res, "res");

@@ -7,4 +7,7 @@ namespace dmp {
 // channel instead of one per producer block (thousands) and zeroes the slots
 // for their next use (they are persistent per layer).
 constexpr int kBnSlots = 64;
+// a slot buffer is [2][kBnSlots][C] fp32 followed by kBnTail words: word 0 is
+// the arrival ticket of the single-pass reduce + finalize (bn.hip)
+constexpr int kBnTail = 4;
 }  // namespace dmp

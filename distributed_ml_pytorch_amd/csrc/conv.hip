@@ -67,6 +67,27 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t rs, unsigned voff,
                "{m0}"(m0));
 }
 
+// q = n / d, r = n % d for 0 <= n < 2^24 with a float reciprocal (one
+// correction step); replaces the ~30-instruction integer division sequence in
+// per-lane index math whose dividend is a small in-tile offset
+__device__ __forceinline__ void small_divmod(int n, int d, float rcp, int& q, int& r) {
+  q = (int)((float)n * rcp);
+  r = n - q * d;
+  if (r < 0) { --q; r += d; }
+  else if (r >= d) { ++q; r -= d; }
+}
+
+// sum of v over the 16 lanes of each DPP row, valid in lane 15 of the row:
+// four v_add_f32_dpp row_shr steps (bound_ctrl zero-fills lanes shifted in
+// from outside the row) instead of four ds_bpermute round trips
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
+}
+
 // wait until at most N of this wave's vector-memory ops are outstanding (and
 // all of its LDS ops have completed)
 template <int N>
@@ -140,16 +161,23 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   int a_h[A_PW], a_w[A_PW];
   unsigned a_base[A_PW];
   bool a_ok[A_PW];
+  // the tile's first row decoded once (scalar), lanes step from it with small
+  // float-reciprocal divisions
+  const int m0i = (int)m0;
+  const int ow0 = m0i % RW, t0 = m0i / RW;
+  const int oh0 = t0 % RH, b0 = t0 / RH;
+  const float rcpW = 1.f / (float)RW, rcpH = 1.f / (float)RH;
 #pragma unroll
   for (int j = 0; j < A_PW; ++j) {
     const int ins = wid + j * NW;
     const int row = ins * RPI + lane / CPR;
     const int a_c = swz<BK>(row, lane % CPR) * 8;      // logical chunk this lane fetches
-    const int m = (int)m0 + row;
+    const int m = m0i + row;
     a_ok[j] = ins < A_INS && m < (int)Mc;
-    const int mm = a_ok[j] ? m : 0;
-    const int ow = mm % RW, t = mm / RW;
-    const int oh = t % RH, b = t / RH;
+    int q1, ow, q2, oh;
+    small_divmod(ow0 + (a_ok[j] ? row : 0), RW, rcpW, q1, ow);
+    small_divmod(oh0 + q1, RH, rcpH, q2, oh);
+    const int b = b0 + q2;
     if (MODE == 0) { a_h[j] = oh * st - a.pad; a_w[j] = ow * st - a.pad; }
     else           { a_h[j] = oh;              a_w[j] = ow; }
     // may wrap for a padded (negative) origin; only used when the tap is in range
@@ -261,7 +289,22 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   }
   __syncthreads();   // all ring reads done before the epilogue reuses LDS
 
-  // epilogue: D^T layout -> lane owns channels n..n+3 of output row m
+  // epilogue: D^T layout -> lane owns channels n..n+3 of output row m.
+  // Stores go through a buffer descriptor with 32-bit offsets; rows past M and
+  // channels past CO get an out-of-range offset and are dropped by the buffer
+  // unit (no per-tile branch).  Bias (fwd) is fetched once per column tile.
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.y, 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
+  float bj[TN][4];
+  bool nok[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+    nok[j] = n < a.CO;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bj[j][r] = (MODE == 0 && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
+  }
   float s_sum[TN][4], s_sq[TN][4];
   if (STATS) {
 #pragma unroll
@@ -272,48 +315,54 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const long long m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+    const bool mok = m < Mc;
     long long pix = m;
     if (MODE == 1) {
-      const long long mm = m < Mc ? m : 0;
-      const int j = (int)(mm % RW);
-      const long long t = mm / RW;
-      const int ii = (int)(t % RH);
-      const long long b = t / RH;
+      const int rloc = mok ? (int)(m - m0) : 0;
+      int q1, j, q2, ii;
+      small_divmod(ow0 + rloc, RW, rcpW, q1, j);
+      small_divmod(oh0 + q1, RH, rcpH, q2, ii);
+      const long long b = b0 + q2;
       pix = (b * a.OH + (long long)ii * st + ph) * a.OW + (long long)j * st + pw;
     }
+    const unsigned rowoff = 2u * (unsigned)(pix * a.CO);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
-      bf16x4 o;
+      u16 h[4];
+      float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        o.v[r] = f2bf(acc[i][j][r] + ((MODE == 0 && a.bias && n + r < a.CO) ? a.bias[n + r] : 0.f));
-      if (m < Mc && n < a.CO) {
-        *reinterpret_cast<bf16x4*>(a.y + pix * a.CO + n) = o;
-        if (STATS) {
+      for (int r = 0; r < 4; ++r) {
+        h[r] = f2bf(acc[i][j][r] + bj[j][r]);
+        v[r] = bf2f(h[r]);   // statistics of the stored (rounded) values
+      }
+      typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+      const u32x2_t packed = {(u32)h[0] | ((u32)h[1] << 16), (u32)h[2] | ((u32)h[3] << 16)};
+      const bool ok = mok && nok[j];
+      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
+      if (STATS) {
+        const float keep = ok ? 1.f : 0.f;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v = bf2f(o.v[r]);
-            s_sum[j][r] += v;
-            s_sq[j][r] += v * v;
-          }
+        for (int r = 0; r < 4; ++r) {
+          const float x = v[r] * keep;
+          s_sum[j][r] += x;
+          s_sq[j][r] += x * x;
         }
       }
     }
   }
   if (STATS) {
+    // sum over the 16 rows of each lane group with DPP row shifts (lane 15 of
+    // every 16-lane row ends up with the row total)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s_sum[j][r] += __shfl_xor(s_sum[j][r], o, 64);
-          s_sq[j][r] += __shfl_xor(s_sq[j][r], o, 64);
-        }
+        s_sum[j][r] = row_sum16(s_sum[j][r]);
+        s_sq[j][r] = row_sum16(s_sq[j][r]);
       }
     float* red = reinterpret_cast<float*>(lds);   // [WM][BN] sums, then [WM][BN] squares
-    if ((lane & 15) == 0) {
+    if ((lane & 15) == 15) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll

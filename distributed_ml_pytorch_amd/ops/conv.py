@@ -255,13 +255,15 @@ def small_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
 
 
 BN_SLOTS = 64   # csrc/bn_slots.h kBnSlots
+BN_TAIL = 4     # csrc/bn_slots.h kBnTail (arrival ticket)
 
 
 def bn_slot_buffer(owner, attr: str, channels: int, device):
-    """Persistent zeroed ``[2][BN_SLOTS][channels]`` fp32 slot buffer cached on ``owner``."""
+    """Persistent zeroed ``[2][BN_SLOTS][channels] + BN_TAIL`` fp32 slot buffer on ``owner``."""
+    n = 2 * BN_SLOTS * channels + BN_TAIL
     buf = getattr(owner, attr, None)
-    if buf is None or buf.device != device or buf.numel() != 2 * BN_SLOTS * channels:
-        buf = torch.zeros(2 * BN_SLOTS * channels, dtype=torch.float32, device=device)
+    if buf is None or buf.device != device or buf.numel() != n:
+        buf = torch.zeros(n, dtype=torch.float32, device=device)
         object.__setattr__(owner, attr, buf)
     return buf
 

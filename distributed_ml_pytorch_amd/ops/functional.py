@@ -120,7 +120,7 @@ class _BNAct(Function):
             # statistics already reduced per block by the producing conv's epilogue
             C = x.shape[1]
             y, stats = native().bn_fwd_from_partials(
-                x, part, part.numel() // (2 * C), residual, gamma, beta, running_mean,
+                x, part, (part.numel() - 4) // (2 * C), residual, gamma, beta, running_mean,
                 running_var, float(momentum), float(eps), bool(relu))
         else:
             y, stats = native().bn_fwd(x, residual, gamma, beta, running_mean, running_var,

@@ -56,6 +56,9 @@ def init_distributed(rank: int | None = None, world_size: int | None = None,
         os.environ["MASTER_ADDR"] = master
     if port:
         os.environ["MASTER_PORT"] = str(port)
+    # DMP_DIST_BACKEND=gloo rehearses the multi-rank GPU path with several ranks
+    # on one device (RCCL refuses two ranks per GPU)
+    backend = _env("DMP_DIST_BACKEND", backend)
     if backend == "auto":
         backend = "nccl" if use_cuda else "gloo"
     if not dist.is_initialized():

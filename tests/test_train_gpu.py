@@ -100,7 +100,7 @@ def test_graph_replay_matches_eager():
     res = {}
     for graph in (False, True):
         torch.manual_seed(0)
-        w = _worker("resnet18", n_push=3, n_pull=3, lr=0.05)
+        w = _worker("resnet18", n_push=3, n_pull=3, lr=0.01)
         w.enable_graph(graph)
         losses = []
         for x, y in zip(xs, ys):
@@ -112,7 +112,8 @@ def test_graph_replay_matches_eager():
     le, pe, ne = res[False]
     lg, pg, ng = res[True]
     assert ne == ng == 6
-    # wgrad uses fp32 atomics (order-dependent), so compare with a tolerance
+    # wgrad and the BN statistics use fp32 atomics (order-dependent sums), so
+    # the two runs differ by rounding that training amplifies: tolerance
     assert max(abs(a - b) for a, b in zip(le, lg)) < 5e-2, (le, lg)
     assert float((pe - pg).norm() / pe.norm()) < 1e-2
 
