@@ -30,6 +30,12 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+
+def _sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
 METRIC = "samples/sec (whole node) ResNet-18 ASGD at 1/2/4/8 MI355X; time-to-target-loss"
 
 
@@ -75,7 +81,7 @@ def time_to_target(a, cfg, info):
     pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device, n_batches=32,
                            dtype=w.compute_dtype, seed=100 + info.rank, learnable=True)
     barrier(info)
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     steps, reached, window = 0, False, []
     while steps < a.ttl_max_steps:
@@ -84,12 +90,18 @@ def time_to_target(a, cfg, info):
         window.append(loss.detach().float())
         steps += 1
         if steps % 10 == 0:
-            mean = float(torch.stack(window).mean().item())
+            m = torch.stack(window).mean().reshape(1)
             window.clear()
+            if info.is_distributed:
+                # every rank must take the same stop decision, or the ranks that keep
+                # training would block in a push collective the others never join
+                dist.all_reduce(m, op=dist.ReduceOp.SUM)
+                m /= info.world_size
+            mean = float(m.item())
             if mean <= a.ttl_target:
                 reached = True
                 break
-    torch.cuda.synchronize()
+    _sync()
     t = time.perf_counter() - t0
     w.finish()
     return {"time_to_target_s": round(t, 3), "ttl_target_loss": a.ttl_target,
@@ -120,12 +132,12 @@ def main():
         x, y = pool.next()
         loss, _ = w.train_step(x, y)
     barrier(info)
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         x, y = pool.next()
         loss, _ = w.train_step(x, y)
-    torch.cuda.synchronize()
+    _sync()
     barrier(info)
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], device=w.device, dtype=torch.float64)
@@ -136,7 +148,7 @@ def main():
     for _ in range(a.profile_steps):
         x, y = pool.next()
         w.train_step(x, y)
-    torch.cuda.synchronize()
+    _sync()
     in_shape = tuple(w.input_shape)
     w.finish()
     ttl = time_to_target(a, cfg, info) if a.ttl_target > 0 else None

@@ -225,3 +225,24 @@ def test_launcher_runs_reference_topology(tmp_path):
     assert os.path.exists(tmp_path / "log" / "node1.csv")
     assert os.path.exists(tmp_path / "log" / "node2.csv")
     assert "[ps] finished" in r.stdout
+
+
+def test_bench_two_ranks_sharded_ps_cpu():
+    """bench.py under torch.distributed.run with 2 gloo ranks: one JSON line from
+    rank 0 and every rank leaves the time-to-target phase together."""
+    import json
+
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--model", "lenet", "--batch", "16", "--n-push", "2", "--n-pull", "2",
+           "--ttl-target", "2.2", "--ttl-max-steps", "60"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["value"] > 0
+    assert out["config"]["global_batch"] == 32
+    assert "sharded" in out["config"]["parallelism"]
