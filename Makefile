@@ -1,0 +1,70 @@
+# Build / run recipes (the reference's Makefile targets, /root/reference/Makefile:1-39,
+# re-pointed at this framework: same role targets, plus the native build and tests).
+PY ?= python
+WORLD ?= 3
+NPROC ?= 8
+MASTER_PORT ?= 29500
+
+.PHONY: build install setup graph first second server single gpu launch launch-gpu bench \
+	bench-scale test test-gpu profile dist clean
+
+# compile every gfx950 HIP kernel + bindings into distributed_ml_pytorch_amd/_native*.so
+build:
+	$(PY) -m distributed_ml_pytorch_amd._build
+
+install: build
+	$(PY) -m pip install --no-build-isolation --no-deps -e .
+
+# (reference: virtualenv + requirements); here the ROCm image already carries torch
+setup: build
+
+graph:
+	mkdir -p docs
+	$(PY) example/graph.py log docs
+
+# three-process reference topology on one node: rank 0 = PS, ranks 1, 2 = workers
+first:
+	$(PY) example/main.py --rank 1 --world-size $(WORLD)
+
+second:
+	$(PY) example/main.py --rank 2 --world-size $(WORLD)
+
+server:
+	$(PY) example/main.py --rank 0 --world-size $(WORLD) --server
+
+single:
+	$(PY) example/main.py --no-distributed
+
+gpu:
+	$(PY) example/main.py --no-distributed --cuda
+
+# all roles at once (replaces the AzureML submit of run-pytorch.py)
+launch:
+	$(PY) run-pytorch.py --nproc $(WORLD) -- --model lenet
+
+launch-gpu:
+	$(PY) run-pytorch.py --nproc $(NPROC) --gpus -- --cuda --model resnet18 --ps sharded
+
+bench:
+	$(PY) bench.py
+
+bench-scale:
+	for n in 1 2 4 8; do \
+	  $(PY) -m torch.distributed.run --nnodes=1 --nproc-per-node $$n --master-addr 127.0.0.1 \
+	    --master-port $(MASTER_PORT) bench.py --gpus $$n || exit $$?; \
+	done
+
+test:
+	$(PY) -m pytest tests -x -q -m "not gpu"
+
+test-gpu:
+	$(PY) -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
+
+profile:
+	bash scripts/gpu_profile.sh
+
+dist:
+	$(PY) -m pip wheel --no-build-isolation --no-deps -w dist .
+
+clean:
+	rm -rf build dist distributed_ml_pytorch_amd/_native*.so
