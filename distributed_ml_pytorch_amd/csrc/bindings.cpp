@@ -1,3 +1,4 @@
+#include <cmath>
 // Python bindings for the gfx950 kernels. Every op checks device, dtype,
 // contiguity and alignment on the host before launching (a mis-shaped launch
 // of a hand-written kernel must fail loudly here, never fault on the GPU), and
@@ -508,6 +509,92 @@ void conv_small_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pa
                                cur_stream());
 }
 
+// ------------------------------------------------------- fused attention
+// qkv: [B, N, 3*H*64] bf16 rows of the qkv projection ([B, N, 3, H, 64])
+void check_attn(const Tensor& qkv, int64_t heads, int64_t& B, int64_t& N, int64_t& D) {
+  check_gpu(qkv, "qkv");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.is_contiguous() && qkv.dim() == 3,
+              "attention: qkv must be a contiguous bf16 [B, N, 3*D] tensor");
+  B = qkv.size(0);
+  N = qkv.size(1);
+  TORCH_CHECK(qkv.size(2) % 3 == 0, "attention: last dim must be 3*D");
+  D = qkv.size(2) / 3;
+  TORCH_CHECK(heads > 0 && D % heads == 0 && D / heads == dmp::attention_head_dim(),
+              "attention: head dim must be ", dmp::attention_head_dim());
+  TORCH_CHECK(N >= 1 && N <= dmp::attention_max_tokens(), "attention: 1 <= N <= ",
+              dmp::attention_max_tokens());
+}
+
+std::vector<Tensor> attention_fwd(Tensor qkv, int64_t heads) {
+  int64_t B, N, D;
+  check_attn(qkv, heads, B, N, D);
+  auto out = at::empty({B, N, D}, qkv.options());
+  auto lse = at::empty({B, heads, N}, qkv.options().dtype(at::kFloat));
+  dmp::launch_attention_fwd(reinterpret_cast<const uint16_t*>(qkv.data_ptr()),
+                            reinterpret_cast<uint16_t*>(out.data_ptr()), lse.data_ptr<float>(),
+                            (int)B, (int)N, (int)heads,
+                            1.f / std::sqrt((float)dmp::attention_head_dim()), cur_stream());
+  return {out, lse};
+}
+
+Tensor attention_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, int64_t heads) {
+  int64_t B, N, D;
+  check_attn(qkv, heads, B, N, D);
+  dout = dout.contiguous();
+  for (const Tensor* t : {&out, &dout}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
+                    t->numel() == B * N * D,
+                "attention_bwd: out / dout must be contiguous bf16 [B, N, D]");
+  }
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.numel() == B * heads * N,
+              "attention_bwd: bad lse");
+  auto dqkv = at::empty_like(qkv);
+  dmp::launch_attention_bwd(reinterpret_cast<const uint16_t*>(qkv.data_ptr()),
+                            reinterpret_cast<const uint16_t*>(out.data_ptr()),
+                            reinterpret_cast<const uint16_t*>(dout.data_ptr()),
+                            lse.data_ptr<float>(), reinterpret_cast<uint16_t*>(dqkv.data_ptr()),
+                            (int)B, (int)N, (int)heads,
+                            1.f / std::sqrt((float)dmp::attention_head_dim()), cur_stream());
+  return dqkv;
+}
+
+// ----------------------------------------------------------- bias gradients
+// out[n] += sum over rows of dy[..., n]; dy: bf16 with the channel dim
+// innermost in memory (contiguous [.., N] or channels_last NCHW)
+void colsum_acc(Tensor dy, Tensor out, optional<Tensor> slots) {
+  check_gpu(dy, "dy");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16, "colsum_acc: dy must be bf16");
+  int64_t N;
+  if (dy.dim() == 4) {
+    N = dy.size(1);
+    if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast))
+      dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  } else {
+    N = dy.size(-1);
+    dy = dy.contiguous();
+  }
+  TORCH_CHECK(N % 8 == 0, "colsum_acc: the summed-into dim must be a multiple of 8, got ", N);
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() &&
+                  out.numel() == N,
+              "colsum_acc: out must be a contiguous fp32 [N] GPU tensor");
+  const int64_t M = dy.numel() / N;
+  if (M == 0) return;
+  // per-device persistent zeroed scratch (every call re-zeroes it; calls on one
+  // stream are ordered, and a graph replays them in the same order)
+  const int64_t need = (int64_t)dmp::colsum_num_slots() * N;
+  Tensor sl;
+  if (slots.has_value() && slots->defined()) {
+    TORCH_CHECK(slots->is_cuda() && slots->scalar_type() == at::kFloat &&
+                    slots->is_contiguous() && slots->numel() >= need,
+                "colsum_acc: slots must be a zeroed contiguous fp32 GPU tensor of >= ", need);
+    sl = *slots;
+  } else {
+    sl = at::zeros({need}, out.options());
+  }
+  dmp::launch_colsum_acc(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                         out.data_ptr<float>(), sl.data_ptr<float>(), M, (int)N, cur_stream());
+}
+
 // ------------------------------------------------------------- transformer
 void check_rows_bf16(const Tensor& t, const char* name) {
   check_gpu(t, name);
@@ -520,8 +607,8 @@ std::vector<Tensor> layernorm_fwd(Tensor x, optional<Tensor> gamma, optional<Ten
   check_rows_bf16(x, "x");
   const int64_t D = x.size(-1);
   const int64_t rows = x.numel() / D;
-  TORCH_CHECK(D % 8 == 0 && D <= dmp::layernorm_max_dim(), "layernorm: D % 8 == 0, D <= ",
-              dmp::layernorm_max_dim());
+  TORCH_CHECK(dmp::layernorm_supported((int)D),
+              "layernorm: D must be a multiple of 8 with D/8 / lanes <= 8, got ", D);
   for (auto* t : {&gamma, &beta})
     if (t->has_value())
       TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == D &&
@@ -537,25 +624,41 @@ std::vector<Tensor> layernorm_fwd(Tensor x, optional<Tensor> gamma, optional<Ten
 }
 
 Tensor layernorm_bwd(Tensor x, Tensor dy, optional<Tensor> gamma, Tensor mean, Tensor rstd,
-                     optional<Tensor> dgamma, optional<Tensor> dbeta) {
+                     optional<Tensor> dgamma, optional<Tensor> dbeta, optional<Tensor> slots) {
   check_rows_bf16(x, "x");
   dy = dy.contiguous();
   check_rows_bf16(dy, "dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "layernorm_bwd: dy shape mismatch");
   const int64_t D = x.size(-1);
   const int64_t rows = x.numel() / D;
+  TORCH_CHECK(dmp::layernorm_supported((int)D), "layernorm_bwd: unsupported D ", D);
   TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_bwd: stats mismatch");
   for (auto* t : {&gamma, &dgamma, &dbeta})
     if (t->has_value())
       TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == D &&
                       (*t)->is_contiguous(), "layernorm gamma/dgamma/dbeta must be fp32 [D]");
+  // [kLnSlots][2][D] fp32 partial-sum slots: a persistent per-layer buffer (zero,
+  // re-zeroed by the param-grad kernel) or a fresh zeroed one
+  Tensor sl;
+  const bool grads = dgamma.has_value() || dbeta.has_value();
+  const int64_t nsl = (int64_t)dmp::layernorm_num_slots() * 2 * D;
+  if (grads) {
+    if (slots.has_value() && slots->defined()) {
+      TORCH_CHECK(slots->is_cuda() && slots->scalar_type() == at::kFloat &&
+                      slots->is_contiguous() && slots->numel() == nsl,
+                  "layernorm slots must be a contiguous fp32 GPU tensor of ", nsl, " elements");
+      sl = *slots;
+    } else {
+      sl = at::zeros({nsl}, x.options().dtype(at::kFloat));
+    }
+  }
   auto dx = at::empty_like(x);
   dmp::launch_layernorm_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                             reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                             ptr_or_null<float>(gamma), mean.data_ptr<float>(),
                             rstd.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
-                            ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta), rows, (int)D,
-                            cur_stream());
+                            ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta),
+                            grads ? sl.data_ptr<float>() : nullptr, rows, (int)D, cur_stream());
   return dx;
 }
 
@@ -745,7 +848,16 @@ PYBIND11_MODULE(_native, m) {
         py::arg("dy"), py::arg("y"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"), py::arg("slots") = py::none());
   m.def("layernorm_fwd", &layernorm_fwd, "row LayerNorm forward -> (y, mean, rstd)");
-  m.def("layernorm_bwd", &layernorm_bwd, "row LayerNorm backward (dgamma/dbeta accumulated)");
+  m.def("layernorm_bwd", &layernorm_bwd, "row LayerNorm backward (dgamma/dbeta accumulated)",
+        py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("slots") = py::none());
+  m.def("layernorm_num_slots", &dmp::layernorm_num_slots, "slot rows of the LayerNorm param grads");
+  m.def("colsum_acc", &colsum_acc, "bias gradient: out[n] += sum_m dy[m][n] (bf16 -> fp32)",
+        py::arg("dy"), py::arg("out"), py::arg("slots") = py::none());
+  m.def("colsum_num_slots", &dmp::colsum_num_slots, "slot rows of the colsum scratch");
+  m.def("attention_fwd", &attention_fwd, "fused MHSA forward on qkv rows -> (out, lse2)");
+  m.def("attention_bwd", &attention_bwd, "fused MHSA backward -> dqkv (qkv layout)");
+  m.def("attention_max_tokens", &dmp::attention_max_tokens, "max sequence length of the fused path");
   m.def("gelu_fwd", &gelu_fwd, "tanh-GELU forward");
   m.def("gelu_bwd", &gelu_bwd, "tanh-GELU backward");
   m.def("softmax_fwd", &softmax_fwd, "scaled row softmax forward");

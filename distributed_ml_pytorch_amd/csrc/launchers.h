@@ -53,13 +53,14 @@ void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, in
 
 
 // transformer.hip: LayerNorm / GELU / softmax (ViT)
-int layernorm_max_dim();
+bool layernorm_supported(int D);
+int layernorm_num_slots();
 void launch_layernorm_fwd(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
                           float* mean, float* rstd, long long rows, int D, float eps,
                           hipStream_t s);
 void launch_layernorm_bwd(const uint16_t* x, const uint16_t* dy, const float* gamma,
                           const float* mean, const float* rstd, uint16_t* dx, float* dgamma,
-                          float* dbeta, long long rows, int D, hipStream_t s);
+                          float* dbeta, float* slots, long long rows, int D, hipStream_t s);
 void launch_gelu_fwd(const uint16_t* x, uint16_t* y, long long n, hipStream_t s);
 void launch_gelu_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, long long n,
                      hipStream_t s);
@@ -76,9 +77,7 @@ void launch_dropout_apply_bf16(const uint16_t* x, const uint8_t* mask, uint16_t*
                                float scale, int mode, long long inner, int C, hipStream_t s);
 void launch_dropout_apply_f32(const float* x, const uint8_t* mask, float* y, long long n,
                               float scale, int mode, long long inner, int C, hipStream_t s);
-}  // namespace dmp
 
-namespace dmp {
 // conv.hip
 int conv_num_configs();
 void conv_config_info(int cfg, int* info);   // {BM, BN, BK, threads, stages}
@@ -108,91 +107,28 @@ void launch_conv_small_wgrad(const uint16_t* dy, const uint16_t* x, int xbytes, 
                              float* dw, float* ws, int B, int H, int W, int CI, int OH, int OW,
                              int CO, int R, int S, int stride, int pad, hipStream_t s);
 
-// transformer.hip: LayerNorm / GELU / softmax (ViT)
-int layernorm_max_dim();
-void launch_layernorm_fwd(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
-                          float* mean, float* rstd, long long rows, int D, float eps,
+// attention.hip: fused MHSA on [B, N, 3, H, 64] qkv rows (ViT)
+int attention_max_tokens();
+int attention_head_dim();
+void launch_attention_fwd(const uint16_t* qkv, uint16_t* out, float* lse2, int B, int N, int H,
+                          float scale, hipStream_t s);
+void launch_attention_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
+                          const float* lse2, uint16_t* dqkv, int B, int N, int H, float scale,
                           hipStream_t s);
-void launch_layernorm_bwd(const uint16_t* x, const uint16_t* dy, const float* gamma,
-                          const float* mean, const float* rstd, uint16_t* dx, float* dgamma,
-                          float* dbeta, long long rows, int D, hipStream_t s);
-void launch_gelu_fwd(const uint16_t* x, uint16_t* y, long long n, hipStream_t s);
-void launch_gelu_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, long long n,
-                     hipStream_t s);
-int softmax_max_len();
-void launch_softmax_fwd(const uint16_t* sc, uint16_t* p, long long rows, int L, float scale,
-                        hipStream_t s);
-void launch_softmax_bwd(const uint16_t* p, const uint16_t* dp, uint16_t* ds, long long rows, int L,
-                        float scale, hipStream_t s);
 
-// dropout.hip: Philox4x32-10 dropout
-void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
-                         const long long* offset, hipStream_t s);
-void launch_dropout_apply_bf16(const uint16_t* x, const uint8_t* mask, uint16_t* y, long long n,
-                               float scale, int mode, long long inner, int C, hipStream_t s);
-void launch_dropout_apply_f32(const float* x, const uint8_t* mask, float* y, long long n,
-                              float scale, int mode, long long inner, int C, hipStream_t s);
-}  // namespace dmp
+// linear.hip: bias gradient out[n] += sum_m dy[m][n] (bf16 dy, fp32 out)
+int colsum_num_slots();
+void launch_colsum_acc(const uint16_t* dy, float* out, float* slots, long long M, int N,
+                       hipStream_t s);
 
-namespace dmp {
+// bn.hip: BN forward from conv-epilogue slot sums (finalize + apply)
 void launch_bn_fwd_partials(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma,
                             const float* beta, float* running_mean, float* running_var,
                             float* stats, float* part, long long M, int C,
                             float momentum, float eps, bool relu, hipStream_t s);
 
-// transformer.hip: LayerNorm / GELU / softmax (ViT)
-int layernorm_max_dim();
-void launch_layernorm_fwd(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
-                          float* mean, float* rstd, long long rows, int D, float eps,
-                          hipStream_t s);
-void launch_layernorm_bwd(const uint16_t* x, const uint16_t* dy, const float* gamma,
-                          const float* mean, const float* rstd, uint16_t* dx, float* dgamma,
-                          float* dbeta, long long rows, int D, hipStream_t s);
-void launch_gelu_fwd(const uint16_t* x, uint16_t* y, long long n, hipStream_t s);
-void launch_gelu_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, long long n,
-                     hipStream_t s);
-int softmax_max_len();
-void launch_softmax_fwd(const uint16_t* sc, uint16_t* p, long long rows, int L, float scale,
-                        hipStream_t s);
-void launch_softmax_bwd(const uint16_t* p, const uint16_t* dp, uint16_t* ds, long long rows, int L,
-                        float scale, hipStream_t s);
-
-// dropout.hip: Philox4x32-10 dropout
-void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
-                         const long long* offset, hipStream_t s);
-void launch_dropout_apply_bf16(const uint16_t* x, const uint8_t* mask, uint16_t* y, long long n,
-                               float scale, int mode, long long inner, int C, hipStream_t s);
-void launch_dropout_apply_f32(const float* x, const uint8_t* mask, float* y, long long n,
-                              float scale, int mode, long long inner, int C, hipStream_t s);
-}  // namespace dmp
-
-namespace dmp {
+// conv.hip: every conv weight of a flat bf16 shadow transposed in one launch
 void launch_conv_weight_transpose_batched(const uint16_t* src, uint16_t* dst,
                                           const long long* table, int n, long long max_elems,
                                           hipStream_t s);
-
-// transformer.hip: LayerNorm / GELU / softmax (ViT)
-int layernorm_max_dim();
-void launch_layernorm_fwd(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
-                          float* mean, float* rstd, long long rows, int D, float eps,
-                          hipStream_t s);
-void launch_layernorm_bwd(const uint16_t* x, const uint16_t* dy, const float* gamma,
-                          const float* mean, const float* rstd, uint16_t* dx, float* dgamma,
-                          float* dbeta, long long rows, int D, hipStream_t s);
-void launch_gelu_fwd(const uint16_t* x, uint16_t* y, long long n, hipStream_t s);
-void launch_gelu_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, long long n,
-                     hipStream_t s);
-int softmax_max_len();
-void launch_softmax_fwd(const uint16_t* sc, uint16_t* p, long long rows, int L, float scale,
-                        hipStream_t s);
-void launch_softmax_bwd(const uint16_t* p, const uint16_t* dp, uint16_t* ds, long long rows, int L,
-                        float scale, hipStream_t s);
-
-// dropout.hip: Philox4x32-10 dropout
-void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
-                         const long long* offset, hipStream_t s);
-void launch_dropout_apply_bf16(const uint16_t* x, const uint8_t* mask, uint16_t* y, long long n,
-                               float scale, int mode, long long inner, int C, hipStream_t s);
-void launch_dropout_apply_f32(const float* x, const uint8_t* mask, float* y, long long n,
-                              float scale, int mode, long long inner, int C, hipStream_t s);
 }  // namespace dmp

@@ -25,142 +25,215 @@ __device__ __forceinline__ void st8(u16* p, const float v[8]) {
 }
 
 // ------------------------------------------------------------------ LayerNorm
+// A row of D = LR * nc * 8 elements is owned by LR consecutive lanes (a
+// power of two <= 64 that divides D / 8), each holding nc <= MAXC 16-B chunks
+// in registers: 64 / LR rows per wave, every lane busy (D = 768: 32 lanes x 3
+// chunks, 2 rows per wave).  Reductions are LR-lane butterflies.
+template <int LR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = LR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ void ld8f(const float* p, float v[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0];
+  const float4 b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 // y = (x - mean) * rstd * gamma + beta; saves mean, rstd (fp32 per row)
-template <int MAXC>
+template <int LR, int MAXC>
 __global__ void __launch_bounds__(256) layernorm_fwd_kernel(
     const u16* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
     u16* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out, long long rows,
     int D, float eps) {
-  const int lane = threadIdx.x & 63;
-  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const int nch = D >> 3;
-  const u16* xr = x + row * D;
+  constexpr int RPW = 64 / LR;
+  const int lane = threadIdx.x & 63, sub = lane % LR;
+  const long long row = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LR;
+  const int nc = D / (8 * LR);
+  const bool ok = row < rows;
+  const u16* xr = x + (ok ? row : 0) * D;
   float v[MAXC][8];
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int ch = lane + c * 64;
-    if (ch < nch) {
-      ld8(xr + ch * 8, v[c]);
+    if (c < nc) {
+      ld8(xr + (sub + c * LR) * 8, v[c]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s += v[c][k];
     }
   }
-  const float mean = wave_sum(s) / (float)D;
+  const float invD = 1.f / (float)D;
+  const float mean = group_sum<LR>(s) * invD;
   float q = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int ch = lane + c * 64;
-    if (ch < nch) {
+    if (c < nc) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float d = v[c][k] - mean;
-        q += d * d;
+        v[c][k] -= mean;
+        q += v[c][k] * v[c][k];
       }
     }
   }
-  const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+  const float rstd = rsqrtf(group_sum<LR>(q) * invD + eps);
+  if (!ok) return;
   u16* yr = y + row * D;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int ch = lane + c * 64;
-    if (ch < nch) {
-      float o[8];
+    if (c < nc) {
+      const int e0 = (sub + c * LR) * 8;
+      float g[8], b[8], o[8];
+      if (gamma) ld8f(gamma + e0, g);
+      if (beta) ld8f(beta + e0, b);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int d = ch * 8 + k;
-        o[k] = (v[c][k] - mean) * rstd * (gamma ? gamma[d] : 1.f) + (beta ? beta[d] : 0.f);
-      }
-      st8(yr + ch * 8, o);
+      for (int k = 0; k < 8; ++k)
+        o[k] = v[c][k] * rstd * (gamma ? g[k] : 1.f) + (beta ? b[k] : 0.f);
+      st8(yr + e0, o);
     }
   }
-  if (lane == 0) {
+  if (sub == 0) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
   }
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
-// dgamma += sum_rows dy * xhat, dbeta += sum_rows dy  (fp32 atomics per block)
-template <int MAXC>
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma.
+// dgamma / dbeta: per-lane partials over the rows the wave visits, folded over
+// the wave's row groups (butterfly) and the 4 waves (LDS), then added into
+// slot blockIdx % kLnSlots of a persistent [kLnSlots][2][D] buffer (<= 32
+// adders per address); layernorm_param_grad_kernel sums the slots into the
+// fp32 grad arena and re-zeroes them.  (One atomic per column per block into a
+// single row serialises at the memory-side atomic unit once ~1000 blocks add.)
+constexpr int kLnSlots = 32;
+
+template <int LR, int MAXC>
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, u16* __restrict__ dx,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, long long rows, int D) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int nch = D >> 3;
-  float pg[MAXC][8], pb[MAXC][8];   // per-lane dgamma / dbeta partials over this wave's rows
+    float* __restrict__ slots, long long rows, int D) {
+  constexpr int RPW = 64 / LR;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, sub = lane % LR;
+  const int nc = D / (8 * LR);
+  float pg[MAXC][8], pb[MAXC][8];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c)
 #pragma unroll
     for (int k = 0; k < 8; ++k) { pg[c][k] = 0.f; pb[c][k] = 0.f; }
-  for (long long row = (long long)blockIdx.x * 4 + wid; row < rows; row += (long long)gridDim.x * 4) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[MAXC][8], g[MAXC][8];
+  const long long step = (long long)gridDim.x * 4 * RPW;
+  for (long long row = ((long long)blockIdx.x * 4 + wid) * RPW + lane / LR; row - lane / LR < rows;
+       row += step) {
+    const bool ok = row < rows;
+    const long long r = ok ? row : 0;
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    float xh[MAXC][8], dv[MAXC][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      const int ch = lane + c * 64;
-      if (ch < nch) {
-        float dv[8];
-        ld8(x + row * D + ch * 8, xh[c]);
-        ld8(dy + row * D + ch * 8, dv);
+      if (c < nc) {
+        const int e0 = (sub + c * LR) * 8;
+        float gm[8];
+        ld8(x + r * D + e0, xh[c]);
+        ld8(dy + r * D + e0, dv[c]);
+        if (gamma) ld8f(gamma + e0, gm);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const int d = ch * 8 + k;
+          if (!ok) dv[c][k] = 0.f;
           xh[c][k] = (xh[c][k] - mean) * rstd;
-          g[c][k] = dv[k] * (gamma ? gamma[d] : 1.f);
-          s1 += g[c][k];
-          s2 += g[c][k] * xh[c][k];
-          pg[c][k] += dv[k] * xh[c][k];
-          pb[c][k] += dv[k];
+          const float g = dv[c][k] * (gamma ? gm[k] : 1.f);
+          s1 += g;
+          s2 += g * xh[c][k];
+          pg[c][k] += dv[c][k] * xh[c][k];
+          pb[c][k] += dv[c][k];
         }
       }
     }
-    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+    const float invD = 1.f / (float)D;
+    const float m1 = group_sum<LR>(s1) * invD, m2 = group_sum<LR>(s2) * invD;
+    if (ok) {
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      const int ch = lane + c * 64;
-      if (ch < nch) {
-        float o[8];
+      for (int c = 0; c < MAXC; ++c) {
+        if (c < nc) {
+          const int e0 = (sub + c * LR) * 8;
+          float gm[8], o[8];
+          if (gamma) ld8f(gamma + e0, gm);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = rstd * (g[c][k] - m1 - xh[c][k] * m2);
-        st8(dx + row * D + ch * 8, o);
+          for (int k = 0; k < 8; ++k)
+            o[k] = rstd * (dv[c][k] * (gamma ? gm[k] : 1.f) - m1 - xh[c][k] * m2);
+          st8(dx + r * D + e0, o);
+        }
       }
     }
   }
-  if (dgamma == nullptr && dbeta == nullptr) return;
-  // block reduce of the 4 waves' partials through LDS, then one atomic per
-  // column per block
-  extern __shared__ float red[];   // [2][4][D]
+  if (slots == nullptr) return;
+  // fold the RPW row groups of the wave (lanes sub, sub + LR, ...)
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    const int ch = lane + c * 64;
-    if (ch < nch) {
+  for (int o = LR; o < 64; o <<= 1) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        red[(0 * 4 + wid) * D + ch * 8 + k] = pg[c][k];
-        red[(1 * 4 + wid) * D + ch * 8 + k] = pb[c][k];
+        pg[c][k] += __shfl_xor(pg[c][k], o, 64);
+        pb[c][k] += __shfl_xor(pb[c][k], o, 64);
+      }
+  }
+  extern __shared__ float red[];   // [4][2][D]
+  if (lane < LR) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      if (c < nc) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int e = (sub + c * LR) * 8 + k;
+          red[(wid * 2 + 0) * D + e] = pg[c][k];
+          red[(wid * 2 + 1) * D + e] = pb[c][k];
+        }
       }
     }
   }
   __syncthreads();
-  for (int d = threadIdx.x; d < D; d += 256) {
-    const float sg = red[0 * D + d] + red[1 * D + d] + red[2 * D + d] + red[3 * D + d];
-    const float sb = red[4 * D + d] + red[5 * D + d] + red[6 * D + d] + red[7 * D + d];
-    if (dgamma) atomicAdd(dgamma + d, sg);
-    if (dbeta) atomicAdd(dbeta + d, sb);
+  float* out = slots + (long long)(blockIdx.x % kLnSlots) * 2 * D;
+  for (int e = threadIdx.x; e < 2 * D; e += 256) {
+    const float v = red[e] + red[2 * D + e] + red[4 * D + e] + red[6 * D + e];
+    atomicAdd(out + e, v);
   }
 }
 
+// dgamma[d] += sum_s slots[s][0][d], dbeta[d] += sum_s slots[s][1][d]; slots re-zeroed
+__global__ void __launch_bounds__(256) layernorm_param_grad_kernel(float* __restrict__ slots,
+                                                                   float* __restrict__ dgamma,
+                                                                   float* __restrict__ dbeta,
+                                                                   int D) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= 2 * D) return;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int sl = 0; sl < kLnSlots; ++sl) {
+    float* p = slots + (long long)sl * 2 * D + e;
+    acc += *p;
+    *p = 0.f;
+  }
+  float* dst = e < D ? dgamma : dbeta;
+  if (dst) dst[e < D ? e : e - D] += acc;
+}
+
 // ----------------------------------------------------------------------- GELU
+// tanh(u) = 1 - 2 / (1 + e^{2u}): one v_exp_f32 + one v_rcp_f32 instead of
+// the ~30-instruction libm tanhf (the GELU pass was VALU-bound with it).
+__device__ __forceinline__ float fast_tanh(float u) {
+  const float e = __expf(2.f * u);
+  return 1.f - 2.f * __frcp_rn(1.f + e);
+}
+
 __device__ __forceinline__ float gelu_tanh(float x, float* dgelu) {
   constexpr float c0 = 0.7978845608028654f, c1 = 0.044715f;
-  const float u = c0 * (x + c1 * x * x * x);
-  const float t = tanhf(u);
+  const float x2 = x * x;
+  const float u = c0 * x * (1.f + c1 * x2);
+  const float t = fast_tanh(u);
   if (dgelu) {
-    const float du = c0 * (1.f + 3.f * c1 * x * x);
+    const float du = c0 * (1.f + 3.f * c1 * x2);
     *dgelu = 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
   }
   return 0.5f * x * (1.f + t);
@@ -258,35 +331,65 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const u16* __restrict_
 }
 
 // ------------------------------------------------------------------ launchers
-#define DMP_LN_DISPATCH(MAXC_EXPR, KERNEL, ...)                                      \
-  do {                                                                                \
-    const int mc_ = (MAXC_EXPR);                                                      \
-    if (mc_ <= 1) hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__);                       \
-    else if (mc_ <= 2) hipLaunchKernelGGL((KERNEL<2>), __VA_ARGS__);                  \
-    else if (mc_ <= 4) hipLaunchKernelGGL((KERNEL<4>), __VA_ARGS__);                  \
-    else hipLaunchKernelGGL((KERNEL<8>), __VA_ARGS__);                                \
+int layernorm_num_slots() { return kLnSlots; }
+
+// lanes per row: the largest power of two <= 64 dividing D/8; chunks per lane <= 8
+static int ln_lanes(int D) {
+  const int nch = D / 8;
+  int lr = 64;
+  while (lr > 1 && nch % lr) lr >>= 1;
+  while (lr > 1 && nch / lr < 1) lr >>= 1;
+  return lr;
+}
+
+#define DMP_LN_LAUNCH(KERNEL, LR_, NC_, GRID, LDS, ...)                                         \
+  do {                                                                                         \
+    if ((NC_) <= 2) hipLaunchKernelGGL((KERNEL<LR_, 2>), GRID, dim3(256), LDS, s, __VA_ARGS__); \
+    else if ((NC_) == 3) hipLaunchKernelGGL((KERNEL<LR_, 3>), GRID, dim3(256), LDS, s, __VA_ARGS__); \
+    else if ((NC_) <= 4) hipLaunchKernelGGL((KERNEL<LR_, 4>), GRID, dim3(256), LDS, s, __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL<LR_, 8>), GRID, dim3(256), LDS, s, __VA_ARGS__);            \
   } while (0)
 
-int layernorm_max_dim() { return 8 * 64 * 8; }
+#define DMP_LN_BY_LR(KERNEL, LR, NC, GRID, LDS, ...)                         \
+  do {                                                                     \
+    switch (LR) {                                                          \
+      case 64: DMP_LN_LAUNCH(KERNEL, 64, NC, GRID, LDS, __VA_ARGS__); break; \
+      case 32: DMP_LN_LAUNCH(KERNEL, 32, NC, GRID, LDS, __VA_ARGS__); break; \
+      case 16: DMP_LN_LAUNCH(KERNEL, 16, NC, GRID, LDS, __VA_ARGS__); break; \
+      case 8: DMP_LN_LAUNCH(KERNEL, 8, NC, GRID, LDS, __VA_ARGS__); break;   \
+      case 4: DMP_LN_LAUNCH(KERNEL, 4, NC, GRID, LDS, __VA_ARGS__); break;   \
+      case 2: DMP_LN_LAUNCH(KERNEL, 2, NC, GRID, LDS, __VA_ARGS__); break;   \
+      default: DMP_LN_LAUNCH(KERNEL, 1, NC, GRID, LDS, __VA_ARGS__); break;  \
+    }                                                                      \
+  } while (0)
+
+// D % 8 == 0 and at most 8 chunks of 8 per lane
+bool layernorm_supported(int D) { return D > 0 && D % 8 == 0 && D / 8 / ln_lanes(D) <= 8; }
 
 void launch_layernorm_fwd(const u16* x, const float* gamma, const float* beta, u16* y,
                           float* mean, float* rstd, long long rows, int D, float eps,
                           hipStream_t s) {
-  const int chunks = (D / 8 + 63) / 64;
-  const dim3 grid((unsigned)((rows + 3) / 4));
-  DMP_LN_DISPATCH(chunks, layernorm_fwd_kernel, grid, dim3(256), 0, s, x, gamma, beta, y, mean, rstd,
-                  rows, D, eps);
+  const int lr = ln_lanes(D), nc = D / 8 / lr;
+  const long long rows_per_block = 4LL * (64 / lr);
+  const dim3 grid((unsigned)((rows + rows_per_block - 1) / rows_per_block));
+  DMP_LN_BY_LR(layernorm_fwd_kernel, lr, nc, grid, 0, x, gamma, beta, y, mean, rstd, rows, D, eps);
 }
 
+// slots: [kLnSlots][2][D] fp32, zero on entry and on return (nullptr: no param grads)
 void launch_layernorm_bwd(const u16* x, const u16* dy, const float* gamma, const float* mean,
-                          const float* rstd, u16* dx, float* dgamma, float* dbeta, long long rows,
-                          int D, hipStream_t s) {
-  const int chunks = (D / 8 + 63) / 64;
-  long long blocks = (rows + 3) / 4;
-  if (blocks > 256) blocks = 256;   // rows per wave grow; atomics per column = blocks
-  const size_t lds = (size_t)8 * D * sizeof(float);
-  DMP_LN_DISPATCH(chunks, layernorm_bwd_kernel, dim3((unsigned)blocks), dim3(256), lds, s, x, dy,
-                  gamma, mean, rstd, dx, dgamma, dbeta, rows, D);
+                          const float* rstd, u16* dx, float* dgamma, float* dbeta, float* slots,
+                          long long rows, int D, hipStream_t s) {
+  const int lr = ln_lanes(D), nc = D / 8 / lr;
+  const long long rows_per_block = 4LL * (64 / lr);
+  long long blocks = (rows + rows_per_block - 1) / rows_per_block;
+  if (blocks > 1024) blocks = 1024;   // <= 32 blocks add into each slot row
+  const bool grads = slots != nullptr && (dgamma != nullptr || dbeta != nullptr);
+  const size_t lds = grads ? (size_t)8 * D * sizeof(float) : 0;
+  DMP_LN_BY_LR(layernorm_bwd_kernel, lr, nc, dim3((unsigned)blocks), lds, x, dy, gamma, mean, rstd,
+               dx, grads ? slots : nullptr, rows, D);
+  if (grads)
+    hipLaunchKernelGGL(layernorm_param_grad_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s,
+                       slots, dgamma, dbeta, D);
 }
 
 void launch_gelu_fwd(const u16* x, u16* y, long long n, hipStream_t s) {

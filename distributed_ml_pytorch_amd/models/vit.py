@@ -2,10 +2,12 @@
 
 Not in the reference (no sequence models there).  ViT-B/16 at
 224x224 = 197 tokens, D=768, 12 heads, MLP 3072, 86,567,656 parameters with a
-1000-class head.  LayerNorm, tanh-GELU and the attention softmax are native
-kernels (``csrc/transformer.hip``); the projection / attention GEMMs are plain
-library GEMMs (hipBLASLt through ``F.linear`` / ``torch.matmul``) whose weight
-gradients accumulate in fp32 straight into the grad arena (``ops.linear``).
+1000-class head.  LayerNorm and tanh-GELU are native kernels
+(``csrc/transformer.hip``), multi-head attention is one fused MFMA kernel per
+direction on the qkv rows (``csrc/attention.hip``); the projection / MLP GEMMs
+are plain library GEMMs (hipBLASLt through ``F.linear``) whose weight gradients
+accumulate in fp32 straight into the grad arena (``ops.linear``) and whose bias
+gradients are one native column-sum pass (``csrc/linear.hip``).
 Patch embedding is a stride-16 conv.
 """
 from __future__ import annotations
@@ -23,7 +25,14 @@ from ..ops.functional import compute_weight
 
 class LayerNorm(nn.LayerNorm):
     def forward(self, x):
-        return DF.layer_norm(x, self.weight, self.bias, self.eps)
+        slots = None
+        if x.is_cuda and self.weight is not None and self.weight.requires_grad:
+            n = DF.LN_SLOTS * 2 * x.shape[-1]
+            slots = self.__dict__.get("_dmp_slots")
+            if slots is None or slots.device != x.device or slots.numel() != n:
+                slots = torch.zeros(n, dtype=torch.float32, device=x.device)
+                self.__dict__["_dmp_slots"] = slots
+        return DF.layer_norm(x, self.weight, self.bias, self.eps, slots)
 
 
 class Attention(nn.Module):
@@ -34,11 +43,9 @@ class Attention(nn.Module):
         self.proj = L.Linear(dim, dim)
 
     def forward(self, x):
-        B, N, D = x.shape
-        qkv = self.qkv(x).view(B, N, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
-        q, k, v = qkv[0], qkv[1], qkv[2]
-        o = DF.attention(q, k, v)
-        return self.proj(o.transpose(1, 2).reshape(B, N, D))
+        # fused MFMA attention on the qkv rows as they come out of the projection
+        # (csrc/attention.hip); SDPA / matmul + native softmax elsewhere
+        return self.proj(DF.attention_qkv(self.qkv(x), self.heads))
 
 
 class Block(nn.Module):

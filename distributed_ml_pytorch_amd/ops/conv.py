@@ -191,14 +191,16 @@ class _NativeConv(Function):
         gb = None
         bias = ctx.bias
         if bias is not None and bias.requires_grad:
-            col = dy.sum(dim=(0, 2, 3), dtype=torch.float32)
-            if getattr(bias, "_dmp_arena", False) and bias.grad is not None:
-                bias.grad.add_(col)
+            if (getattr(bias, "_dmp_arena", False) and bias.grad is not None
+                    and dy.shape[1] % 8 == 0):
+                from .linear import bias_grad_acc
+
+                bias_grad_acc(dy, bias.grad)
                 cb = getattr(bias, "_dmp_grad_ready", None)
                 if cb is not None:
                     cb(bias)
             else:
-                gb = col.to(bias.dtype)
+                gb = dy.sum(dim=(0, 2, 3), dtype=torch.float32).to(bias.dtype)
         return dx, None, gw, None, None, None, None, gb
 
 

@@ -272,13 +272,13 @@ def dropout(x, p: float, training: bool, channelwise: bool = False, state=None, 
 # ----------------------------------------------------------------- layernorm
 class _LayerNorm(Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps):
+    def forward(ctx, x, gamma, beta, eps, slots=None):
         x = x.contiguous()
         g32 = gamma.detach() if gamma is not None else None
         b32 = beta.detach() if beta is not None else None
         y, mean, rstd = native().layernorm_fwd(x, g32, b32, float(eps))
         ctx.save_for_backward(x, mean, rstd)
-        ctx.gamma, ctx.beta = gamma, beta
+        ctx.gamma, ctx.beta, ctx.slots = gamma, beta, slots
         return y
 
     @staticmethod
@@ -293,21 +293,36 @@ class _LayerNorm(Function):
         db = db_arena if db_arena is not None else (
             torch.zeros_like(beta, dtype=torch.float32) if need_b else None)
         g32 = gamma.detach() if gamma is not None else None
-        dx = native().layernorm_bwd(x, dy, g32, mean, rstd, dg, db)
+        dx = native().layernorm_bwd(x, dy, g32, mean, rstd, dg, db, ctx.slots)
         if dg_arena is not None or db_arena is not None:
             _notify(gamma, beta)
         ret_g = None if (dg_arena is not None or not need_g) else dg.to(gamma.dtype)
         ret_b = None if (db_arena is not None or not need_b) else db.to(beta.dtype)
-        return dx, ret_g, ret_b, None
+        return dx, ret_g, ret_b, None, None
 
 
-def layer_norm(x, weight, bias, eps: float):
+LN_SLOTS = 32   # csrc/transformer.hip kLnSlots
+
+
+def layernorm_supported(D: int) -> bool:
+    """Mirror of csrc/transformer.hip layernorm_supported: D % 8 == 0 and at most 8
+    16-B chunks per lane with the widest power-of-two lane group dividing D/8."""
+    if D <= 0 or D % 8:
+        return False
+    nch, lr = D // 8, 64
+    while lr > 1 and nch % lr:
+        lr //= 2
+    return nch // lr <= 8
+
+
+def layer_norm(x, weight, bias, eps: float, slots=None):
     """LayerNorm over the last dim: native row kernel for bf16 GPU input with fp32
-    affine params (``csrc/transformer.hip``), PyTorch otherwise."""
-    if (x.is_cuda and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0 and x.shape[-1] <= 4096
+    affine params (``csrc/transformer.hip``), PyTorch otherwise.  ``slots``: the
+    layer's persistent zeroed ``[LN_SLOTS * 2 * D]`` fp32 param-grad slot buffer."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and layernorm_supported(x.shape[-1])
             and (weight is None or weight.dtype == torch.float32)
             and (bias is None or bias.dtype == torch.float32)):
-        return _LayerNorm.apply(x, weight, bias, eps)
+        return _LayerNorm.apply(x, weight, bias, eps, slots)
     w = compute_weight(weight, x.dtype)
     b = compute_weight(bias, x.dtype)
     return F.layer_norm(x, (x.shape[-1],), w, b, eps)
@@ -347,6 +362,47 @@ class _ScaledSoftmax(Function):
     def backward(ctx, dp):
         (p,) = ctx.saved_tensors
         return native().softmax_bwd(p, dp, float(ctx.scale)), None
+
+
+class _FusedQKVAttention(Function):
+    @staticmethod
+    def forward(ctx, qkv, heads):
+        qkv = qkv.contiguous()
+        out, lse = native().attention_fwd(qkv, int(heads))
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.heads = int(heads)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        return native().attention_bwd(qkv, out, dout, lse, ctx.heads), None
+
+
+def fused_attention_supported(qkv, heads: int) -> bool:
+    if not (qkv.is_cuda and qkv.dtype == torch.bfloat16 and qkv.dim() == 3):
+        return False
+    D = qkv.shape[-1] // 3
+    return (qkv.shape[-1] % 3 == 0 and D % heads == 0 and D // heads == 64
+            and 1 <= qkv.shape[1] <= 256)
+
+
+def attention_qkv(qkv, heads: int):
+    """Multi-head self-attention straight from the qkv projection rows.
+
+    ``qkv``: [B, N, 3*D] (= [B, N, 3, heads, D/heads]); returns [B, N, D] (the
+    proj Linear's input rows).  On GPU (head dim 64, N <= 256) this is the
+    fused MFMA kernel pair of ``csrc/attention.hip``: scores never leave the
+    chip and the backward writes d(qkv) in place of the qkv layout (no
+    permute copies, zero fills or gradient adds).  Elsewhere: SDPA.
+    """
+    B, N, three_d = qkv.shape
+    D = three_d // 3
+    if fused_attention_supported(qkv, heads):
+        return _FusedQKVAttention.apply(qkv, heads)
+    q, k, v = qkv.view(B, N, 3, heads, D // heads).permute(2, 0, 3, 1, 4)
+    o = attention(q, k, v)
+    return o.transpose(1, 2).reshape(B, N, D)
 
 
 def attention(q, k, v):

@@ -5,8 +5,8 @@ Forward and data gradient are plain bf16 GEMMs (hipBLASLt through
 cast.  The weight gradient is ONE bf16 x bf16 -> fp32 GEMM that accumulates
 straight into the fp32 arena gradient view (``addmm`` with an fp32
 ``out_dtype``, ``beta = 1``): no bf16 weight-gradient tensor, no mixed-dtype
-add kernel, no AccumulateGrad.  The bias gradient is an fp32 column sum added
-in place.  Both fire the parameter's grad-ready hook (bucketed all-reduce in
+add kernel, no AccumulateGrad.  The bias gradient is one native column-sum
+pass (``csrc/linear.hip``) adding straight into the fp32 arena view.  Both fire the parameter's grad-ready hook (bucketed all-reduce in
 sync DP) as soon as they land.
 
 Parity: the reference's ``nn.Linear`` layers (/root/reference/example/models.py
@@ -18,7 +18,30 @@ import torch
 import torch.nn.functional as F
 from torch.autograd import Function
 
+from ._ext import native
 from .functional import _notify
+
+
+_COLSUM_SCRATCH: dict = {}
+
+
+def colsum_scratch(device, n: int) -> torch.Tensor:
+    """Per-device zeroed fp32 slot scratch of the bias-grad column sum
+    (csrc/linear.hip); every call leaves it zeroed, and calls on one stream are
+    ordered, so all layers share it."""
+    need = native().colsum_num_slots() * n
+    buf = _COLSUM_SCRATCH.get(device)
+    if buf is None or buf.numel() < need:
+        buf = torch.zeros(max(need, native().colsum_num_slots() * 4096), dtype=torch.float32,
+                          device=device)
+        _COLSUM_SCRATCH[device] = buf
+    return buf
+
+
+def bias_grad_acc(dy, out):
+    """``out += dy`` summed over every dim but the channel/last one (native, one pass)."""
+    n = out.numel()
+    native().colsum_acc(dy, out, colsum_scratch(dy.device, n))
 
 
 def _arena_grad(p):
@@ -51,12 +74,20 @@ class _ArenaLinear(Function):
         elif w is not None and w.requires_grad:
             gw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).to(w.dtype)
         if b is not None and b.requires_grad:
-            col = dy2.sum(0, dtype=torch.float32)
             g = _arena_grad(b)
+            vec = dy2.dtype == torch.bfloat16 and N % 8 == 0    # 16-B column chunks
             if g is not None:
-                g.add_(col)
+                if vec:
+                    bias_grad_acc(dy2, g)        # one pass straight into the arena
+                else:
+                    g.add_(dy2.sum(0, dtype=torch.float32))
                 _notify(b)
             else:
+                col = torch.zeros(N, dtype=torch.float32, device=dy.device)
+                if vec:
+                    bias_grad_acc(dy2, col)
+                else:
+                    col += dy2.sum(0, dtype=torch.float32)
                 gb = col.to(b.dtype)
         return dx, None, None, gw, gb
 

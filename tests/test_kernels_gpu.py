@@ -232,27 +232,53 @@ def test_dropout_kernel(mode, dtype):
     assert layer(x) is x
 
 
-@pytest.mark.parametrize("D", [768, 192, 4096])
-def test_layernorm_kernel(D):
-    from distributed_ml_pytorch_amd.ops.functional import layer_norm
+@pytest.mark.parametrize("rows,D", [(111, 768), (111, 192), (111, 4096), (111, 64), (37, 24),
+                                    (12608, 768), (5000, 1024)])
+def test_layernorm_kernel(rows, D):
+    """Native LayerNorm fwd/bwd vs fp32 PyTorch; the persistent param-grad slot
+    buffer must come back zeroed, so a second backward with it is exact too."""
+    from distributed_ml_pytorch_amd.ops.functional import LN_SLOTS, layer_norm, layernorm_supported
+
+    assert layernorm_supported(D)
+    torch.manual_seed(0)
+    slots = torch.zeros(LN_SLOTS * 2 * D, device="cuda")
+    rel = lambda a, r: float((a.float() - r).norm() / r.norm())
+    for _ in range(2):
+        x = (torch.randn(rows, D, device="cuda") * 2 + 0.5).to(torch.bfloat16).requires_grad_(True)
+        w = (1 + 0.1 * torch.randn(D, device="cuda")).requires_grad_(True)
+        b = (0.1 * torch.randn(D, device="cuda")).requires_grad_(True)
+        y = layer_norm(x, w, b, 1e-6, slots)
+        xr = x.detach().float().requires_grad_(True)
+        wr = w.detach().clone().requires_grad_(True)
+        br = b.detach().clone().requires_grad_(True)
+        yr = F.layer_norm(xr, (D,), wr, br, 1e-6)
+        torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+        g = torch.randn_like(yr)
+        y.backward(g.to(torch.bfloat16))
+        yr.backward(g.to(torch.bfloat16).float())
+        assert rel(x.grad, xr.grad) < 1e-2
+        assert rel(w.grad, wr.grad) < 1e-2
+        assert rel(b.grad, br.grad) < 1e-2
+        assert float(slots.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("M,N", [(12608, 768), (300, 3072), (7, 8), (1000, 4104)])
+def test_colsum_acc(M, N):
+    from distributed_ml_pytorch_amd.ops._ext import native
 
     torch.manual_seed(0)
-    x = (torch.randn(3, 37, D, device="cuda") * 2 + 0.5).to(torch.bfloat16).requires_grad_(True)
-    w = (1 + 0.1 * torch.randn(D, device="cuda")).requires_grad_(True)
-    b = (0.1 * torch.randn(D, device="cuda")).requires_grad_(True)
-    y = layer_norm(x, w, b, 1e-6)
-    xr = x.detach().float().requires_grad_(True)
-    wr = w.detach().clone().requires_grad_(True)
-    br = b.detach().clone().requires_grad_(True)
-    yr = F.layer_norm(xr, (D,), wr, br, 1e-6)
-    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
-    g = torch.randn_like(yr)
-    y.backward(g.to(torch.bfloat16))
-    yr.backward(g.to(torch.bfloat16).float())
-    rel = lambda a, r: float((a.float() - r).norm() / r.norm())
-    assert rel(x.grad, xr.grad) < 1e-2
-    assert rel(w.grad, wr.grad) < 1e-2
-    assert rel(b.grad, br.grad) < 1e-2
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    out = torch.randn(N, device="cuda")
+    ref = out + dy.float().sum(0)
+    slots = torch.zeros(native().colsum_num_slots() * N, device="cuda")
+    native().colsum_acc(dy, out, slots)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-2)
+    assert float(slots.abs().max()) == 0.0
+    x4 = torch.randn(4, 64, 5, 7, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    o4 = torch.zeros(64, device="cuda")
+    native().colsum_acc(x4, o4)
+    torch.testing.assert_close(o4, x4.float().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
 
 
 def test_gelu_kernel():
@@ -286,3 +312,28 @@ def test_attention_softmax(N):
     orf.backward(g.to(torch.bfloat16).float())
     for a, r in ((q, qr), (k, kr), (v, vr)):
         assert rel(a.grad, r.grad) < 3e-2
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (3, 65, 2), (1, 256, 1), (2, 5, 3), (4, 32, 4)])
+def test_fused_qkv_attention(B, N, H):
+    """csrc/attention.hip fwd + bwd vs fp32 SDPA on the same qkv rows."""
+    from distributed_ml_pytorch_amd.ops.functional import attention_qkv, fused_attention_supported
+
+    torch.manual_seed(0)
+    D = 64 * H
+    qkv = torch.randn(B, N, 3 * D, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    assert fused_attention_supported(qkv, H)
+    o = attention_qkv(qkv, H)
+    qr = qkv.detach().float().requires_grad_(True)
+    q, k, v = qr.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    orf = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, N, D)
+    rel = lambda a, r: float((a.float() - r).norm() / r.norm())
+    assert o.shape == (B, N, D)
+    assert rel(o, orf) < 1e-2, rel(o, orf)
+    g = torch.randn_like(orf).to(torch.bfloat16)
+    o.backward(g)
+    orf.backward(g.float())
+    for t in range(3):
+        a = qkv.grad.view(B, N, 3, D)[:, :, t]
+        r = qr.grad.view(B, N, 3, D)[:, :, t]
+        assert rel(a, r) < 2e-2, (t, rel(a, r))
