@@ -3,9 +3,10 @@
 Forward and data gradient are plain bf16 GEMMs (hipBLASLt through
 ``F.linear`` / ``matmul``) on the arena's bf16 weight shadow, so no per-step
 cast.  The weight gradient is ONE bf16 x bf16 -> fp32 GEMM that accumulates
-straight into the fp32 arena gradient view (``addmm`` with an fp32
-``out_dtype``, ``beta = 1``): no bf16 weight-gradient tensor, no mixed-dtype
-add kernel, no AccumulateGrad.  The bias gradient is one native column-sum
+straight into the fp32 arena gradient view -- the native MFMA wgrad kernel
+(a 1x1 convolution's weight gradient) when the dims are multiples of 64,
+else ``addmm`` with an fp32 ``out_dtype`` and ``beta = 1``: no bf16
+weight-gradient tensor, no mixed-dtype add kernel, no AccumulateGrad.  The bias gradient is one native column-sum
 pass (``csrc/linear.hip``) adding straight into the fp32 arena view.  Both fire the parameter's grad-ready hook (bucketed all-reduce in
 sync DP) as soon as they land.
 
@@ -51,6 +52,31 @@ def _arena_grad(p):
     return g if g is not None and g.is_contiguous() else None
 
 
+def _native_wgrad_ok(dy2, x2) -> bool:
+    M, N = dy2.shape
+    K = x2.shape[1]
+    return (dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and N % 64 == 0
+            and K % 64 == 0 and M * max(N, K) * 2 < (1 << 30)
+            and dy2.is_contiguous() and x2.is_contiguous())
+
+
+def _native_wgrad(dy2, x2, g):
+    """g[N, K] += dy2^T @ x2 as a 1x1 convolution weight gradient on the native
+    MFMA wgrad kernel (csrc/conv_wgrad.hip): fp32 atomics straight into the
+    arena.  Measured against hipBLASLt's fp32-output addmm on the ViT-B/16
+    shapes (scripts/linear_vs_conv1x1.py, profiles/linear_vs_conv1x1_r1.txt):
+    1.1-2x faster; forward / dgrad stay on hipBLASLt (it wins those)."""
+    from .conv import _wgrad_cfg
+
+    M, N = dy2.shape
+    K = x2.shape[1]
+    dy4 = dy2.view(M, 1, 1, N).permute(0, 3, 1, 2)     # NCHW view of NHWC memory
+    x4 = x2.view(M, 1, 1, K).permute(0, 3, 1, 2)
+    g4 = g.view(N, K, 1, 1)
+    cfg = _wgrad_cfg(dy4, x4, (N, K, 1, 1), 1, 0)
+    native().conv_wgrad(dy4, x4, g4, 1, 0, cfg)
+
+
 class _ArenaLinear(Function):
     @staticmethod
     def forward(ctx, x, w16, b16, w, b):
@@ -69,7 +95,10 @@ class _ArenaLinear(Function):
         gw = gb = None
         g = _arena_grad(w)
         if g is not None:
-            torch.ops.aten.addmm.dtype_out(g, dy2.t(), x2, torch.float32, out=g)
+            if _native_wgrad_ok(dy2, x2):
+                _native_wgrad(dy2, x2, g)
+            else:
+                torch.ops.aten.addmm.dtype_out(g, dy2.t(), x2, torch.float32, out=g)
             _notify(w)
         elif w is not None and w.requires_grad:
             gw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).to(w.dtype)

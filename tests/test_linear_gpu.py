@@ -6,6 +6,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("M,K,N,bias", [(256, 512, 10, True), (96, 768, 3072, True),
+                                        (394, 3072, 768, True),
                                         (33, 120, 84, False)])
 def test_arena_linear_grads(M, K, N, bias):
     from distributed_ml_pytorch_amd.ops import layers as L
