@@ -280,37 +280,40 @@ Tensor gap_bwd(Tensor dy, int64_t H, int64_t W) {
   return dx;
 }
 
-std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K) {
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K, int64_t S, int64_t P) {
+  if (S < 0) S = K;
   check_nhwc_bf16(x, "x");
   TORCH_CHECK(x.dim() == 4, "maxpool expects 4-D input");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
-  TORCH_CHECK(C % 8 == 0 && K >= 1 && K <= 15, "maxpool: C % 8 == 0 and 1 <= K <= 15");
-  const int Ho = H / (int)K, Wo = W / (int)K;
+  TORCH_CHECK(C % 8 == 0 && K >= 1 && K <= 15 && S >= 1 && P >= 0 && 2 * P <= K,
+              "maxpool: C % 8 == 0, 1 <= K <= 15, S >= 1, 0 <= P <= K/2");
+  const int Ho = dmp::maxpool_out(H, (int)K, (int)S, (int)P);
+  const int Wo = dmp::maxpool_out(W, (int)K, (int)S, (int)P);
   TORCH_CHECK(Ho > 0 && Wo > 0, "maxpool: window larger than input");
   auto mf = at::MemoryFormat::ChannelsLast;
   auto y = at::empty({N, C, Ho, Wo}, x.options().memory_format(mf));
   auto idx = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(mf));
   dmp::launch_maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                           reinterpret_cast<uint16_t*>(y.data_ptr()), idx.data_ptr<uint8_t>(), N, H,
-                          W, C, (int)K, cur_stream());
+                          W, C, (int)K, (int)S, (int)P, cur_stream());
   return {y, idx};
 }
 
-Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t K) {
+Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t K, int64_t S, int64_t P) {
+  if (S < 0) S = K;
   auto mf = at::MemoryFormat::ChannelsLast;
   dy = dy.contiguous(mf);
   check_nhwc_bf16(dy, "dy");
   TORCH_CHECK(idx.sizes() == dy.sizes() && idx.is_contiguous(mf), "maxpool idx mismatch");
   const int N = (int)dy.size(0), C = (int)dy.size(1);
-  TORCH_CHECK(dy.size(2) == H / K && dy.size(3) == W / K, "maxpool_bwd: shape mismatch");
-  Tensor dx = (H % K == 0 && W % K == 0)
-                  ? at::empty({N, C, H, W}, dy.options().memory_format(mf))
-                  // (at::zeros ignores the memory format of its options: allocate
-                  //  channels_last explicitly, then clear the un-pooled border)
-                  : at::empty({N, C, H, W}, dy.options().memory_format(mf)).zero_();
+  TORCH_CHECK(dy.size(2) == dmp::maxpool_out((int)H, (int)K, (int)S, (int)P) &&
+                  dy.size(3) == dmp::maxpool_out((int)W, (int)K, (int)S, (int)P),
+              "maxpool_bwd: shape mismatch");
+  // gather-form kernel writes every input element (un-pooled borders get 0)
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(mf));
   dmp::launch_maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
                           reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)H, (int)W, C, (int)K,
-                          cur_stream());
+                          (int)S, (int)P, cur_stream());
   return dx;
 }
 
@@ -866,7 +869,10 @@ PYBIND11_MODULE(_native, m) {
   m.def("dropout_bwd", &dropout_bwd, "dropout backward from the saved keep mask");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pool forward");
   m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
-  m.def("maxpool_fwd", &maxpool_fwd, "NHWC KxK/sK max pool forward");
-  m.def("maxpool_bwd", &maxpool_bwd, "NHWC KxK/sK max pool backward");
+  m.def("maxpool_fwd", &maxpool_fwd, "NHWC KxK / stride S / pad P max pool forward",
+        py::arg("x"), py::arg("K"), py::arg("S") = -1, py::arg("P") = 0);
+  m.def("maxpool_bwd", &maxpool_bwd, "NHWC KxK / stride S / pad P max pool backward",
+        py::arg("dy"), py::arg("idx"), py::arg("H"), py::arg("W"), py::arg("K"),
+        py::arg("S") = -1, py::arg("P") = 0);
   m.attr("arch") = "gfx950";
 }

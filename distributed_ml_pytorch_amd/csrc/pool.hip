@@ -1,9 +1,10 @@
 // NHWC pooling kernels (bf16, 8 channels = 16 B per thread).
 //
 //  * global average pool  [N,H,W,C] -> [N,C]   (ResNet head, avg_pool2d(4) on CIFAR)
-//  * max pool k x k / stride k (non-overlapping windows), with uint8 argmax
-//    indices for the backward scatter.  The reference uses 2x2/s2 max pooling
-//    in both its models (/root/reference/example/models.py:16-17,29,32,41).
+//  * max pool k x k / stride s / padding p (the reference's 2x2/s2 pooling,
+//    /root/reference/example/models.py:16-17,29,32,41, and the ImageNet
+//    ResNet stem's overlapping 3x3/s2/p1), uint8 argmax indices, gather-form
+//    backward.
 #include "common.h"
 
 namespace dmp {
@@ -48,11 +49,13 @@ __global__ void __launch_bounds__(256) gap_bwd_kernel(const u16* __restrict__ dy
   }
 }
 
-// Max pool, window K x K, stride K, no padding, floor mode.
+// Max pool, window K x K, stride S, zero..K/2 padding (padded taps never win),
+// floor mode; the argmax tap (i*K + j, K <= 15) is kept as uint8 per element.
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const u16* __restrict__ x,
                                                           u16* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H,
-                                                          int W, int C, int K, int Ho, int Wo) {
+                                                          int W, int C, int K, int S, int P,
+                                                          int Ho, int Wo) {
   const int tpr = C >> 3;
   const long long total = (long long)N * Ho * Wo * tpr;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -66,9 +69,13 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const u16* __restrict_
     uint8_t bi[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+    const int h0 = ho * S - P, w0 = wo * S - P;
     for (int i = 0; i < K; ++i) {
+      const int h = h0 + i;
+      if ((unsigned)h >= (unsigned)H) continue;
       for (int j = 0; j < K; ++j) {
-        const int h = ho * K + i, w = wo * K + j;
+        const int w = w0 + j;
+        if ((unsigned)w >= (unsigned)W) continue;
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((n * H + h) * W + w) * C + cg * 8);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -88,36 +95,43 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const u16* __restrict_
   }
 }
 
-// dx must be zero-initialised by the caller only when H or W is not a multiple
-// of K (floor mode leaves un-pooled border rows/cols untouched).
+// Gather form (no atomics, no zero fill): every input element sums dy over the
+// outputs whose window covers it and whose saved argmax is this tap.
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const u16* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx,
                                                           u16* __restrict__ dx, int N, int H,
-                                                          int W, int C, int K, int Ho, int Wo) {
+                                                          int W, int C, int K, int S, int P,
+                                                          int Ho, int Wo) {
   const int tpr = C >> 3;
-  const long long total = (long long)N * Ho * Wo * tpr;
+  const long long total = (long long)N * H * W * tpr;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
     const int cg = (int)(t % tpr);
     long long r = t / tpr;
-    const int wo = (int)(r % Wo); r /= Wo;
-    const int ho = (int)(r % Ho);
-    const long long n = r / Ho;
-    const bf16x8 g = *reinterpret_cast<const bf16x8*>(dy + t * 8);
-    const uint2 packed = *reinterpret_cast<const uint2*>(idx + t * 8);
-    uint8_t bi[8];
+    const int w = (int)(r % W); r /= W;
+    const int h = (int)(r % H);
+    const long long n = r / H;
+    // outputs ho with ho*S - P <= h <= ho*S - P + K - 1
+    const int hlo = max(0, (h + P - K + S) / S), hhi = min(Ho - 1, (h + P) / S);
+    const int wlo = max(0, (w + P - K + S) / S), whi = min(Wo - 1, (w + P) / S);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int ho = hlo; ho <= hhi; ++ho) {
+      for (int wo = wlo; wo <= whi; ++wo) {
+        const uint8_t me = (uint8_t)((h - (ho * S - P)) * K + (w - (wo * S - P)));
+        const long long o = ((n * Ho + ho) * Wo + wo) * C + cg * 8;
+        const bf16x8 g = *reinterpret_cast<const bf16x8*>(dy + o);
+        const uint2 packed = *reinterpret_cast<const uint2*>(idx + o);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { bi[k] = (packed.x >> (8 * k)) & 0xff; bi[4 + k] = (packed.y >> (8 * k)) & 0xff; }
-    for (int i = 0; i < K; ++i) {
-      for (int j = 0; j < K; ++j) {
-        const uint8_t me = (uint8_t)(i * K + j);
-        bf16x8 o;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o.v[k] = (bi[k] == me) ? g.v[k] : (u16)0;
-        const int h = ho * K + i, w = wo * K + j;
-        *reinterpret_cast<bf16x8*>(dx + ((n * H + h) * W + w) * C + cg * 8) = o;
+        for (int k = 0; k < 8; ++k) {
+          const uint8_t bi = (uint8_t)(((k < 4 ? packed.x : packed.y) >> (8 * (k & 3))) & 0xff);
+          if (bi == me) acc[k] += bf2f(g.v[k]);
+        }
       }
     }
+    bf16x8 out;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out.v[k] = f2bf(acc[k]);
+    *reinterpret_cast<bf16x8*>(dx + t * 8) = out;
   }
 }
 
@@ -131,20 +145,22 @@ void launch_gap_bwd(const u16* dy, u16* dx, int N, int HW, int C, hipStream_t s)
   hipLaunchKernelGGL(gap_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy, dx, N, HW, C);
 }
 
+int maxpool_out(int H, int K, int S, int P) { return (H + 2 * P - K) / S + 1; }
+
 void launch_maxpool_fwd(const u16* x, u16* y, uint8_t* idx, int N, int H, int W, int C, int K,
-                        hipStream_t s) {
-  const int Ho = H / K, Wo = W / K;
+                        int S, int P, hipStream_t s) {
+  const int Ho = maxpool_out(H, K, S, P), Wo = maxpool_out(W, K, S, P);
   const long long total = (long long)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, x, y, idx,
-                     N, H, W, C, K, Ho, Wo);
+                     N, H, W, C, K, S, P, Ho, Wo);
 }
 
 void launch_maxpool_bwd(const u16* dy, const uint8_t* idx, u16* dx, int N, int H, int W, int C,
-                        int K, hipStream_t s) {
-  const int Ho = H / K, Wo = W / K;
-  const long long total = (long long)N * Ho * Wo * (C / 8);
+                        int K, int S, int P, hipStream_t s) {
+  const int Ho = maxpool_out(H, K, S, P), Wo = maxpool_out(W, K, S, P);
+  const long long total = (long long)N * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy, idx,
-                     dx, N, H, W, C, K, Ho, Wo);
+                     dx, N, H, W, C, K, S, P, Ho, Wo);
 }
 
 }  // namespace dmp

@@ -73,7 +73,7 @@ class ResNet(nn.Module):
             self.pool = None
         elif stem == "imagenet":
             self.conv1 = L.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-            self.pool = nn.MaxPool2d(3, stride=2, padding=1)
+            self.pool = L.MaxPool2d(3, stride=2, padding=1)
         else:
             raise ValueError(f"unknown stem {stem!r}")
         self.bn1 = L.BatchNorm2d(64, relu=True)

@@ -205,25 +205,29 @@ def global_avg_pool(x):
 
 class _MaxPool(Function):
     @staticmethod
-    def forward(ctx, x, k):
+    def forward(ctx, x, k, s, p):
         x = x.contiguous(memory_format=CL)
-        y, idx = native().maxpool_fwd(x, k)
+        y, idx = native().maxpool_fwd(x, k, s, p)
         ctx.save_for_backward(idx)
-        ctx.meta = (x.shape[2], x.shape[3], k)
+        ctx.meta = (x.shape[2], x.shape[3], k, s, p)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
-        H, W, k = ctx.meta
-        return native().maxpool_bwd(dy, idx, H, W, k), None
+        H, W, k, s, p = ctx.meta
+        return native().maxpool_bwd(dy, idx, H, W, k, s, p), None, None, None
 
 
 def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0):
+    """Max pool (floor mode): native NHWC kernel for bf16 GPU input (any
+    window <= 15, stride, padding <= window/2), PyTorch otherwise."""
     stride = kernel_size if stride is None else stride
-    if (x.is_cuda and x.dtype == torch.bfloat16 and stride == kernel_size and padding == 0
-            and x.shape[1] % 8 == 0 and x.shape[2] >= kernel_size and x.shape[3] >= kernel_size):
-        return _MaxPool.apply(x, int(kernel_size))
+    if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+            and 1 <= kernel_size <= 15 and stride >= 1 and 0 <= 2 * padding <= kernel_size
+            and x.shape[2] + 2 * padding >= kernel_size
+            and x.shape[3] + 2 * padding >= kernel_size):
+        return _MaxPool.apply(x, int(kernel_size), int(stride), int(padding))
     return F.max_pool2d(x, kernel_size, stride, padding)
 
 

@@ -185,16 +185,18 @@ def test_global_avg_pool():
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-3)
 
 
-@pytest.mark.parametrize("shape,k", [((8, 64, 8, 8), 2), ((4, 192, 5, 5), 2), ((2, 16, 9, 9), 3)])
-def test_max_pool(shape, k):
+@pytest.mark.parametrize("shape,k,st,pd", [((8, 64, 8, 8), 2, 2, 0), ((4, 192, 5, 5), 2, 2, 0),
+                                           ((2, 16, 9, 9), 3, 3, 0), ((2, 64, 16, 16), 3, 2, 1),
+                                           ((3, 64, 15, 15), 3, 2, 1), ((2, 8, 11, 7), 5, 2, 2)])
+def test_max_pool(shape, k, st, pd):
     from distributed_ml_pytorch_amd.ops.functional import max_pool2d
 
     x = _bf(torch.randn(shape, device="cuda")).contiguous(memory_format=CL).requires_grad_(True)
-    y = max_pool2d(x, k)
+    y = max_pool2d(x, k, st, pd)
     xr = x.detach().float().requires_grad_(True)
-    yr = F.max_pool2d(xr, k)
+    yr = F.max_pool2d(xr, k, st, pd)
     torch.testing.assert_close(y.float(), yr, rtol=0, atol=0)
-    dy = torch.randn_like(yr)
+    dy = _bf(torch.randn_like(yr)).float()      # the native backward sees bf16 dy
     (y.float() * dy).sum().backward()
     (yr * dy).sum().backward()
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
