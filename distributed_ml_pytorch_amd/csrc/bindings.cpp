@@ -226,9 +226,11 @@ std::vector<Tensor> bn_bwd(Tensor x, Tensor dy, optional<Tensor> y, optional<Ten
     dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc_bf16(dy, "dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "dy shape mismatch");
-  if (relu) {
-    TORCH_CHECK(y.has_value(), "relu backward needs the forward output");
+  // relu without y: the mask is recomputed from x and stats (forward had no residual)
+  const bool have_y = relu && y.has_value() && y->defined();
+  if (have_y) {
     check_nhwc_bf16(*y, "y");
+    TORCH_CHECK(y->sizes() == x.sizes(), "y shape mismatch");
   }
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * C, "bad stats");
   for (auto* t : {&gamma, &dgamma, &dbeta}) {
@@ -246,7 +248,7 @@ std::vector<Tensor> bn_bwd(Tensor x, Tensor dy, optional<Tensor> y, optional<Ten
   auto coef = at::empty({3, C}, fopt);
   dmp::launch_bn_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                      reinterpret_cast<const uint16_t*>(dy.data_ptr()),
-                     relu ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr,
+                     have_y ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr,
                      ptr_or_null<float>(gamma), stats.data_ptr<float>(),
                      ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta), coef.data_ptr<float>(),
                      part.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),

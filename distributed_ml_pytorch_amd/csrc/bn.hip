@@ -27,10 +27,27 @@ __device__ __forceinline__ void store8(u16* p, const float v[8]) {
   *reinterpret_cast<bf16x8*>(p) = r;
 }
 
+// Pre-activation of the forward apply, shared by the forward and the backward's
+// ReLU-mask recomputation so both round identically (explicit fma).
+__device__ __forceinline__ float bn_pre(float x, float sc, float sh) { return __fmaf_rn(x, sc, sh); }
+
+// ReLU mask source of the backward: 0 = no ReLU, 1 = from the saved output y
+// (BN + residual + ReLU: the mask depends on the residual), 2 = recomputed from
+// x and the folded scale/shift in stats (no residual): one tensor read fewer in
+// both backward passes.
+__device__ __forceinline__ void relu_mask_from_x(const float xv[8], const float* __restrict__ stats,
+                                                 int C, int c0, float g[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float y = fmaxf(bn_pre(xv[k], stats[2 * C + c0 + k], stats[3 * C + c0 + k]), 0.f);
+    g[k] = bf2f(f2bf(y)) > 0.f ? g[k] : 0.f;   // exactly the y > 0 test on the stored y
+  }
+}
+
 // -------- per-block channel partial sums --------------------------------
 // MODE 0: s += x, q += x*x                       (forward statistics)
 // MODE 1: s += dz, q += dz*(x-mean)*invstd        (backward reduction)
-template <int MODE, bool RELU>
+template <int MODE, int RELU>
 __global__ void __launch_bounds__(256) bn_partial_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
     const float* __restrict__ stats, float* __restrict__ part, long long M, int C) {
@@ -49,26 +66,57 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) { mean[k] = stats[cg * 8 + k]; inv[k] = stats[C + cg * 8 + k]; }
   }
-  if (r0 < rpi) {
-    for (long long row = start + r0; row < end; row += rpi) {
-      const long long off = row * C + cg * 8;
-      float xv[8];
-      load8(x + off, xv);
-      if (MODE == 0) {
+  auto accum = [&](const float xv[8], float g[8]) {
+    if (MODE == 0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) { s[k] += xv[k]; q[k] += xv[k] * xv[k]; }
-      } else {
-        float g[8];
+      for (int k = 0; k < 8; ++k) { s[k] += xv[k]; q[k] += xv[k] * xv[k]; }
+    } else {
+      if (RELU == 2) relu_mask_from_x(xv, stats, C, cg * 8, g);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] += g[k] * (xv[k] - mean[k]) * inv[k]; }
+    }
+  };
+  // 4 rows per trip with every load issued before any is consumed: the
+  // one-row loop kept ~2 loads in flight per lane and ran at ~2.5 TB/s
+  // (ResNet-50 bs128, gpurun_out/mprof/steady_resnet50.txt)
+  constexpr int U = 4;
+  if (r0 < rpi) {
+    long long row = start + r0;
+    for (; row + (U - 1) * rpi < end; row += U * rpi) {
+      bf16x8 xr[U], dr[U], yr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long off = (row + u * rpi) * C + cg * 8;
+        xr[u] = *reinterpret_cast<const bf16x8*>(x + off);
+        if (MODE == 1) dr[u] = *reinterpret_cast<const bf16x8*>(dy + off);
+        if (MODE == 1 && RELU == 1) yr[u] = *reinterpret_cast<const bf16x8*>(y + off);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float xv[8], g[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xv[k] = bf2f(xr[u].v[k]);
+          g[k] = MODE == 1 ? bf2f(dr[u].v[k]) : 0.f;
+          if (MODE == 1 && RELU == 1) g[k] = bf2f(yr[u].v[k]) > 0.f ? g[k] : 0.f;
+        }
+        accum(xv, g);
+      }
+    }
+    for (; row < end; row += rpi) {
+      const long long off = row * C + cg * 8;
+      float xv[8], g[8];
+      load8(x + off, xv);
+      if (MODE == 1) {
         load8(dy + off, g);
-        if (RELU) {
+        if (RELU == 1) {
           float yv[8];
           load8(y + off, yv);
 #pragma unroll
           for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
         }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] += g[k] * (xv[k] - mean[k]) * inv[k]; }
       }
+      accum(xv, g);
     }
   }
   // LDS reduce over the rpi row-lanes that share a channel group.
@@ -173,7 +221,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(
     load8(x + v * 8, xv);
     float o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = xv[k] * scale[c0 + k] + shift[c0 + k];
+    for (int k = 0; k < 8; ++k) o[k] = bn_pre(xv[k], scale[c0 + k], shift[c0 + k]);
     if (RES) {
       float rv[8];
       load8(res + v * 8, rv);
@@ -212,11 +260,11 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(
   coef[2 * C + c] = Cc;
 }
 
-template <bool RELU, bool WRITE_DRES>
+template <int RELU, bool WRITE_DRES>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
-    const float* __restrict__ coef, u16* __restrict__ dx, u16* __restrict__ dres, long long nvec,
-    int C) {
+    const float* __restrict__ coef, const float* __restrict__ stats, u16* __restrict__ dx,
+    u16* __restrict__ dres, long long nvec, int C) {
   const int tpr = C >> 3;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
@@ -224,11 +272,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     float xv[8], g[8];
     load8(x + v * 8, xv);
     load8(dy + v * 8, g);
-    if (RELU) {
+    if (RELU == 1) {
       float yv[8];
       load8(y + v * 8, yv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    } else if (RELU == 2) {
+      relu_mask_from_x(xv, stats, C, c0, g);
     }
     if (WRITE_DRES) store8(dres + v * 8, g);
     float o[8];
@@ -241,9 +291,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
 // ---------------------------------------------------------------- launchers
 int bn_num_partials(long long M, int C) {
   long long vecs = M * (C / 8);
-  long long g = vecs / (256 * 16);
+  long long g = vecs / (256 * 8);   // >= 8 rows (two 4-row trips) per thread
   if (g < 1) g = 1;
-  if (g > 512) g = 512;
+  if (g > 2048) g = 2048;
   if (g > M) g = M;
   return (int)g;
 }
@@ -256,7 +306,7 @@ void launch_bn_fwd(const u16* x, const u16* res, u16* y, const float* gamma, con
   const int rpi = 256 / (C / 8);
   const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
   if (training) {
-    hipLaunchKernelGGL((bn_partial_kernel<0, false>), dim3(G), dim3(256), lds, s, x, nullptr,
+    hipLaunchKernelGGL((bn_partial_kernel<0, 0>), dim3(G), dim3(256), lds, s, x, nullptr,
                        nullptr, nullptr, part, M, C);
   }
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part,
@@ -273,27 +323,39 @@ void launch_bn_fwd(const u16* x, const u16* res, u16* y, const float* gamma, con
   }
 }
 
+// y == nullptr with relu: the ReLU mask is recomputed from x (no residual in
+// the forward); otherwise it is read from y.
 void launch_bn_bwd(const u16* x, const u16* dy, const u16* y, const float* gamma,
                    const float* stats, float* dgamma, float* dbeta, float* coef, float* part,
                    u16* dx, u16* dres, long long M, int C, bool relu, hipStream_t s) {
   const int G = bn_num_partials(M, C);
   const int rpi = 256 / (C / 8);
   const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
-  if (relu)
-    hipLaunchKernelGGL((bn_partial_kernel<1, true>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, M, C);
-  else
-    hipLaunchKernelGGL((bn_partial_kernel<1, false>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, M, C);
+  const int mode = !relu ? 0 : (y ? 1 : 2);
+#define DMP_BN_PART(R)                                                                          \
+  hipLaunchKernelGGL((bn_partial_kernel<1, R>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, \
+                     M, C)
+  if (mode == 0) DMP_BN_PART(0);
+  else if (mode == 1) DMP_BN_PART(1);
+  else DMP_BN_PART(2);
+#undef DMP_BN_PART
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part,
                      kBnSlots, M, C, gamma, stats, dgamma, dbeta, coef);
   const long long nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, 256));
-  if (relu) {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), grid, dim3(256), 0, s, x, dy, y, coef, dx, dres, nvec, C);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), grid, dim3(256), 0, s, x, dy, y, coef, dx, dres, nvec, C);
+#define DMP_BN_BAPPLY(R, D)                                                                   \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<R, D>), grid, dim3(256), 0, s, x, dy, y, coef, stats, \
+                     dx, dres, nvec, C)
+  if (dres) {
+    if (mode == 0) DMP_BN_BAPPLY(0, true);
+    else if (mode == 1) DMP_BN_BAPPLY(1, true);
+    else DMP_BN_BAPPLY(2, true);
   } else {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), grid, dim3(256), 0, s, x, dy, y, coef, dx, dres, nvec, C);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), grid, dim3(256), 0, s, x, dy, y, coef, dx, dres, nvec, C);
+    if (mode == 0) DMP_BN_BAPPLY(0, false);
+    else if (mode == 1) DMP_BN_BAPPLY(1, false);
+    else DMP_BN_BAPPLY(2, false);
   }
+#undef DMP_BN_BAPPLY
 }
 
 }  // namespace dmp

@@ -130,7 +130,9 @@ class _BNAct(Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.gamma, ctx.beta = gamma, beta
-        ctx.save_for_backward(x, y if relu else None, stats)
+        # the backward re-derives the ReLU mask from x and the folded scale/shift
+        # unless a residual entered the forward (then the mask needs y)
+        ctx.save_for_backward(x, y if (relu and residual is not None) else None, stats)
         return y
 
     @staticmethod
