@@ -392,7 +392,7 @@ void conv_weight_transpose_batched(Tensor src, Tensor dst, Tensor table, int64_t
 }
 
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
-                  int64_t cfg, optional<Tensor> wt_pre) {
+                  int64_t cfg, optional<Tensor> wt_pre, optional<Tensor> addend) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc_bf16(dy, "dy");
   check_gpu(w, "w");
@@ -420,10 +420,19 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
                                       g.CI, cur_stream());
   }
   auto dx = at::empty({B, g.CI, g.H, g.W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const uint16_t* add_ptr = nullptr;
+  Tensor add_t;
+  if (addend.has_value() && addend->defined()) {
+    add_t = addend->contiguous(at::MemoryFormat::ChannelsLast);
+    check_nhwc_bf16(add_t, "addend");
+    TORCH_CHECK(add_t.sizes() == dx.sizes(), "dgrad: addend must have the input's shape");
+    add_ptr = reinterpret_cast<const uint16_t*>(add_t.data_ptr());
+  }
   dmp::launch_conv_dgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                          reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                          reinterpret_cast<uint16_t*>(dx.data_ptr()), B, g.H, g.W, g.CI, g.OH,
-                         g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream());
+                         g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream(),
+                         add_ptr);
   return dx;
 }
 
@@ -824,7 +833,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("cfg") = -1, py::arg("slots") = py::none(), py::arg("bias") = py::none());
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM conv data gradient", py::arg("dy"),
         py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"),
-        py::arg("cfg") = -1, py::arg("wt") = py::none());
+        py::arg("cfg") = -1, py::arg("wt") = py::none(), py::arg("addend") = py::none());
   m.def("conv_weight_transpose_batched", &conv_weight_transpose_batched,
         "transpose every conv weight of a flat bf16 shadow in one launch");
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient (fp32 accumulate)",

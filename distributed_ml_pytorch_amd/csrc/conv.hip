@@ -46,6 +46,7 @@ struct ConvArgs {
   int B, GH, GW, CI, OH, OW, CO, R, S, stride, pad;
   long long M;      // fwd: B*OH*OW; dgrad: rows of the largest parity class
   const float* bias;   // optional fp32 [CO] added in the fwd epilogue
+  const u16* addend;   // dgrad: optional [B][H][W][CI] bf16 added to dX in the epilogue
 };
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -295,6 +296,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   // unit (no per-tile branch).  Bias (fwd) is fetched once per column tile.
   const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.y, 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
+  // dgrad accumulate: dX = dgrad + addend (the residual branch's gradient of the
+  // same input, fused here instead of an autograd add over the whole tensor)
+  const bool add_in = MODE == 1 && a.addend != nullptr;
+  const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
   float bj[TN][4];
   bool nok[TN];
 #pragma unroll
@@ -329,16 +335,25 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+      typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+      const bool ok = mok && nok[j];
+      float ad[4] = {0.f, 0.f, 0.f, 0.f};
+      if (add_in) {
+        const u32x2_t av =
+            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? rowoff + 2u * n : kOOB, 0, 0);
+        ad[0] = __uint_as_float(av.x << 16);
+        ad[1] = __uint_as_float(av.x & 0xffff0000u);
+        ad[2] = __uint_as_float(av.y << 16);
+        ad[3] = __uint_as_float(av.y & 0xffff0000u);
+      }
       u16 h[4];
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        h[r] = f2bf(acc[i][j][r] + bj[j][r]);
+        h[r] = f2bf(acc[i][j][r] + bj[j][r] + ad[r]);
         v[r] = bf2f(h[r]);   // statistics of the stored (rounded) values
       }
-      typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
       const u32x2_t packed = {(u32)h[0] | ((u32)h[1] << 16), (u32)h[2] | ((u32)h[3] << 16)};
-      const bool ok = mok && nok[j];
       __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
       if (STATS) {
         const float keep = ok ? 1.f : 0.f;
@@ -495,7 +510,7 @@ void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int
                      int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                      hipStream_t s, const float* bias) {
   ConvArgs a{x, w, y, part, B, H, W, CI, OH, OW, CO, R, S, stride, pad,
-             (long long)B * OH * OW, bias};
+             (long long)B * OH * OW, bias, nullptr};
   if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(a.M, CO);
   if (part) dispatch<0, true>(a, cfg, 1, s);
   else dispatch<0, false>(a, cfg, 1, s);
@@ -504,9 +519,10 @@ void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int
 // dX (B,H,W,CI) from dY (B,OH,OW,CO) and Wt [CI][R][S][CO]; stride*stride parity classes.
 void launch_conv_dgrad(const u16* dy, const u16* wt, u16* dx, int B, int H, int W, int CI,
                        int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                       hipStream_t s) {
+                       hipStream_t s, const u16* addend) {
   const long long rows = (long long)B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
-  ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad, rows, nullptr};
+  ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad, rows, nullptr,
+             addend};
   if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(rows * stride * stride, CI);
   dispatch<1, false>(a, cfg, stride * stride, s);
 }

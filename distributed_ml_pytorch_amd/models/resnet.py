@@ -34,8 +34,11 @@ class BasicBlock(nn.Module):
                 L.Conv2d(cin, planes, 1, stride=stride, bias=False), L.BatchNorm2d(planes))
 
     def forward(self, x):
-        h = self.bn1(self.conv1(x))
-        sc = x if self.shortcut is None else self.shortcut(x)
+        # the shortcut reads x through conv1's alias: its gradient is summed into
+        # x's gradient by conv1's dgrad epilogue (no autograd add)
+        h, xa = self.conv1(x, alias=True)
+        h = self.bn1(h)
+        sc = xa if self.shortcut is None else self.shortcut(xa)
         return self.bn2(self.conv2(h), residual=sc)
 
 
@@ -57,9 +60,9 @@ class Bottleneck(nn.Module):
                 L.Conv2d(cin, out, 1, stride=stride, bias=False), L.BatchNorm2d(out))
 
     def forward(self, x):
-        h = self.bn1(self.conv1(x))
-        h = self.bn2(self.conv2(h))
-        sc = x if self.shortcut is None else self.shortcut(x)
+        h, xa = self.conv1(x, alias=True)
+        h = self.bn2(self.conv2(self.bn1(h)))
+        sc = xa if self.shortcut is None else self.shortcut(xa)
         return self.bn3(self.conv3(h), residual=sc)
 
 

@@ -132,7 +132,7 @@ def _wgrad_cfg(dy, x, shape, stride, pad):
 
 class _NativeConv(Function):
     @staticmethod
-    def forward(ctx, x, w16, master, stride, pad, want_stats, slots=None, bias=None):
+    def forward(ctx, x, w16, master, stride, pad, want_stats, slots=None, bias=None, alias=False):
         # the BN-partials output never receives a gradient: do not let autograd
         # materialise (zero-fill) one for it every backward
         ctx.set_materialize_grads(False)
@@ -147,15 +147,20 @@ class _NativeConv(Function):
         ctx.save_for_backward(x, w16)
         ctx.master = master
         ctx.geom = (x.shape[2], x.shape[3], stride, pad)
+        # alias: x handed back as a third output (a view whose gradient arrives
+        # here) -- a block routes its shortcut through it, so the shortcut's
+        # gradient is added inside this conv's dgrad epilogue instead of by an
+        # autograd add over the whole activation
+        xa = x if alias else None
         if want_stats:
             ctx.mark_non_differentiable(part)
-            return y, part
-        return y, None
+            return y, part, xa
+        return y, None, xa
 
     @staticmethod
-    def backward(ctx, dy, _dpart):
+    def backward(ctx, dy, _dpart, dxa=None):
         if dy is None:
-            return None, None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None, dxa
         x, w16 = ctx.saved_tensors
         H, W, stride, pad = ctx.geom
         dy = dy.contiguous(memory_format=torch.channels_last)
@@ -169,7 +174,9 @@ class _NativeConv(Function):
             shadow = getattr(master, "_dmp_w16", None)
             if arena is not None and shadow is not None and shadow.data_ptr() == w16.data_ptr():
                 wt = arena.transposed_conv_shadow(master)
-            dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt)
+            dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt, dxa)
+        elif dxa is not None:
+            dx = dxa
         gw = None
         if master is not None and master.requires_grad:
             wcfg = _wgrad_cfg(dy, x, tuple(master.shape), stride, pad)
@@ -201,7 +208,7 @@ class _NativeConv(Function):
                     cb(bias)
             else:
                 gb = dy.sum(dim=(0, 2, 3), dtype=torch.float32).to(bias.dtype)
-        return dx, None, gw, None, None, None, None, gb
+        return dx, None, gw, None, None, None, None, gb, None
 
 
 class _SmallConv(Function):
@@ -283,11 +290,13 @@ def native_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
 
 
 def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=False,
-           slots=None):
+           slots=None, alias=False):
     """Returns ``y`` (with BN slot sums attached as ``y._dmp_bn_part`` when ``want_stats``).
 
     ``slots``: the layer's persistent ``[2][64][CO]`` fp32 BN slot buffer (zeroed;
     the consuming BatchNorm's finalize re-zeroes it); a fresh one when None.
+    ``alias``: return ``(y, x_alias)``; gradients reaching ``x_alias`` are summed
+    into this conv's input gradient by the dgrad kernel itself.
     """
     if x.is_cuda and x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
@@ -297,11 +306,12 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
             if w16 is None or not w16.is_contiguous(memory_format=torch.channels_last):
                 w16 = master.detach().to(torch.bfloat16).contiguous(
                     memory_format=torch.channels_last)
-            y, part = _NativeConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
-                                        bool(want_stats), slots if want_stats else None, b)
+            y, part, xa = _NativeConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
+                                            bool(want_stats), slots if want_stats else None, b,
+                                            bool(alias))
             if part is not None:
                 y._dmp_bn_part = part
-            return y
+            return (y, xa) if alias else y
         if master is not None and b is None and small_conv_supported(
                 x, master, stride, padding, dilation, groups):
             w16 = getattr(master, "_dmp_w16", None)
@@ -312,5 +322,6 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
                                        bool(want_stats), slots if want_stats else None)
             if part is not None:
                 y._dmp_bn_part = part
-            return y
-    return F.conv2d(x, w, b, stride, padding, dilation, groups)
+            return (y, x) if alias else y
+    y = F.conv2d(x, w, b, stride, padding, dilation, groups)
+    return (y, x) if alias else y

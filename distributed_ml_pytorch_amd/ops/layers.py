@@ -25,7 +25,9 @@ class Conv2d(nn.Conv2d):
 
     emit_bn_stats = False
 
-    def forward(self, x):
+    def forward(self, x, alias: bool = False):
+        """``alias=True`` returns ``(y, x_alias)``: route the block's shortcut
+        through ``x_alias`` and its gradient is added in this conv's dgrad."""
         if (x.is_cuda and (self.bias is None or native_conv_supported(
                 x, self.weight, self.stride, self.padding, self.dilation, self.groups))
                 and (native_conv_supported(x, self.weight, self.stride, self.padding,
@@ -35,10 +37,12 @@ class Conv2d(nn.Conv2d):
             want = self.emit_bn_stats and self.training
             slots = bn_slot_buffer(self, "_dmp_slots", self.out_channels, x.device) if want else None
             return _conv2d(x, None, self.bias, self.stride, self.padding, self.dilation,
-                           self.groups, master=self.weight, want_stats=want, slots=slots)
+                           self.groups, master=self.weight, want_stats=want, slots=slots,
+                           alias=alias)
         w = DF.compute_weight(self.weight, x.dtype)
         b = DF.compute_weight(self.bias, x.dtype)
-        return _conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups)
+        return _conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups,
+                       alias=alias)
 
 
 class Linear(nn.Linear):

@@ -205,3 +205,43 @@ def test_conv_layer_bias_native():
     assert _rel(conv.weight.grad, w.grad) < 1e-2
     assert _rel(conv.bias.grad, b.grad) < 1e-2
     assert _rel(x.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("stride,cin,planes", [(1, 64, 64), (2, 64, 128)])
+def test_resnet_block_alias_shortcut_grad(stride, cin, planes):
+    """BasicBlock on the native path (the shortcut's gradient is summed inside
+    conv1's dgrad epilogue through the alias output) vs an fp32 functional
+    reference of the same block."""
+    from distributed_ml_pytorch_amd.models.resnet import BasicBlock
+
+    torch.manual_seed(0)
+    blk = BasicBlock(cin, planes, stride).cuda()
+    x = torch.randn(4, cin, 16, 16, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=CL).requires_grad_(True)
+    y = blk(x)
+    g = torch.randn(y.shape, device="cuda")
+    (y.float() * g).sum().backward()
+
+    def w(conv):
+        return conv.weight.detach().to(torch.bfloat16).float()
+
+    def bn(t, m):
+        return F.batch_norm(t, None, None, m.weight.detach(), m.bias.detach(), True, 0.1, m.eps)
+
+    xr = x.detach().float().requires_grad_(True)
+    h = F.relu(bn(F.conv2d(xr, w(blk.conv1), None, stride, 1), blk.bn1))
+    if blk.shortcut is None:
+        sc = xr
+    else:
+        sc = bn(F.conv2d(xr, w(blk.shortcut[0]), None, stride, 0), blk.shortcut[1])
+    yr = F.relu(bn(F.conv2d(h, w(blk.conv2), None, 1, 1), blk.bn2) + sc)
+    (yr * g).sum().backward()
+    assert _rel(y, yr) < 3e-2
+    assert _rel(x.grad, xr.grad) < 6e-2      # two bf16 conv+BN levels deep
+    # the same native block with the shortcut gradient summed by autograd instead
+    xb = x.detach().clone().requires_grad_(True)
+    h = blk.bn1(blk.conv1(xb))
+    sc = xb if blk.shortcut is None else blk.shortcut(xb)
+    yb = blk.bn2(blk.conv2(h), residual=sc)
+    (yb.float() * g).sum().backward()
+    assert _rel(x.grad, xb.grad) < 1e-2
