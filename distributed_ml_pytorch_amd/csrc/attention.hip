@@ -17,9 +17,11 @@
 // A D tile whose ROW index is a reduction index of the next product feeds that
 // product directly: two adjacent 16-row D blocks, packed {block0[0..3],
 // block1[0..3]}, are the 8 k-values {4g..4g+3, 16+4g..16+4g+3} of a 32-deep
-// k-step; the other operand is read from a transposed LDS tile with the same
-// k permutation (two 8-B reads).  So every product runs on registers + LDS
-// with no shuffles:
+// k-step; the other operand is read with the same k permutation by two
+// ds_read_b64_tr_b16 hardware-transposed reads of the ROW-MAJOR token image
+// (ld_tr_perm), so each of K/V (or Q/dO) is staged once, with 16-B stores, and
+// serves both the row-wise and the transposed reads.  Every product runs on
+// registers + LDS with no shuffles:
 //   forward  (query strips):  S^T = K Q^T  ->  softmax  ->  O^T = V^T P^T
 //   dQ       (query strips):  S^T, dP^T = V dO^T  ->  dS^T  ->  dQ^T = K^T dS^T
 //   dK, dV   (key strips):    S = Q K^T, dP = dO V^T -> dS -> dV^T = dO^T P,
@@ -34,6 +36,7 @@ namespace dmp {
 namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kDH = 64;          // head dim
 constexpr int kRS = kDH + 8;     // row stride (elements) of row-major [token][64] LDS tiles
@@ -55,14 +58,6 @@ __device__ __forceinline__ bf16x8 pack8(const f32x4& lo, const f32x4& hi) {
   return r;
 }
 
-// k-permuted operand from a transposed tile: 4 values at p, 4 at p + 16
-__device__ __forceinline__ bf16x8 ld_perm(const u16* p) {
-  bf16x8 r;
-  *reinterpret_cast<uint2*>(&r.v[0]) = *reinterpret_cast<const uint2*>(p);
-  *reinterpret_cast<uint2*>(&r.v[4]) = *reinterpret_cast<const uint2*>(p + 16);
-  return r;
-}
-
 __device__ __forceinline__ bf16x8 ld16(const u16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 __device__ __forceinline__ void st4(u16* p, const f32x4& v, float s) {
@@ -72,25 +67,48 @@ __device__ __forceinline__ void st4(u16* p, const f32x4& v, float s) {
   *reinterpret_cast<uint2*>(p) = w;
 }
 
-// Stage token rows [0, NP) of one head's slice t (0 q, 1 k, 2 v) of a
-// [B, N, 3, H, 64] tensor (or of a [B, N, H, 64] one with t = -1) into LDS:
-// row-major (stride kRS) and/or transposed (stride TS).  Rows >= N are zero.
+// k-permuted operand read TRANSPOSED out of a row-major [token][kRS] image with
+// ds_read_b64_tr_b16: lane 16g + 4q + p addresses token row0 + 4g + q (and
+// row0 + 16 + 4g + q), head dims col0 + 4p .. col0 + 4p + 3; lane 16g + i gets
+// head dim col0 + i of those 4 tokens, i.e. A[i][k] for k = {4g..4g+3,
+// 16+4g..16+4g+3}.  The gather crosses lanes, so EXEC must be full: every call
+// site sits in wave-uniform control flow.
+__device__ __forceinline__ bf16x8 ld_tr_perm(const u16* img, int row0, int col0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const u16* a = img + (row0 + 4 * g + q) * kRS + col0 + 4 * p;
+  const s16x4_t lo =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(a));
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4_t*)(a + 16 * kRS));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// Stage token rows [0, NP) of two [token][64] head slices into row-major LDS
+// images (stride kRS).  Rows >= N repeat row N-1 -- finite values that every
+// consumer gives zero weight -- so the loads are unconditional and each thread
+// issues all of its 2 * U loads before its first LDS store (one HBM round trip
+// instead of one per row chunk).
 template <int NT>
-__device__ __forceinline__ void stage_head(const u16* __restrict__ src, long long tok0, int N,
-                                           int NP, int rowstride, u16* rm, u16* tr, int TS) {
-  for (int i = threadIdx.x; i < NP * 8; i += NT) {
-    const int n = i >> 3, c = i & 7;
-    bf16x8 v;
-    if (n < N) {
-      v = ld16(src + (tok0 + n) * rowstride + c * 8);
-    } else {
+__device__ __forceinline__ void stage2(const u16* __restrict__ s0, int rs0,
+                                       const u16* __restrict__ s1, int rs1, long long tok0, int N,
+                                       int NP, u16* d0, u16* d1) {
+  constexpr int U = 16 * kMaxKB * 8 / NT;
+  const int total = NP * 8;
+  bf16x8 v0[U], v1[U];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v.v[k] = 0;
-    }
-    if (rm) *reinterpret_cast<bf16x8*>(rm + n * kRS + c * 8) = v;
-    if (tr) {
+  for (int u = 0; u < U; ++u) {
+    const int i = min(u * NT + (int)threadIdx.x, total - 1);
+    const long long t = tok0 + min(i >> 3, N - 1);
+    v0[u] = ld16(s0 + t * rs0 + (i & 7) * 8);
+    v1[u] = ld16(s1 + t * rs1 + (i & 7) * 8);
+  }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) tr[(c * 8 + k) * TS + n] = v.v[k];
+  for (int u = 0; u < U; ++u) {
+    const int i = u * NT + threadIdx.x;
+    if (i < total) {
+      const int o = (i >> 3) * kRS + (i & 7) * 8;
+      *reinterpret_cast<bf16x8*>(d0 + o) = v0[u];
+      *reinterpret_cast<bf16x8*>(d1 + o) = v1[u];
     }
   }
 }
@@ -104,14 +122,13 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const u16* __restrict
                                                           float* __restrict__ lse2, int N, int H,
                                                           float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  const int NP = (N + 31) & ~31, TS = NP + 8, D = H * kDH;
+  const int NP = (N + 31) & ~31, D = H * kDH;
   u16* Ks = smem;              // [NP][kRS]
-  u16* Vt = smem + NP * kRS;   // [64][TS]
+  u16* Vs = smem + NP * kRS;   // [NP][kRS], read transposed
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const long long tok0 = (long long)b * N;
   const u16* base = qkv + h * kDH;
-  stage_head<64 * NW>(base + D, tok0, N, NP, 3 * D, Ks, nullptr, TS);
-  stage_head<64 * NW>(base + 2 * D, tok0, N, NP, 3 * D, nullptr, Vt, TS);
+  stage2<64 * NW>(base + D, 3 * D, base + 2 * D, 3 * D, tok0, N, NP, Ks, Vs);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
@@ -161,7 +178,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const u16* __restrict
         const bf16x8 pb = pack8(s[2 * kp], s[2 * kp + 1]);
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb)
-          o[nb] = mfma(ld_perm(Vt + (nb * 16 + l16) * TS + 32 * kp + 4 * g), pb, o[nb]);
+          o[nb] = mfma(ld_tr_perm(Vs, 32 * kp, nb * 16, lane), pb, o[nb]);
       }
     }
     if (q < N) {
@@ -181,15 +198,13 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
     const float* __restrict__ lse2, u16* __restrict__ dqkv, int N, int H, float scale_log2,
     float scale) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  const int NP = (N + 31) & ~31, TS = NP + 8, D = H * kDH;
-  u16* Ks = smem;                   // [NP][kRS]
+  const int NP = (N + 31) & ~31, D = H * kDH;
+  u16* Ks = smem;                   // [NP][kRS], read row-wise and transposed
   u16* Vs = Ks + NP * kRS;          // [NP][kRS]
-  u16* Kt = Vs + NP * kRS;          // [64][TS]
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const long long tok0 = (long long)b * N;
   const u16* base = qkv + h * kDH;
-  stage_head<64 * NW>(base + D, tok0, N, NP, 3 * D, Ks, Kt, TS);
-  stage_head<64 * NW>(base + 2 * D, tok0, N, NP, 3 * D, Vs, nullptr, TS);
+  stage2<64 * NW>(base + D, 3 * D, base + 2 * D, 3 * D, tok0, N, NP, Ks, Vs);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
@@ -235,7 +250,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
         const bf16x8 db = pack8(ds[0], ds[1]);
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb)
-          dq[nb] = mfma(ld_perm(Kt + (nb * 16 + l16) * TS + 32 * kp + 4 * g), db, dq[nb]);
+          dq[nb] = mfma(ld_tr_perm(Ks, 32 * kp, nb * 16, lane), db, dq[nb]);
       }
     }
     if (q < N) {
@@ -253,34 +268,46 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkv_kernel(
     const float* __restrict__ lse2, u16* __restrict__ dqkv, int N, int H, float scale_log2,
     float scale) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  const int NP = (N + 31) & ~31, TS = NP + 8, D = H * kDH;
-  u16* Qs = smem;                   // [NP][kRS]
-  u16* Ds = Qs + NP * kRS;          // dO [NP][kRS]
-  u16* Qt = Ds + NP * kRS;          // [64][TS]
-  u16* Dt = Qt + kDH * TS;          // dO^T [64][TS]
-  float* Ls = reinterpret_cast<float*>(Dt + kDH * TS);   // [NP] lse2 (+inf past N)
-  float* Di = Ls + NP;                                   // [NP] rowsum(dO * O)
+  constexpr int NT = 64 * NW, U = 16 * kMaxKB * 8 / NT;
+  const int NP = (N + 31) & ~31, D = H * kDH;
+  u16* Qs = smem;                   // [NP][kRS], read row-wise and transposed
+  u16* Ds = Qs + NP * kRS;          // dO [NP][kRS], read row-wise and transposed
+  float* Ls = reinterpret_cast<float*>(Ds + NP * kRS);   // [NP] lse2 (+inf past N)
+  float* Di = Ls + NP;                                   // [NP] rowsum(dO * O) (0 past N)
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const long long tok0 = (long long)b * N;
   const u16* base = qkv + h * kDH;
-  stage_head<64 * NW>(base, tok0, N, NP, 3 * D, Qs, Qt, TS);
-  stage_head<64 * NW>(dout + h * kDH, tok0, N, NP, D, Ds, Dt, TS);
-  // Di[q] = dO[q] . O[q]: 8 threads per row, 8 elements each
-  for (int i = threadIdx.x; i < NP * 8; i += 64 * NW) {
-    const int n = i >> 3, c = i & 7;
-    float d = 0.f;
-    if (n < N) {
-      const bf16x8 ov = ld16(out + (tok0 + n) * D + h * kDH + c * 8);
-      const bf16x8 dv = ld16(dout + (tok0 + n) * D + h * kDH + c * 8);
+  // stage Q and dO (as stage2) and reduce Di[q] = dO[q] . O[q] from the dO
+  // chunks already in registers: 8 consecutive threads own one row
+  {
+    const int total = NP * 8;
+    bf16x8 vq[U], vd[U], vo[U];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) d += bf2f(ov.v[k]) * bf2f(dv.v[k]);
+    for (int u = 0; u < U; ++u) {
+      const int i = min(u * NT + (int)threadIdx.x, total - 1);
+      const long long t = tok0 + min(i >> 3, N - 1);
+      vq[u] = ld16(base + t * 3 * D + (i & 7) * 8);
+      vd[u] = ld16(dout + t * D + h * kDH + (i & 7) * 8);
+      vo[u] = ld16(out + t * D + h * kDH + (i & 7) * 8);
     }
-    d += __shfl_xor(d, 1, 64);
-    d += __shfl_xor(d, 2, 64);
-    d += __shfl_xor(d, 4, 64);
-    if (c == 0) {
-      Di[n] = d;
-      Ls[n] = n < N ? lse2[(long long)bh * N + n] : INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = u * NT + threadIdx.x, n = i >> 3;
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d += bf2f(vo[u].v[k]) * bf2f(vd[u].v[k]);
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      if (i < total) {
+        const int o = n * kRS + (i & 7) * 8;
+        *reinterpret_cast<bf16x8*>(Qs + o) = vq[u];
+        *reinterpret_cast<bf16x8*>(Ds + o) = vd[u];
+        if ((i & 7) == 0) {
+          Di[n] = n < N ? d : 0.f;
+          Ls[n] = n < N ? lse2[(long long)bh * N + n] : INFINITY;
+        }
+      }
     }
   }
   __syncthreads();
@@ -323,9 +350,8 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkv_kernel(
         const bf16x8 pb = pack8(pp[0], pp[1]), db = pack8(ds[0], ds[1]);
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) {
-          const int off = (nb * 16 + l16) * TS + 32 * qp + 4 * g;
-          dv[nb] = mfma(ld_perm(Dt + off), pb, dv[nb]);
-          dk[nb] = mfma(ld_perm(Qt + off), db, dk[nb]);
+          dv[nb] = mfma(ld_tr_perm(Ds, 32 * qp, nb * 16, lane), pb, dv[nb]);
+          dk[nb] = mfma(ld_tr_perm(Qs, 32 * qp, nb * 16, lane), db, dk[nb]);
         }
       }
     }
@@ -345,18 +371,17 @@ int attention_max_tokens() { return 16 * kMaxKB; }
 int attention_head_dim() { return kDH; }
 
 namespace {
-constexpr int kFwdWaves = 4, kBwdWaves = 8;
+constexpr int kFwdWaves = 8, kBwdWaves = 8;
+// two row-major [NP][kRS] bf16 images per kernel (+ lse2 / Di rows for dK,dV):
+// 64.5 KiB at N = 197, two workgroups per CU
 size_t fwd_lds(int N) {
   const int NP = (N + 31) & ~31;
-  return ((size_t)NP * kRS + (size_t)kDH * (NP + 8)) * 2;
+  return (size_t)2 * NP * kRS * 2;
 }
-size_t dq_lds(int N) {
-  const int NP = (N + 31) & ~31;
-  return ((size_t)2 * NP * kRS + (size_t)kDH * (NP + 8)) * 2;
-}
+size_t dq_lds(int N) { return fwd_lds(N); }
 size_t dkv_lds(int N) {
   const int NP = (N + 31) & ~31;
-  return ((size_t)2 * NP * kRS + (size_t)2 * kDH * (NP + 8)) * 2 + (size_t)2 * NP * 4;
+  return fwd_lds(N) + (size_t)2 * NP * 4;
 }
 template <typename K>
 void allow_lds(K kernel, size_t bytes) {
