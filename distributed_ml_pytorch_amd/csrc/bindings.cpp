@@ -797,6 +797,18 @@ std::vector<std::vector<int64_t>> conv_configs() {
   return out;
 }
 
+// halo-tile cfg ids applicable to a conv over a [*, C, H, W] input (3x3 / stride 1 / pad 1)
+std::vector<int64_t> conv_halo_configs(int64_t H, int64_t W, int64_t C, int64_t R, int64_t S,
+                                       int64_t stride, int64_t pad) {
+  std::vector<int64_t> out;
+  for (int i = 0; i < dmp::conv_num_halo_configs(); ++i) {
+    const int c = dmp::conv_halo_base() + i;
+    if (dmp::conv_halo_ok(c, (int)H, (int)W, (int)C, (int)R, (int)S, (int)stride, (int)pad))
+      out.push_back(c);
+  }
+  return out;
+}
+
 std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optional<Tensor> res,
                                          optional<Tensor> gamma, optional<Tensor> beta,
                                          optional<Tensor> running_mean,
@@ -840,6 +852,8 @@ PYBIND11_MODULE(_native, m) {
         py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("cfg") = -1);
   m.def("conv_configs", &conv_configs, "[(id, BM, BN, BK, threads)] of the compiled conv tiles");
+  m.def("conv_halo_configs", &conv_halo_configs,
+        "3x3/stride-1 halo-tile cfg ids applicable to (H, W, C, R, S, stride, pad)");
   m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials");
   m.def("conv_small_fwd", &conv_small_fwd, "few-input-channel conv forward (+BN partials)",
         py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),

@@ -402,6 +402,268 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   }
 }
 
+// ------------------------------------------------ 3x3 stride-1 halo tiles
+// The implicit GEMM above gathers its A operand once per tap: a 3x3 conv
+// pulls every input pixel through L2 / the Infinity Cache nine times, and on
+// the 32x32 / 16x16 ResNet-18 layers that traffic (not the MFMA work) sets the
+// kernel time (~7.8 TB/s measured on 64->64 32x32, the Infinity-Cache gather
+// rate).  For 3x3 / stride 1 / pad 1 this kernel instead stages, per 32-channel
+// chunk, the block's input pixels ONCE with their one-pixel halo -- a tile of
+// TB images x (TH+2) rows x (W+2) columns, out-of-image positions fetched as
+// zeros through the buffer descriptor -- plus all 9 taps of the weight chunk,
+// and runs the nine tap products out of LDS by offsetting the pixel row
+// (tap (r, s) of output pixel (th, tw) = halo row (th + r) * (W+2) + tw + s).
+// The block's BM output pixels are whole image rows (TB = 1, TH = BM / W) or
+// whole images (TH = H, TB = BM / (H*W)), so they are a contiguous range of
+// NHWC rows and the epilogue is the forward one.  FLIP runs the stride-1 data
+// gradient: the same conv over dY with Wt[ci][r][s][co] and the taps mirrored.
+// NS = 2: two LDS stages (halo + 9 weight tiles each), one barrier per chunk;
+// NS = 1: one stage, more resident blocks per CU.
+struct HaloGeom {
+  int TH, TB, HROWS, A_INS;
+};
+
+constexpr int kHaloAPW = 6;   // max halo DMA instructions per wave per stage
+
+template <int BM, int BN, int BK, int WM, int WN, int NS, bool FLIP, bool STATS>
+__global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, HaloGeom hg) {
+  constexpr int NW = WM * WN;
+  constexpr int CPR = BK / 8, RPI = 64 / CPR;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int B_ROWS = 9 * BN, B_INS = B_ROWS / RPI, B_PW = (B_INS + NW - 1) / NW;
+  static_assert(B_ROWS % RPI == 0, "weight tile rows");
+  extern __shared__ __attribute__((aligned(16))) u16 lds_h[];
+  const int A_EL = hg.A_INS * RPI * BK;
+  const int STAGE = A_EL + B_ROWS * BK;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int H = a.GH, W = a.GW, C = a.CI, TH = hg.TH, HW2 = W + 2;
+  const int img = H * W;
+  const int b0 = (int)(m0 / img), h0 = (int)(m0 - (long long)b0 * img) / W;
+  const int per_img = (TH + 2) * HW2;
+
+  // halo DMA slots: lane's row of each 1-KiB piece -> (image, h, w) of the
+  // source pixel; positions outside the image (or past the batch) read zeros
+  unsigned a_base[kHaloAPW];
+#pragma unroll
+  for (int j = 0; j < kHaloAPW; ++j) {
+    const int ins = wid + j * NW;
+    const int row = ins * RPI + lane / CPR;
+    const int tb = row / per_img, rem = row - tb * per_img;
+    const int hh = rem / HW2, ww = rem - hh * HW2;
+    const int b = b0 + tb, h = h0 - 1 + hh, w = ww - 1;
+    const bool ok = ins < hg.A_INS && row < hg.HROWS && b < a.B && (unsigned)h < (unsigned)H &&
+                    (unsigned)w < (unsigned)W;
+    a_base[j] = ok ? 2u * (unsigned)(((b * H + h) * W + w) * C + swz<BK>(row, lane % CPR) * 8)
+                   : kOOB;
+  }
+  // weight DMA slots: row = tap * BN + output channel
+  unsigned b_base[B_PW];
+#pragma unroll
+  for (int j = 0; j < B_PW; ++j) {
+    const int ins = wid + j * NW;
+    const int row = ins * RPI + lane / CPR;
+    const int t = row / BN, co = row - t * BN;
+    const bool ok = ins < B_INS && n0 + co < a.CO;
+    b_base[j] = ok ? 2u * (unsigned)(((n0 + co) * 9 + t) * C + swz<BK>(row, lane % CPR) * 8) : kOOB;
+  }
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, 0, (int)(2LL * a.B * H * W * C), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.w, 0, (int)(2LL * a.CO * 9 * C), 0x00020000);
+
+  auto stage = [&](int buf, int c) {
+    u16* As = lds_h + buf * STAGE;
+    u16* Bs = As + A_EL;
+    const unsigned cd = 2u * (unsigned)(c * BK);
+#pragma unroll
+    for (int j = 0; j < kHaloAPW; ++j) {
+      const int ins = wid + j * NW;
+      if (ins < hg.A_INS)
+        bdma16(rsA, a_base[j] == kOOB ? kOOB : a_base[j] + cd, As + ins * (RPI * BK));
+    }
+#pragma unroll
+    for (int j = 0; j < B_PW; ++j) {
+      const int ins = wid + j * NW;
+      if (B_INS % NW == 0 || ins < B_INS)
+        bdma16(rsB, b_base[j] == kOOB ? kOOB : b_base[j] + cd, Bs + ins * (RPI * BK));
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // halo row of each of the lane's output pixels at tap (0, 0)
+  int hrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
+    const int tb = ml / (TH * W), r2 = ml - tb * TH * W;
+    const int th = r2 / W, tw = r2 - th * W;
+    hrow[i] = (tb * (TH + 2) + th) * HW2 + tw;
+  }
+  int offB[BK / 32];
+  {
+    const int rb = wn * (BN / WN) + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) offB[ks] = rb * BK + swz<BK>(rb, ks * 4 + (lane >> 4)) * 8;
+  }
+  auto compute = [&](int buf) {
+    const u16* As = lds_h + buf * STAGE;
+    const u16* Bs = As + A_EL;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int rowoff = (t / 3) * HW2 + (t % 3);
+      const int wt = FLIP ? 8 - t : t;
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 af[TM], bw[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = hrow[i] + rowoff;
+          af[i] = *reinterpret_cast<const bf16x8*>(
+              As + row * BK + swz<BK>(row, ks * 4 + (lane >> 4)) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bw[j] = *reinterpret_cast<const bf16x8*>(Bs + wt * BN * BK + offB[ks] + j * 16 * BK);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bw[j], af[i], acc[i][j]);
+      }
+    }
+  };
+
+  const int KC = C / BK;
+  if constexpr (NS == 2) {
+    stage(0, 0);
+    for (int c = 0; c < KC; ++c) {
+      wait_vm<0>();                       // chunk c landed (this wave's DMAs) ...
+      __builtin_amdgcn_s_barrier();       // ... for every wave; chunk c-1's slot is free
+      asm volatile("" ::: "memory");
+      if (c + 1 < KC) stage((c + 1) & 1, c + 1);
+      compute(c & 1);
+    }
+  } else {
+    // one stage: half the LDS, so two or three blocks share a CU and one
+    // block's load / epilogue overlaps another's MFMA work
+    for (int c = 0; c < KC; ++c) {
+      if (c > 0) __syncthreads();         // everyone done reading chunk c-1
+      stage(0, c);
+      wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      compute(0);
+    }
+  }
+  __syncthreads();   // all stage reads done before the epilogue reuses LDS
+
+  // epilogue (forward layout: output row m = pixel m): bias (fwd), residual
+  // gradient addend (FLIP), BN partial sums (STATS) -- as conv_igemm_kernel
+  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+  const long long Mtot = (long long)a.B * a.OH * a.OW;
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.y, 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  const bool add_in = FLIP && a.addend != nullptr;
+  const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  float bj[TN][4];
+  bool nok[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+    nok[j] = n < a.CO;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bj[j][r] = (!FLIP && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
+  }
+  float s_sum[TN][4], s_sq[TN][4];
+  if (STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s_sum[j][r] = 0.f; s_sq[j][r] = 0.f; }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const long long m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+    const bool mok = m < Mtot;
+    const unsigned rowoff = 2u * (unsigned)(m * a.CO);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+      const bool ok = mok && nok[j];
+      float ad[4] = {0.f, 0.f, 0.f, 0.f};
+      if (add_in) {
+        const u32x2_t av =
+            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? rowoff + 2u * n : kOOB, 0, 0);
+        ad[0] = __uint_as_float(av.x << 16);
+        ad[1] = __uint_as_float(av.x & 0xffff0000u);
+        ad[2] = __uint_as_float(av.y << 16);
+        ad[3] = __uint_as_float(av.y & 0xffff0000u);
+      }
+      u16 hv[4];
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hv[r] = f2bf(acc[i][j][r] + bj[j][r] + ad[r]);
+        v[r] = bf2f(hv[r]);
+      }
+      const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
+      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
+      if (STATS) {
+        const float keep = ok ? 1.f : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = v[r] * keep;
+          s_sum[j][r] += x;
+          s_sq[j][r] += x * x;
+        }
+      }
+    }
+  }
+  if (STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s_sum[j][r] = row_sum16(s_sum[j][r]);
+        s_sq[j][r] = row_sum16(s_sq[j][r]);
+      }
+    float* red = reinterpret_cast<float*>(lds_h);   // [WM][BN] sums, then [WM][BN] squares
+    if ((lane & 15) == 15) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = wn * (BN / WN) + j * 16 + 4 * (lane >> 4) + r;
+          red[wm * BN + nl] = s_sum[j][r];
+          red[WM * BN + wm * BN + nl] = s_sq[j][r];
+        }
+    }
+    __syncthreads();
+    for (int nl = tid; nl < BN; nl += 64 * NW) {
+      const int n = n0 + nl;
+      if (n < a.CO) {
+        float ss = 0.f, qq = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) { ss += red[w * BN + nl]; qq += red[WM * BN + w * BN + nl]; }
+        const int slot = blockIdx.x % kBnSlots;
+        atomicAdd(a.part + (long long)slot * a.CO + n, ss);
+        atomicAdd(a.part + (long long)(kBnSlots + slot) * a.CO + n, qq);
+      }
+    }
+  }
+}
+
 // W[co][r][s][ci] -> Wt[ci][r][s][co]  (bf16)
 __global__ void __launch_bounds__(256) conv_weight_transpose_kernel(
     const u16* __restrict__ w, u16* __restrict__ wt, int CO, int RS, int CI) {
@@ -500,7 +762,104 @@ static void dispatch(const ConvArgs& a, int cfg, int classes, hipStream_t s) {
   }
 }
 
+// Halo-tile configurations (BM, BN, BK, WM, WN), cfg ids kHaloBase + i; only for
+// 3x3 / stride 1 / pad 1 and block tiles of whole rows or whole images.
+#define DMP_HALO_CONFIGS(X)   \
+  X(0, 256, 64, 32, 4, 2, 2)  \
+  X(1, 128, 64, 32, 2, 2, 2)  \
+  X(2, 64, 64, 32, 2, 2, 2)   \
+  X(3, 128, 64, 32, 4, 2, 2)  \
+  X(4, 256, 64, 32, 2, 2, 2)  \
+  X(5, 128, 64, 32, 2, 2, 1)  \
+  X(6, 256, 64, 32, 4, 2, 1)  \
+  X(7, 64, 64, 32, 2, 2, 1)   \
+  X(8, 128, 64, 32, 4, 2, 1)
+
+constexpr int kHaloBase = 100, kNumHaloConfigs = 9;
+
+static bool halo_cfg(int cfg, int* bm, int* bn, int* bk, int* nw, int* ns) {
+  switch (cfg - kHaloBase) {
+#define X(i, BM, BN, BK, WM, WN, NS) \
+  case i: *bm = BM; *bn = BN; *bk = BK; *nw = WM * WN; *ns = NS; return true;
+    DMP_HALO_CONFIGS(X)
+#undef X
+  }
+  return false;
+}
+
+// geometry of a halo config on a (B, H, W, C) input; false when it does not apply
+static bool halo_geom(int cfg, int H, int W, int C, int R, int S, int stride, int pad,
+                      HaloGeom* g, size_t* lds) {
+  int bm, bn, bk, nw, ns;
+  if (!halo_cfg(cfg, &bm, &bn, &bk, &nw, &ns)) return false;
+  if (R != 3 || S != 3 || stride != 1 || pad != 1 || C % bk != 0) return false;
+  const int img = H * W;
+  HaloGeom h{};
+  if (bm <= img) {
+    if (bm % W != 0 || img % bm != 0) return false;
+    h.TH = bm / W;
+    h.TB = 1;
+  } else {
+    if (bm % img != 0) return false;
+    h.TH = H;
+    h.TB = bm / img;
+  }
+  const int rpi = 64 / (bk / 8);
+  h.HROWS = h.TB * (h.TH + 2) * (W + 2);
+  h.A_INS = (h.HROWS + rpi - 1) / rpi;
+  if (h.A_INS > kHaloAPW * nw) return false;
+  const size_t stage = (size_t)h.A_INS * rpi * bk + (size_t)9 * bn * bk;
+  const size_t bytes = (size_t)ns * stage * 2;
+  if (bytes > 160 * 1024) return false;
+  *g = h;
+  *lds = bytes;
+  return true;
+}
+
+bool conv_halo_ok(int cfg, int H, int W, int C, int R, int S, int stride, int pad) {
+  HaloGeom g;
+  size_t lds;
+  return halo_geom(cfg, H, W, C, R, S, stride, pad, &g, &lds);
+}
+
+int conv_num_halo_configs() { return kNumHaloConfigs; }
+int conv_halo_base() { return kHaloBase; }
+
+template <int BM, int BN, int BK, int WM, int WN, int NS, bool FLIP, bool STATS>
+static void launch_halo_t(const ConvArgs& a, const HaloGeom& g, size_t lds, hipStream_t s) {
+  auto kern = conv_halo_kernel<BM, BN, BK, WM, WN, NS, FLIP, STATS>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const long long M = (long long)a.B * a.OH * a.OW;
+  const dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((a.CO + BN - 1) / BN));
+  hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, a, g);
+}
+
+// true if launched (cfg is a halo config that applies to this geometry)
+template <bool FLIP, bool STATS>
+static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
+  HaloGeom g;
+  size_t lds;
+  if (a.GH != a.OH || a.GW != a.OW) return false;
+  if (!halo_geom(cfg, a.GH, a.GW, a.CI, a.R, a.S, a.stride, a.pad, &g, &lds)) return false;
+  switch (cfg - kHaloBase) {
+#define X(i, BM, BN, BK, WM, WN, NS) \
+  case i: launch_halo_t<BM, BN, BK, WM, WN, NS, FLIP, STATS>(a, g, lds, s); return true;
+    DMP_HALO_CONFIGS(X)
+#undef X
+  }
+  return false;
+}
+
 int conv_fwd_num_mblocks(long long M, int CO, int cfg) {
+  {
+    int bm, bn, bk, nw, ns;
+    if (halo_cfg(cfg, &bm, &bn, &bk, &nw, &ns)) return (int)((M + bm - 1) / bm);
+  }
   if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(M, CO);
   const int bm = config_bm(cfg);
   return (int)((M + bm - 1) / bm);
@@ -511,6 +870,10 @@ void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int
                      hipStream_t s, const float* bias) {
   ConvArgs a{x, w, y, part, B, H, W, CI, OH, OW, CO, R, S, stride, pad,
              (long long)B * OH * OW, bias, nullptr};
+  if (cfg >= kHaloBase) {
+    if (part ? launch_halo<false, true>(a, cfg, s) : launch_halo<false, false>(a, cfg, s)) return;
+    cfg = -1;   // not applicable to this geometry: heuristic implicit-GEMM tile
+  }
   if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(a.M, CO);
   if (part) dispatch<0, true>(a, cfg, 1, s);
   else dispatch<0, false>(a, cfg, 1, s);
@@ -523,6 +886,11 @@ void launch_conv_dgrad(const u16* dy, const u16* wt, u16* dx, int B, int H, int 
   const long long rows = (long long)B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
   ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad, rows, nullptr,
              addend};
+  if (cfg >= kHaloBase) {
+    // stride 1, 3x3, pad 1: dX = the same conv over dY with Wt and mirrored taps
+    if (launch_halo<true, false>(a, cfg, s)) return;
+    cfg = -1;
+  }
   if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(rows * stride * stride, CI);
   dispatch<1, false>(a, cfg, stride * stride, s);
 }

@@ -107,16 +107,31 @@ def _wgrad_candidates(K: int):
     return cands
 
 
+_HALO_ENABLED = os.environ.get("DMP_CONV_HALO", "1") != "0"
+
+
+def _halo_candidates(H, W, C, R, S, stride, pad):
+    """3x3 / stride-1 halo-tile kernels (csrc/conv.hip conv_halo_kernel) that apply
+    to a conv gathering a [*, C, H, W] input; timed by the tuner next to the
+    implicit-GEMM tiles."""
+    if not _HALO_ENABLED:
+        return []
+    return list(native().conv_halo_configs(H, W, C, R, S, stride, pad))
+
+
 def _fwd_cfg(x, w16, stride, pad):
     key = ("fwd", *x.shape, w16.shape[0], w16.shape[2], w16.shape[3], stride, pad)
-    return TUNER.best(key, lambda c: native().conv_fwd(x, w16, stride, pad, True, c),
-                      _igemm_candidates(w16.shape[0]))
+    cands = _igemm_candidates(w16.shape[0]) + _halo_candidates(
+        x.shape[2], x.shape[3], x.shape[1], w16.shape[2], w16.shape[3], stride, pad)
+    return TUNER.best(key, lambda c: native().conv_fwd(x, w16, stride, pad, True, c), cands)
 
 
 def _dgrad_cfg(dy, w16, H, W, stride, pad):
     key = ("dgrad", *dy.shape, w16.shape[1], H, W, w16.shape[2], w16.shape[3], stride, pad)
-    return TUNER.best(key, lambda c: native().conv_dgrad(dy, w16, H, W, stride, pad, c),
-                      _igemm_candidates(w16.shape[1]))
+    cands = _igemm_candidates(w16.shape[1])
+    if (H, W) == tuple(dy.shape[2:]):
+        cands += _halo_candidates(H, W, dy.shape[1], w16.shape[2], w16.shape[3], stride, pad)
+    return TUNER.best(key, lambda c: native().conv_dgrad(dy, w16, H, W, stride, pad, c), cands)
 
 
 def _wgrad_cfg(dy, x, shape, stride, pad):

@@ -88,6 +88,48 @@ def test_every_tile_config(shape):
         assert _rel(dw, wr.grad) < 1e-2, cfg
 
 
+HALO_SHAPES = [
+    # B, C, H, W, CO: every ResNet-18 CIFAR 3x3 stride-1 geometry, partial last tile
+    (4, 64, 32, 32, 64),
+    (3, 128, 16, 16, 128),
+    (5, 256, 8, 8, 256),
+    (9, 512, 4, 4, 512),
+    (2, 64, 8, 8, 128),
+]
+
+
+@pytest.mark.parametrize("B,C,H,W,CO", HALO_SHAPES)
+def test_halo_conv_configs(B, C, H, W, CO):
+    """3x3/stride-1 halo-tile kernel, every applicable config: forward (+BN partial
+    sums) and the mirrored-tap data gradient (+ residual addend) vs fp32."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    torch.manual_seed(0)
+    x = torch.randn(B, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(CO, C, 3, 3, device="cuda") / (C * 9) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    xr = x.float().requires_grad_(True)
+    yr = F.conv2d(xr, w.float(), None, 1, 1)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr.backward(dy.float())
+    add = torch.randn_like(x)
+    cfgs = list(nat.conv_halo_configs(H, W, C, 3, 3, 1, 1))
+    assert cfgs, "no halo config applies"
+    for cfg in cfgs:
+        y, part, G = nat.conv_fwd(x, w, 1, 1, True, cfg)
+        assert _rel(y, yr) < 1e-2, cfg
+        ps = part[:2 * int(G) * CO].view(2, int(G), CO).sum(1)
+        yf = y.float()
+        torch.testing.assert_close(ps[0], yf.sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+        torch.testing.assert_close(ps[1], (yf * yf).sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+    for cfg in list(nat.conv_halo_configs(H, W, CO, 3, 3, 1, 1)):
+        dx = nat.conv_dgrad(dy, w, H, W, 1, 1, cfg)
+        assert _rel(dx, xr.grad) < 1e-2, cfg
+        dxa = nat.conv_dgrad(dy, w, H, W, 1, 1, cfg, None, add)
+        assert _rel(dxa, xr.grad + add.float()) < 1e-2, cfg
+
+
 def test_conv_layer_autograd_and_bn_fusion():
     """Conv2d(native) -> BatchNorm2d(partials) matches the stock fp32 chain."""
     from distributed_ml_pytorch_amd.ops import layers as L
