@@ -809,6 +809,20 @@ std::vector<int64_t> conv_halo_configs(int64_t H, int64_t W, int64_t C, int64_t 
   return out;
 }
 
+// halo wgrad cfg ids applicable to dW of a conv over [B, CI, H, W] -> CO channels
+std::vector<int64_t> conv_wgrad_halo_configs(int64_t B, int64_t H, int64_t W, int64_t CI,
+                                             int64_t CO, int64_t R, int64_t S, int64_t stride,
+                                             int64_t pad) {
+  std::vector<int64_t> out;
+  for (int i = 0; i < dmp::conv_wgrad_num_halo_configs(); ++i) {
+    const int c = dmp::conv_wgrad_halo_base() + i;
+    if (dmp::conv_wgrad_halo_ok(c, (int)B, (int)H, (int)W, (int)CI, (int)CO, (int)R, (int)S,
+                                (int)stride, (int)pad))
+      out.push_back(c);
+  }
+  return out;
+}
+
 std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optional<Tensor> res,
                                          optional<Tensor> gamma, optional<Tensor> beta,
                                          optional<Tensor> running_mean,
@@ -852,6 +866,8 @@ PYBIND11_MODULE(_native, m) {
         py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("cfg") = -1);
   m.def("conv_configs", &conv_configs, "[(id, BM, BN, BK, threads)] of the compiled conv tiles");
+  m.def("conv_wgrad_halo_configs", &conv_wgrad_halo_configs,
+        "3x3/stride-1 halo wgrad cfg ids applicable to (B, H, W, CI, CO, R, S, stride, pad)");
   m.def("conv_halo_configs", &conv_halo_configs,
         "3x3/stride-1 halo-tile cfg ids applicable to (H, W, C, R, S, stride, pad)");
   m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials");

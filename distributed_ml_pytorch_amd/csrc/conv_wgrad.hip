@@ -244,6 +244,233 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
     }
 }
 
+// ------------------------------------------------- 3x3 stride-1 halo wgrad
+// dW[co][r][s][ci] += sum_p dY[p][co] * X[p shifted by (r-1, s-1)][ci] for 3x3 /
+// stride 1 / pad 1.  The gather kernel above fetches X once per tap column
+// tile; here a block owns one tap ROW r, a 64 x 64 (co, ci) tile and a run of
+// BM-pixel tiles (whole image rows / whole images, as the forward halo kernel),
+// and per tile stages dY [BM][64] plus the input rows the tap row reads,
+// X[h - 1 + r][-1 .. W] (W + 2 columns, zero outside the image), ONCE: the
+// three taps s = 0, 1, 2 are the same staged rows offset by s.  Both images are
+// [row][64] with the 32-B granule swizzle and read with ds_read_b64_tr_b16;
+// a lane supplies its own row address per tr read, so the shifted pixel->row
+// map needs no layout change.  4 waves, wave w: all 64 co x ci 16w..16w+15 x 3
+// taps (12 accumulator tiles).  Partial sums go to dW with fp32 atomics, or
+// plain read-add-write when one block owns the tile (splits == 1).
+struct WgradHaloGeom {
+  int TH, TB, XROWS, XINS, ntiles, tiles_per_split;
+};
+
+constexpr int kWhXPW = 8;   // max X-row DMA instructions per wave per tile
+
+template <int BM>
+__global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, WgradHaloGeom hg,
+                                                              int atomic) {
+  constexpr int NW = 4, CW = 64;                  // 64-channel rows (128 B)
+  constexpr int D_INS = BM * 8 / 64;              // dY DMA instructions per tile
+  constexpr int D_PW = D_INS / NW;
+  static_assert(D_INS % NW == 0, "dY split");
+  extern __shared__ __attribute__((aligned(16))) u16 lds_w[];
+  const int D_EL = BM * CW;
+  const int STAGE = D_EL + hg.XINS * 8 * CW;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ci0 = blockIdx.x * CW;
+  const int co0 = (blockIdx.y / 3) * CW, r = blockIdx.y % 3;
+  const int t_begin = blockIdx.z * hg.tiles_per_split;
+  const int t_end = min(hg.ntiles, t_begin + hg.tiles_per_split);
+  if (t_begin >= t_end) return;
+  const int H = a.GH, W = a.GW, C = a.CI, CO = a.CO, TH = hg.TH, W2 = W + 2;
+  const int img = H * W;
+  const long long P = a.P;
+
+  // dY DMA slots (fixed per lane): row of the tile, swizzled source column
+  int d_row[D_PW], d_col[D_PW];
+#pragma unroll
+  for (int j = 0; j < D_PW; ++j) {
+    const int row = (wid + j * NW) * 8 + lane / 8, pch = lane % 8;
+    d_row[j] = row;
+    d_col[j] = co0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8;
+  }
+  // X DMA slots: staged row -> (image in tile, row in tile, column incl. halo)
+  int x_tb[kWhXPW], x_th[kWhXPW], x_w[kWhXPW], x_col[kWhXPW];
+#pragma unroll
+  for (int j = 0; j < kWhXPW; ++j) {
+    const int row = (wid + j * NW) * 8 + lane / 8, pch = lane % 8;
+    const int tb = row / (TH * W2), rem = row - tb * TH * W2;
+    x_tb[j] = tb;
+    x_th[j] = rem / W2;
+    x_w[j] = rem - x_th[j] * W2 - 1;
+    x_col[j] = ci0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8;
+  }
+  const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.dy, 0, (int)(2 * P * CO), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, 0, (int)(2LL * a.B * H * W * C), 0x00020000);
+
+  auto stage = [&](int buf, int t) {
+    u16* Ds = lds_w + buf * STAGE;
+    u16* Xs = Ds + D_EL;
+    const long long m0 = (long long)t * BM;
+    const int b0 = (int)(m0 / img), h0 = (int)(m0 - (long long)b0 * img) / W;
+#pragma unroll
+    for (int j = 0; j < D_PW; ++j) {
+      const long long p = m0 + d_row[j];
+      bdma16w(rsD, p < P ? 2u * (unsigned)(p * CO + d_col[j]) : kOOBw, Ds + (wid + j * NW) * 512);
+    }
+#pragma unroll
+    for (int j = 0; j < kWhXPW; ++j) {
+      const int ins = wid + j * NW;
+      if (ins < hg.XINS) {
+        const int b = b0 + x_tb[j], h = h0 - 1 + r + x_th[j], w = x_w[j];
+        const bool ok = x_tb[j] < hg.TB && b < a.B && (unsigned)h < (unsigned)H &&
+                        (unsigned)w < (unsigned)W;
+        bdma16w(rsX, ok ? 2u * (unsigned)(((b * H + h) * W + w) * C + x_col[j]) : kOOBw,
+                Xs + ins * 512);
+      }
+    }
+  };
+
+  // staged X row of the lane's reduction rows (pixels pk*32 + 8g + q and +4)
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pc = li & 3;
+  int xr_lo[BM / 32], xr_hi[BM / 32];
+#pragma unroll
+  for (int pk = 0; pk < BM / 32; ++pk) {
+#pragma unroll
+    for (int hsel = 0; hsel < 2; ++hsel) {
+      const int pl = pk * 32 + 8 * g + q + 4 * hsel;
+      const int tb = pl / (TH * W), r2 = pl - tb * TH * W;
+      const int th = r2 / W, tw = r2 - th * W;
+      const int xr = (tb * TH + th) * W2 + tw;
+      if (hsel) xr_hi[pk] = xr; else xr_lo[pk] = xr;
+    }
+  }
+  auto tr = [&](const u16* img_, int row, int col) -> s16x4_t {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4_t*)(img_ + wg_off<CW>(row, col)));
+  };
+
+  f32x4 acc[3][4];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[s][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const u16* Ds = lds_w + buf * STAGE;
+    const u16* Xs = Ds + D_EL;
+#pragma unroll
+    for (int pk = 0; pk < BM / 32; ++pk) {
+      bf16x8 af[4], bx[3];
+      const int drow = pk * 32 + 8 * g + q;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const s16x4_t lo = tr(Ds, drow, i * 16 + 4 * pc), hi = tr(Ds, drow + 4, i * 16 + 4 * pc);
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const s16x4_t lo = tr(Xs, xr_lo[pk] + s, wid * 16 + 4 * pc);
+        const s16x4_t hi = tr(Xs, xr_hi[pk] + s, wid * 16 + 4 * pc);
+        bx[s] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[s][i] = mfma16w(af[i], bx[s], acc[s][i]);
+    }
+  };
+
+  stage(0, t_begin);
+  for (int t = t_begin; t < t_end; ++t) {
+    wait_vm<0>();                       // tile t landed (this wave's DMAs) ...
+    __builtin_amdgcn_s_barrier();       // ... for every wave; tile t-1's buffer is free
+    asm volatile("" ::: "memory");
+    if (t + 1 < t_end) stage((t + 1 - t_begin) & 1, t + 1);
+    compute((t - t_begin) & 1);
+  }
+  // D layout: lane holds rows co = 4*(lane>>4)+rr of column ci = lane & 15
+  const long long K = 9LL * C;
+  const int ci = ci0 + wid * 16 + (lane & 15);
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = co0 + i * 16 + 4 * (lane >> 4) + rr;
+        float* dst = a.dw + (long long)co * K + (r * 3 + s) * C + ci;
+        if (atomic) atomicAdd(dst, acc[s][i][rr]);
+        else *dst += acc[s][i][rr];
+      }
+}
+
+// halo wgrad cfg ids: kWhBase + bm_sel * 4 + spl, BM = 64 << bm_sel, target
+// block count 128 << spl
+constexpr int kWhBase = 1000;
+
+static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R, int S, int stride,
+                            int pad, WgradHaloGeom* g, int* bm_out, size_t* lds, int* splits) {
+  const int id = cfg - kWhBase;
+  if (id < 0 || id >= 12) return false;
+  const int bm = 64 << (id / 4), target = 128 << (id % 4);
+  if (R != 3 || S != 3 || stride != 1 || pad != 1 || CI % 64 || CO % 64) return false;
+  const int img = H * W;
+  WgradHaloGeom h{};
+  if (bm <= img) {
+    if (bm % W != 0 || img % bm != 0) return false;
+    h.TH = bm / W;
+    h.TB = 1;
+  } else {
+    if (bm % img != 0) return false;
+    h.TH = H;
+    h.TB = bm / img;
+  }
+  h.XROWS = h.TB * h.TH * (W + 2);
+  h.XINS = (h.XROWS + 7) / 8;
+  if (h.XINS > kWhXPW * 4) return false;
+  const long long M = (long long)B * img;
+  h.ntiles = (int)((M + bm - 1) / bm);
+  const int per = (CI / 64) * (CO / 64) * 3;
+  int sp = target / per;
+  if (sp < 1) sp = 1;
+  if (sp > h.ntiles) sp = h.ntiles;
+  h.tiles_per_split = (h.ntiles + sp - 1) / sp;
+  sp = (h.ntiles + h.tiles_per_split - 1) / h.tiles_per_split;
+  const size_t stage = (size_t)bm * 64 + (size_t)h.XINS * 8 * 64;
+  *lds = 2 * stage * 2;
+  if (*lds > 160 * 1024) return false;
+  *g = h;
+  *bm_out = bm;
+  *splits = sp;
+  return true;
+}
+
+bool conv_wgrad_halo_ok(int cfg, int B, int H, int W, int CI, int CO, int R, int S, int stride,
+                        int pad) {
+  WgradHaloGeom g;
+  int bm, sp;
+  size_t lds;
+  return wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &lds, &sp);
+}
+int conv_wgrad_halo_base() { return kWhBase; }
+int conv_wgrad_num_halo_configs() { return 12; }
+
+template <int BM>
+static void launch_wgrad_halo_t(const WgradArgs& a, const WgradHaloGeom& g, size_t lds, int splits,
+                                hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<BM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const dim3 grid((unsigned)(a.CI / 64), (unsigned)(a.CO / 64 * 3), (unsigned)splits);
+  hipLaunchKernelGGL(conv_wgrad_halo_kernel<BM>, grid, dim3(256), lds, s, a, g,
+                     splits > 1 ? 1 : 0);
+}
+
 // cfg bits: [1:0] BNW (0 auto, 1 -> 64, 2 -> 128, 3 -> 192), [2] BP (0 -> 64, 1 -> 32),
 // [3] NS (0 -> 2, 1 -> 3), [7:4] minimum rows of P per block in units of 512 (0 auto).
 template <int BNW, int WM, int WN>
@@ -261,6 +488,18 @@ void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int
                        int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s) {
   WgradArgs a{dy, x, dw, B, H, W, CI, OH, OW, CO, R, S, stride, pad, (long long)B * OH * OW, 0};
+  if (cfg >= kWhBase) {
+    WgradHaloGeom g;
+    int bm, sp;
+    size_t lds;
+    if (wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &lds, &sp)) {
+      if (bm == 64) launch_wgrad_halo_t<64>(a, g, lds, sp, s);
+      else if (bm == 128) launch_wgrad_halo_t<128>(a, g, lds, sp, s);
+      else launch_wgrad_halo_t<256>(a, g, lds, sp, s);
+      return;
+    }
+    cfg = -1;   // not applicable: gather kernel, heuristic variant
+  }
   const long long K = (long long)R * S * CI;
   const int sel = cfg < 0 ? 0 : (cfg & 3);
   int bnw = sel == 1 ? 64 : (sel == 2 ? 128 : (sel == 3 ? 192 : 0));

@@ -88,6 +88,11 @@ int conv_fwd_num_mblocks(long long M, int CO, int cfg);
 int conv_num_halo_configs();
 int conv_halo_base();
 bool conv_halo_ok(int cfg, int H, int W, int C, int R, int S, int stride, int pad);
+// 3x3 / stride-1 halo wgrad: cfg ids conv_wgrad_halo_base() + [0, conv_wgrad_num_halo_configs())
+int conv_wgrad_halo_base();
+int conv_wgrad_num_halo_configs();
+bool conv_wgrad_halo_ok(int cfg, int B, int H, int W, int CI, int CO, int R, int S, int stride,
+                        int pad);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int B, int H,
                      int W, int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
                      int cfg, hipStream_t s, const float* bias = nullptr);

@@ -141,8 +141,12 @@ def _wgrad_cfg(dy, x, shape, stride, pad):
     scratch = torch.empty(shape, dtype=torch.float32, device=x.device,
                           memory_format=torch.channels_last).zero_()
     K = shape[1] * shape[2] * shape[3]
-    return TUNER.best(key, lambda c: native().conv_wgrad(dy, x, scratch, stride, pad, c),
-                      _wgrad_candidates(K))
+    cands = _wgrad_candidates(K)
+    if _HALO_ENABLED:
+        cands += list(native().conv_wgrad_halo_configs(x.shape[0], x.shape[2], x.shape[3],
+                                                       shape[1], shape[0], shape[2], shape[3],
+                                                       stride, pad))
+    return TUNER.best(key, lambda c: native().conv_wgrad(dy, x, scratch, stride, pad, c), cands)
 
 
 class _NativeConv(Function):

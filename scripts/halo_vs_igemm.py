@@ -44,6 +44,17 @@ def main():
             tot_h += min(th, ti)
             print(f"{str((B, C, H, W)):>26} {name:>6} {ti:9.1f} {ci:4d} {th:8.1f} {ch:4d} "
                   f"{flop / ti / 1e6:6.0f}/{flop / th / 1e6:.0f}")
+        from distributed_ml_pytorch_amd.ops.conv import _wgrad_candidates
+
+        dw = torch.zeros(C, C, 3, 3, device="cuda").contiguous(memory_format=CL)
+        run = lambda c: nat.conv_wgrad(dy, x, dw, 1, 1, c)     # noqa: E731
+        ti, ci = min((timeit(lambda c=c: run(c)), c) for c in _wgrad_candidates(9 * C))
+        hw = list(nat.conv_wgrad_halo_configs(B, H, W, C, C, 3, 3, 1, 1))
+        th, ch = min((timeit(lambda c=c: run(c)), c) for c in hw) if hw else (float("nan"), -1)
+        tot_i += ti
+        tot_h += min(th, ti)
+        print(f"{str((B, C, H, W)):>26} {'wgrad':>6} {ti:9.1f} {ci:4d} {th:8.1f} {ch:4d} "
+              f"{flop / ti / 1e6:6.0f}/{flop / th / 1e6:.0f}")
     print(f"total igemm {tot_i:.1f} us, with halo where faster {tot_h:.1f} us")
 
 

@@ -100,8 +100,9 @@ HALO_SHAPES = [
 
 @pytest.mark.parametrize("B,C,H,W,CO", HALO_SHAPES)
 def test_halo_conv_configs(B, C, H, W, CO):
-    """3x3/stride-1 halo-tile kernel, every applicable config: forward (+BN partial
-    sums) and the mirrored-tap data gradient (+ residual addend) vs fp32."""
+    """3x3/stride-1 halo-tile kernels, every applicable config: forward (+BN partial
+    sums), the mirrored-tap data gradient (+ residual addend) and the tap-row
+    weight gradient (fp32 accumulate) vs fp32."""
     from distributed_ml_pytorch_amd.ops._ext import native
 
     nat = native()
@@ -110,7 +111,8 @@ def test_halo_conv_configs(B, C, H, W, CO):
     w = (torch.randn(CO, C, 3, 3, device="cuda") / (C * 9) ** 0.5).to(torch.bfloat16)
     w = w.contiguous(memory_format=CL)
     xr = x.float().requires_grad_(True)
-    yr = F.conv2d(xr, w.float(), None, 1, 1)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, 1, 1)
     dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
     yr.backward(dy.float())
     add = torch.randn_like(x)
@@ -128,6 +130,14 @@ def test_halo_conv_configs(B, C, H, W, CO):
         assert _rel(dx, xr.grad) < 1e-2, cfg
         dxa = nat.conv_dgrad(dy, w, H, W, 1, 1, cfg, None, add)
         assert _rel(dxa, xr.grad + add.float()) < 1e-2, cfg
+    wcfgs = list(nat.conv_wgrad_halo_configs(B, H, W, C, CO, 3, 3, 1, 1))
+    assert wcfgs, "no halo wgrad config applies"
+    for cfg in wcfgs:
+        dw = torch.zeros(CO, C, 3, 3, device="cuda").contiguous(memory_format=CL)
+        nat.conv_wgrad(dy, x, dw, 1, 1, cfg)
+        assert _rel(dw, wr.grad) < 1e-2, cfg
+        nat.conv_wgrad(dy, x, dw, 1, 1, cfg)       # accumulates (atomic or owned tiles)
+        assert _rel(dw, 2 * wr.grad) < 1e-2, cfg
 
 
 def test_conv_layer_autograd_and_bn_fusion():
