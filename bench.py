@@ -171,8 +171,8 @@ def main():
             "dtype": a.dtype,
             "data": f"synthetic ({'x'.join(map(str, in_shape))} images, random labels, "
                     "HBM-resident); random-init weights",
-            "config": {"model": f"{a.model} (CIFAR stem)" if a.model.startswith("resnet")
-                       else a.model,
+            "config": {"model": (f"{a.model} ({'CIFAR' if in_shape[-1] <= 64 else 'ImageNet'} stem)"
+                                 if a.model.startswith("resnet") else a.model),
                        "global_batch": global_batch, "per_gpu_batch": a.batch,
                        "seq_len": None, "image": "x".join(map(str, in_shape)),
                        "parallelism": par, "n_push": a.n_push, "n_pull": a.n_pull,
