@@ -617,7 +617,7 @@ void check_rows_bf16(const Tensor& t, const char* name) {
 }
 
 std::vector<Tensor> layernorm_fwd(Tensor x, optional<Tensor> gamma, optional<Tensor> beta,
-                                  double eps) {
+                                  double eps, optional<Tensor> residual) {
   check_rows_bf16(x, "x");
   const int64_t D = x.size(-1);
   const int64_t rows = x.numel() / D;
@@ -630,15 +630,27 @@ std::vector<Tensor> layernorm_fwd(Tensor x, optional<Tensor> gamma, optional<Ten
   auto y = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({rows}, fopt), rstd = at::empty({rows}, fopt);
+  Tensor r, h;
+  const bool fused = residual.has_value() && residual->defined();
+  if (fused) {
+    r = residual->contiguous();
+    check_rows_bf16(r, "residual");
+    TORCH_CHECK(r.sizes() == x.sizes(), "layernorm: residual shape mismatch");
+    h = at::empty_like(x);
+  }
   dmp::launch_layernorm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                             ptr_or_null<float>(gamma), ptr_or_null<float>(beta),
                             reinterpret_cast<uint16_t*>(y.data_ptr()), mean.data_ptr<float>(),
-                            rstd.data_ptr<float>(), rows, (int)D, (float)eps, cur_stream());
+                            rstd.data_ptr<float>(), rows, (int)D, (float)eps, cur_stream(),
+                            fused ? reinterpret_cast<const uint16_t*>(r.data_ptr()) : nullptr,
+                            fused ? reinterpret_cast<uint16_t*>(h.data_ptr()) : nullptr);
+  if (fused) return {y, mean, rstd, h};
   return {y, mean, rstd};
 }
 
 Tensor layernorm_bwd(Tensor x, Tensor dy, optional<Tensor> gamma, Tensor mean, Tensor rstd,
-                     optional<Tensor> dgamma, optional<Tensor> dbeta, optional<Tensor> slots) {
+                     optional<Tensor> dgamma, optional<Tensor> dbeta, optional<Tensor> slots,
+                     optional<Tensor> dres) {
   check_rows_bf16(x, "x");
   dy = dy.contiguous();
   check_rows_bf16(dy, "dy");
@@ -667,12 +679,20 @@ Tensor layernorm_bwd(Tensor x, Tensor dy, optional<Tensor> gamma, Tensor mean, T
     }
   }
   auto dx = at::empty_like(x);
+  Tensor dr;
+  if (dres.has_value() && dres->defined()) {
+    dr = dres->contiguous();
+    check_rows_bf16(dr, "dres");
+    TORCH_CHECK(dr.sizes() == x.sizes(), "layernorm_bwd: dres shape mismatch");
+  }
   dmp::launch_layernorm_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                             reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                             ptr_or_null<float>(gamma), mean.data_ptr<float>(),
                             rstd.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
                             ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta),
-                            grads ? sl.data_ptr<float>() : nullptr, rows, (int)D, cur_stream());
+                            grads ? sl.data_ptr<float>() : nullptr, rows, (int)D, cur_stream(),
+                            dr.defined() ? reinterpret_cast<const uint16_t*>(dr.data_ptr())
+                                         : nullptr);
   return dx;
 }
 
@@ -891,10 +911,13 @@ PYBIND11_MODULE(_native, m) {
   m.def("bn_bwd", &bn_bwd, "NHWC batchnorm(+residual)(+relu) backward", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"), py::arg("slots") = py::none());
-  m.def("layernorm_fwd", &layernorm_fwd, "row LayerNorm forward -> (y, mean, rstd)");
+  m.def("layernorm_fwd", &layernorm_fwd,
+        "row LayerNorm forward -> (y, mean, rstd[, h = x + residual])", py::arg("x"),
+        py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("residual") = py::none());
   m.def("layernorm_bwd", &layernorm_bwd, "row LayerNorm backward (dgamma/dbeta accumulated)",
         py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
-        py::arg("dgamma"), py::arg("dbeta"), py::arg("slots") = py::none());
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("slots") = py::none(),
+        py::arg("dres") = py::none());
   m.def("layernorm_num_slots", &dmp::layernorm_num_slots, "slot rows of the LayerNorm param grads");
   m.def("colsum_acc", &colsum_acc, "bias gradient: out[n] += sum_m dy[m][n] (bf16 -> fp32)",
         py::arg("dy"), py::arg("out"), py::arg("slots") = py::none());

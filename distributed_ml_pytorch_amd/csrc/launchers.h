@@ -56,12 +56,15 @@ void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, in
 // transformer.hip: LayerNorm / GELU / softmax (ViT)
 bool layernorm_supported(int D);
 int layernorm_num_slots();
+// radd/hout: fused residual add (h = x + radd written to hout, LayerNorm of h)
 void launch_layernorm_fwd(const uint16_t* x, const float* gamma, const float* beta, uint16_t* y,
                           float* mean, float* rstd, long long rows, int D, float eps,
-                          hipStream_t s);
+                          hipStream_t s, const uint16_t* radd = nullptr, uint16_t* hout = nullptr);
+// dadd: gradient added to dx (the residual stream's direct gradient)
 void launch_layernorm_bwd(const uint16_t* x, const uint16_t* dy, const float* gamma,
                           const float* mean, const float* rstd, uint16_t* dx, float* dgamma,
-                          float* dbeta, float* slots, long long rows, int D, hipStream_t s);
+                          float* dbeta, float* slots, long long rows, int D, hipStream_t s,
+                          const uint16_t* dadd = nullptr);
 void launch_gelu_fwd(const uint16_t* x, uint16_t* y, long long n, hipStream_t s);
 void launch_gelu_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, long long n,
                      hipStream_t s);

@@ -43,12 +43,15 @@ __device__ __forceinline__ void ld8f(const float* p, float v[8]) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-// y = (x - mean) * rstd * gamma + beta; saves mean, rstd (fp32 per row)
+// y = (x - mean) * rstd * gamma + beta; saves mean, rstd (fp32 per row).
+// With radd: the residual add of a pre-norm transformer block is fused in --
+// h = bf16(x + radd) is written to hout and normalised (one pass over the
+// stream instead of an add kernel plus a LayerNorm read).
 template <int LR, int MAXC>
 __global__ void __launch_bounds__(256) layernorm_fwd_kernel(
     const u16* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
     u16* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out, long long rows,
-    int D, float eps) {
+    int D, float eps, const u16* __restrict__ radd, u16* __restrict__ hout) {
   constexpr int RPW = 64 / LR;
   const int lane = threadIdx.x & 63, sub = lane % LR;
   const long long row = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LR;
@@ -61,6 +64,13 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(
   for (int c = 0; c < MAXC; ++c) {
     if (c < nc) {
       ld8(xr + (sub + c * LR) * 8, v[c]);
+      if (radd) {
+        float t[8];
+        ld8(radd + (ok ? row : 0) * D + (sub + c * LR) * 8, t);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[c][k] = bf2f(f2bf(v[c][k] + t[k]));
+        if (ok) st8(hout + row * D + (sub + c * LR) * 8, v[c]);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) s += v[c][k];
     }
@@ -100,7 +110,9 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(
   }
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma.
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) (+ dadd),  g = dy * gamma.
+// dadd: the gradient reaching the residual-stream value h directly (fused
+// add-LayerNorm), summed in fp32 before the single bf16 rounding.
 // dgamma / dbeta: per-lane partials over the rows the wave visits, folded over
 // the wave's row groups (butterfly) and the 4 waves (LDS), then added into
 // slot blockIdx % kLnSlots of a persistent [kLnSlots][2][D] buffer (<= 32
@@ -113,7 +125,7 @@ template <int LR, int MAXC>
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, const float* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, u16* __restrict__ dx,
-    float* __restrict__ slots, long long rows, int D) {
+    float* __restrict__ slots, long long rows, int D, const u16* __restrict__ dadd) {
   constexpr int RPW = 64 / LR;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, sub = lane % LR;
   const int nc = D / (8 * LR);
@@ -162,6 +174,12 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(
 #pragma unroll
           for (int k = 0; k < 8; ++k)
             o[k] = rstd * (dv[c][k] * (gamma ? gm[k] : 1.f) - m1 - xh[c][k] * m2);
+          if (dadd) {
+            float t[8];
+            ld8(dadd + r * D + e0, t);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] += t[k];
+          }
           st8(dx + r * D + e0, o);
         }
       }
@@ -368,17 +386,18 @@ bool layernorm_supported(int D) { return D > 0 && D % 8 == 0 && D / 8 / ln_lanes
 
 void launch_layernorm_fwd(const u16* x, const float* gamma, const float* beta, u16* y,
                           float* mean, float* rstd, long long rows, int D, float eps,
-                          hipStream_t s) {
+                          hipStream_t s, const u16* radd, u16* hout) {
   const int lr = ln_lanes(D), nc = D / 8 / lr;
   const long long rows_per_block = 4LL * (64 / lr);
   const dim3 grid((unsigned)((rows + rows_per_block - 1) / rows_per_block));
-  DMP_LN_BY_LR(layernorm_fwd_kernel, lr, nc, grid, 0, x, gamma, beta, y, mean, rstd, rows, D, eps);
+  DMP_LN_BY_LR(layernorm_fwd_kernel, lr, nc, grid, 0, x, gamma, beta, y, mean, rstd, rows, D, eps,
+               radd, hout);
 }
 
 // slots: [kLnSlots][2][D] fp32, zero on entry and on return (nullptr: no param grads)
 void launch_layernorm_bwd(const u16* x, const u16* dy, const float* gamma, const float* mean,
                           const float* rstd, u16* dx, float* dgamma, float* dbeta, float* slots,
-                          long long rows, int D, hipStream_t s) {
+                          long long rows, int D, hipStream_t s, const u16* dadd) {
   const int lr = ln_lanes(D), nc = D / 8 / lr;
   const long long rows_per_block = 4LL * (64 / lr);
   long long blocks = (rows + rows_per_block - 1) / rows_per_block;
@@ -386,7 +405,7 @@ void launch_layernorm_bwd(const u16* x, const u16* dy, const float* gamma, const
   const bool grads = slots != nullptr && (dgamma != nullptr || dbeta != nullptr);
   const size_t lds = grads ? (size_t)8 * D * sizeof(float) : 0;
   DMP_LN_BY_LR(layernorm_bwd_kernel, lr, nc, dim3((unsigned)blocks), lds, x, dy, gamma, mean, rstd,
-               dx, grads ? slots : nullptr, rows, D);
+               dx, grads ? slots : nullptr, rows, D, dadd);
   if (grads)
     hipLaunchKernelGGL(layernorm_param_grad_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s,
                        slots, dgamma, dbeta, D);

@@ -25,14 +25,21 @@ from ..ops.functional import compute_weight
 
 class LayerNorm(nn.LayerNorm):
     def forward(self, x):
-        slots = None
-        if x.is_cuda and self.weight is not None and self.weight.requires_grad:
-            n = DF.LN_SLOTS * 2 * x.shape[-1]
-            slots = self.__dict__.get("_dmp_slots")
-            if slots is None or slots.device != x.device or slots.numel() != n:
-                slots = torch.zeros(n, dtype=torch.float32, device=x.device)
-                self.__dict__["_dmp_slots"] = slots
-        return DF.layer_norm(x, self.weight, self.bias, self.eps, slots)
+        return DF.layer_norm(x, self.weight, self.bias, self.eps, self._slots(x))
+
+    def _slots(self, x):
+        if not (x.is_cuda and self.weight is not None and self.weight.requires_grad):
+            return None
+        n = DF.LN_SLOTS * 2 * x.shape[-1]
+        slots = self.__dict__.get("_dmp_slots")
+        if slots is None or slots.device != x.device or slots.numel() != n:
+            slots = torch.zeros(n, dtype=torch.float32, device=x.device)
+            self.__dict__["_dmp_slots"] = slots
+        return slots
+
+    def add_forward(self, x, r):
+        """(h, LayerNorm(h)) with h = x + r, fused (pre-norm residual add)."""
+        return DF.add_layer_norm(x, r, self.weight, self.bias, self.eps, self._slots(x))
 
 
 class Attention(nn.Module):
@@ -61,6 +68,18 @@ class Block(nn.Module):
     def forward(self, x):
         x = x + self.attn(self.norm1(x))
         return x + self.fc2(DF.gelu(self.fc1(self.norm2(x))))
+
+    def forward_fused(self, h, pending=None):
+        """Residual stream ``h`` plus the previous block's unadded MLP output
+        ``pending``: every residual add is fused into the LayerNorm that reads
+        its result (add + norm1, add + norm2).  Returns ``(h, mlp_out)`` with
+        ``mlp_out`` still to be added by the caller (next block / final norm)."""
+        if pending is None:
+            y = self.norm1(h)
+        else:
+            h, y = self.norm1.add_forward(h, pending)
+        h, y = self.norm2.add_forward(h, self.attn(y))
+        return h, self.fc2(DF.gelu(self.fc1(y)))
 
 
 class VisionTransformer(nn.Module):
@@ -92,10 +111,14 @@ class VisionTransformer(nn.Module):
         h = h.flatten(2).transpose(1, 2)              # [B, N, D]
         cls = compute_weight(self.cls_token, h.dtype).expand(h.shape[0], -1, -1)
         h = torch.cat([cls, h], dim=1) + compute_weight(self.pos_embed, h.dtype)
+        pending = None
         for blk in self.blocks:
-            h = blk(h)
-        h = self.norm(h)
-        return self.head(h[:, 0].contiguous())
+            h, pending = blk.forward_fused(h, pending)
+        if pending is None:
+            y = self.norm(h)
+        else:
+            _, y = self.norm.add_forward(h, pending)
+        return self.head(y[:, 0].contiguous())
 
 
 def vit_b16(num_classes: int = 1000, image_size: int = 224) -> VisionTransformer:

@@ -307,6 +307,46 @@ class _LayerNorm(Function):
         return dx, ret_g, ret_b, None, None
 
 
+class _AddLayerNorm(Function):
+    """h = x + r; y = LayerNorm(h) in one native pass (pre-norm transformer
+    residual add fused into the next LayerNorm).  Backward: dh_total = dh +
+    LN_bwd(dy) formed inside the LayerNorm-backward kernel; x and r both get it."""
+
+    @staticmethod
+    def forward(ctx, x, r, gamma, beta, eps, slots=None):
+        ctx.set_materialize_grads(False)
+        x = x.contiguous()
+        g32 = gamma.detach() if gamma is not None else None
+        b32 = beta.detach() if beta is not None else None
+        y, mean, rstd, h = native().layernorm_fwd(x, g32, b32, float(eps), r.contiguous())
+        ctx.save_for_backward(h, mean, rstd)
+        ctx.gamma, ctx.beta, ctx.slots = gamma, beta, slots
+        return h, y
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        if dy is None:
+            return dh, dh, None, None, None, None
+        h, mean, rstd = ctx.saved_tensors
+        gamma, beta = ctx.gamma, ctx.beta
+        dg_arena, db_arena = _arena_grad(gamma), _arena_grad(beta)
+        need_g = gamma is not None and ctx.needs_input_grad[2]
+        need_b = beta is not None and ctx.needs_input_grad[3]
+        dg = dg_arena if dg_arena is not None else (
+            torch.zeros_like(gamma, dtype=torch.float32) if need_g else None)
+        db = db_arena if db_arena is not None else (
+            torch.zeros_like(beta, dtype=torch.float32) if need_b else None)
+        g32 = gamma.detach() if gamma is not None else None
+        if dh is not None and dh.dtype != h.dtype:
+            dh = dh.to(h.dtype)
+        dx = native().layernorm_bwd(h, dy.to(h.dtype), g32, mean, rstd, dg, db, ctx.slots, dh)
+        if dg_arena is not None or db_arena is not None:
+            _notify(gamma, beta)
+        ret_g = None if (dg_arena is not None or not need_g) else dg.to(gamma.dtype)
+        ret_b = None if (db_arena is not None or not need_b) else db.to(beta.dtype)
+        return dx, dx, ret_g, ret_b, None, None
+
+
 LN_SLOTS = 32   # csrc/transformer.hip kLnSlots
 
 
@@ -319,6 +359,18 @@ def layernorm_supported(D: int) -> bool:
     while lr > 1 and nch % lr:
         lr //= 2
     return nch // lr <= 8
+
+
+def add_layer_norm(x, r, weight, bias, eps: float, slots=None):
+    """``h = x + r`` and ``LayerNorm(h)`` -> ``(h, y)``: one native pass for bf16 GPU
+    rows (``csrc/transformer.hip``), add + :func:`layer_norm` otherwise."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and r.dtype == torch.bfloat16
+            and x.shape == r.shape and layernorm_supported(x.shape[-1])
+            and (weight is None or weight.dtype == torch.float32)
+            and (bias is None or bias.dtype == torch.float32)):
+        return _AddLayerNorm.apply(x, r, weight, bias, eps, slots)
+    h = x + r
+    return h, layer_norm(h, weight, bias, eps, slots)
 
 
 def layer_norm(x, weight, bias, eps: float, slots=None):

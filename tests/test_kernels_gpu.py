@@ -264,6 +264,43 @@ def test_layernorm_kernel(rows, D):
         assert float(slots.abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("rows,D,use_h", [(12608, 768, True), (394, 768, False), (37, 200, True)])
+def test_add_layernorm_kernel(rows, D, use_h):
+    """Fused residual add + LayerNorm: h = bf16(x + r), y = LN(h); the backward
+    adds the residual stream's own gradient (dh) inside the LN-backward kernel."""
+    from distributed_ml_pytorch_amd.ops.functional import LN_SLOTS, add_layer_norm
+
+    torch.manual_seed(0)
+    slots = torch.zeros(LN_SLOTS * 2 * D, device="cuda")
+    rel = lambda a, r: float((a.float() - r).norm() / r.norm())
+    x = torch.randn(rows, D, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    r = torch.randn(rows, D, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(D, device="cuda")).requires_grad_(True)
+    b = (0.1 * torch.randn(D, device="cuda")).requires_grad_(True)
+    h, y = add_layer_norm(x, r, w, b, 1e-6, slots)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    hr = xr + rr
+    yr = F.layer_norm(hr, (D,), wr, br, 1e-6)
+    torch.testing.assert_close(h.float(), hr, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    gy = torch.randn_like(yr).to(torch.bfloat16)
+    gh = torch.randn_like(hr).to(torch.bfloat16)
+    if use_h:
+        torch.autograd.backward([y, h], [gy, gh])
+        torch.autograd.backward([yr, hr], [gy.float(), gh.float()])
+    else:
+        y.backward(gy)
+        yr.backward(gy.float())
+    assert rel(x.grad, xr.grad) < 1e-2
+    assert rel(r.grad, rr.grad) < 1e-2
+    assert rel(w.grad, wr.grad) < 1e-2
+    assert rel(b.grad, br.grad) < 1e-2
+    assert float(slots.abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("M,N", [(12608, 768), (300, 3072), (7, 8), (1000, 4104)])
 def test_colsum_acc(M, N):
     from distributed_ml_pytorch_amd.ops._ext import native
