@@ -13,7 +13,9 @@
 // Compile-time variants (host tuner picks per shape, ops/tuner.py):
 //   BNW  - k columns per block (64 / 128 / 192; a 192 tile spans three taps so
 //          dY is re-read K/192 times instead of once per tap)
-//   WM x WN wave layout over the 64 x BNW tile: the LDS-read : MFMA ratio of a
+//   BMW  - output channels per block (64, or 128 for wide 1x1 GEMMs such as the
+//          ViT linear layers: half the dY re-reads, 20 tr-reads per 24 MFMAs)
+//   WM x WN wave layout over the BMW x BNW tile: the LDS-read : MFMA ratio of a
 //          wave tile TM x TN is (TM+TN)*2 tr-reads per TM*TN MFMAs; the CU does
 //          ~2 tr-reads per MFMA slot, so thin 64x16 wave tiles are LDS-bound
 //          while 64x48 ones are MFMA-bound
@@ -81,9 +83,9 @@ __device__ __forceinline__ int wg_off(int row, int col) {
   return row * ROWE + ((((col >> 4) ^ wg_f<ROWE>(row))) << 4) + (col & 15);
 }
 
-template <int BNW, int WM, int WN, int BP, int NS>
+template <int BNW, int WM, int WN, int BP, int NS, int BMW>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
-  constexpr int BMW = 64, NW = 4;
+  constexpr int NW = 4;
   static_assert(WM * WN == NW, "4 waves");
   constexpr int TM = BMW / WM / 16, TN = BNW / WN / 16;
   constexpr int A_EL = BP * BMW, B_EL = BP * BNW;
@@ -472,15 +474,16 @@ static void launch_wgrad_halo_t(const WgradArgs& a, const WgradHaloGeom& g, size
 }
 
 // cfg bits: [1:0] BNW (0 auto, 1 -> 64, 2 -> 128, 3 -> 192), [2] BP (0 -> 64, 1 -> 32),
-// [3] NS (0 -> 2, 1 -> 3), [7:4] minimum rows of P per block in units of 512 (0 auto).
-template <int BNW, int WM, int WN>
+// [3] NS (0 -> 2, 1 -> 3), [7:4] minimum rows of P per block in units of 512 (0 auto),
+// [8] BMW 128 (CO % 128 == 0).
+template <int BNW, int WM, int WN, int BMW = 64>
 static void launch_wgrad_variant(const WgradArgs& a, dim3 grid, int bp, int ns, hipStream_t s) {
   if (bp == 32) {
-    if (ns == 3) hipLaunchKernelGGL((conv_wgrad_kernel<BNW, WM, WN, 32, 3>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((conv_wgrad_kernel<BNW, WM, WN, 32, 2>), grid, dim3(256), 0, s, a);
+    if (ns == 3) hipLaunchKernelGGL((conv_wgrad_kernel<BNW, WM, WN, 32, 3, BMW>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<BNW, WM, WN, 32, 2, BMW>), grid, dim3(256), 0, s, a);
   } else {
-    if (ns == 3) hipLaunchKernelGGL((conv_wgrad_kernel<BNW, WM, WN, 64, 3>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((conv_wgrad_kernel<BNW, WM, WN, 64, 2>), grid, dim3(256), 0, s, a);
+    if (ns == 3) hipLaunchKernelGGL((conv_wgrad_kernel<BNW, WM, WN, 64, 3, BMW>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<BNW, WM, WN, 64, 2, BMW>), grid, dim3(256), 0, s, a);
   }
 }
 
@@ -507,7 +510,8 @@ void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int
   if (K % bnw != 0) bnw = 64;
   const int bp = (cfg >= 0 && (cfg & 4)) ? 32 : 64;
   const int ns = (cfg >= 0 && (cfg & 8)) ? 3 : 2;
-  const long long tiles = (K / bnw) * (CO / 64);
+  const int bmw = (cfg >= 0 && (cfg & 256) && CO % 128 == 0) ? 128 : 64;
+  const long long tiles = (K / bnw) * (CO / bmw);
   long long min_chunk = cfg < 0 ? 0 : (long long)((cfg >> 4) & 15) * 512;
   if (min_chunk <= 0) min_chunk = 2048;
   long long splits = (768 + tiles - 1) / tiles;
@@ -516,7 +520,13 @@ void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int
   chunk = (chunk + bp - 1) / bp * bp;
   splits = (a.P + chunk - 1) / chunk;
   a.p_chunk = (int)chunk;
-  const dim3 grid((unsigned)(K / bnw), (unsigned)(CO / 64), (unsigned)splits);
+  const dim3 grid((unsigned)(K / bnw), (unsigned)(CO / bmw), (unsigned)splits);
+  if (bmw == 128) {
+    if (bnw == 192) launch_wgrad_variant<192, 2, 2, 128>(a, grid, bp, ns, s);
+    else if (bnw == 128) launch_wgrad_variant<128, 2, 2, 128>(a, grid, bp, ns, s);
+    else launch_wgrad_variant<64, 2, 2, 128>(a, grid, bp, ns, s);
+    return;
+  }
   if (bnw == 192) launch_wgrad_variant<192, 1, 4>(a, grid, bp, ns, s);
   else if (bnw == 128) launch_wgrad_variant<128, 2, 2>(a, grid, bp, ns, s);
   else launch_wgrad_variant<64, 2, 2>(a, grid, bp, ns, s);

@@ -94,16 +94,18 @@ def _igemm_candidates(out_channels: int):
     return [c[0] for c in _configs() if c[2] <= max(64, out_channels)]
 
 
-def _wgrad_candidates(K: int):
-    """cfg = BNW sel | BP32 << 2 | NS3 << 3 | (min P rows / 512) << 4 (csrc/conv_wgrad.hip)."""
+def _wgrad_candidates(K: int, CO: int | None = None):
+    """cfg = BNW sel | BP32 << 2 | NS3 << 3 | (min P rows / 512) << 4 | BMW128 << 8
+    (csrc/conv_wgrad.hip); the 128-channel tiles only when ``CO % 128 == 0``."""
     cands = []
-    for sel, bnw in ((1, 64), (2, 128), (3, 192)):
-        if K % bnw:
-            continue
-        for bp32 in (0, 1):
-            for ns3 in (0, 1):
-                for chunk in (2, 4, 8):          # x512 rows of P per block
-                    cands.append(sel | (bp32 << 2) | (ns3 << 3) | (chunk << 4))
+    for bm in ((0, 1) if CO is not None and CO % 128 == 0 else (0,)):
+        for sel, bnw in ((1, 64), (2, 128), (3, 192)):
+            if K % bnw:
+                continue
+            for bp32 in (0, 1):
+                for ns3 in (0, 1):
+                    for chunk in (2, 4, 8):          # x512 rows of P per block
+                        cands.append(sel | (bp32 << 2) | (ns3 << 3) | (chunk << 4) | (bm << 8))
     return cands
 
 
@@ -141,7 +143,7 @@ def _wgrad_cfg(dy, x, shape, stride, pad):
     scratch = torch.empty(shape, dtype=torch.float32, device=x.device,
                           memory_format=torch.channels_last).zero_()
     K = shape[1] * shape[2] * shape[3]
-    cands = _wgrad_candidates(K)
+    cands = _wgrad_candidates(K, shape[0])
     if _HALO_ENABLED:
         cands += list(native().conv_wgrad_halo_configs(x.shape[0], x.shape[2], x.shape[3],
                                                        shape[1], shape[0], shape[2], shape[3],

@@ -55,7 +55,7 @@ def main():
         # weight gradient accumulated in fp32
         tb = timeit(lambda: torch.ops.aten.addmm.dtype_out(g, dy.t(), x, torch.float32, out=g))
         best = min((timeit(lambda c=c: nat.conv_wgrad(dy4, x4, g4, 1, 0, c)), c)
-                   for c in _wgrad_candidates(K))
+                   for c in _wgrad_candidates(K, N))
         print(f"{K:>7}->{N:<7} {'wgrad':>6} {tb*1e3:9.1f} {best[0]*1e3:10.1f} {best[1]:5d}  "
               f"{flop/tb/1e9:.0f}/{flop/best[0]/1e9:.0f}")
 

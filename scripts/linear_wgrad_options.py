@@ -37,7 +37,7 @@ def main():
         dy4 = dy.view(M, 1, 1, N).permute(0, 3, 1, 2)
         g4 = g.view(N, K, 1, 1)
         tn, cfg = min((timeit(lambda c=c: nat.conv_wgrad(dy4, x4, g4, 1, 0, c)), c)
-                      for c in _wgrad_candidates(K))
+                      for c in _wgrad_candidates(K, N))
         tb = timeit(lambda: torch.mm(dy.t(), x))
         tba = timeit(lambda: g.add_(torch.mm(dy.t(), x)))
         tf = timeit(lambda: torch.ops.aten.addmm.dtype_out(g, dy.t(), x, torch.float32, out=g))

@@ -82,7 +82,7 @@ def test_every_tile_config(shape):
         assert _rel(dx, xr.grad) < 1e-2, cfg
     from distributed_ml_pytorch_amd.ops.conv import _wgrad_candidates
 
-    for cfg in _wgrad_candidates(CI * k * k):
+    for cfg in _wgrad_candidates(CI * k * k, CO):
         dw = torch.zeros(CO, CI, k, k, device="cuda").contiguous(memory_format=CL)
         nat.conv_wgrad(dy, x, dw, st, pd, cfg)
         assert _rel(dw, wr.grad) < 1e-2, cfg
