@@ -436,7 +436,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   return dx;
 }
 
-void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t cfg) {
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t cfg,
+                optional<Tensor> dbias) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc_bf16(dy, "dy");
   check_nhwc_bf16(x, "x");
@@ -447,10 +448,17 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int
   auto g = conv_geom(x, dw, stride, pad);
   TORCH_CHECK(dy.size(0) == g.B && dy.size(1) == g.CO && dy.size(2) == g.OH && dy.size(3) == g.OW,
               "wgrad: dy shape mismatch");
+  float* db = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(dbias->is_cuda() && dbias->scalar_type() == at::kFloat &&
+                    dbias->is_contiguous() && dbias->numel() == g.CO,
+                "wgrad: dbias must be a contiguous fp32 [CO] GPU tensor");
+    db = dbias->data_ptr<float>();
+  }
   dmp::launch_conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                          reinterpret_cast<const uint16_t*>(x.data_ptr()), dw.data_ptr<float>(),
                          g.B, g.H, g.W, g.CI, g.OH, g.OW, g.CO, g.R, g.S, (int)stride, (int)pad,
-                         (int)cfg, cur_stream());
+                         (int)cfg, cur_stream(), db);
 }
 
 // few-input-channel (stem) convolutions: x any dense bf16 4-D layout,
@@ -884,7 +892,7 @@ PYBIND11_MODULE(_native, m) {
         "transpose every conv weight of a flat bf16 shadow in one launch");
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient (fp32 accumulate)",
         py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
-        py::arg("cfg") = -1);
+        py::arg("cfg") = -1, py::arg("dbias") = py::none());
   m.def("conv_configs", &conv_configs, "[(id, BM, BN, BK, threads)] of the compiled conv tiles");
   m.def("conv_wgrad_halo_configs", &conv_wgrad_halo_configs,
         "3x3/stride-1 halo wgrad cfg ids applicable to (B, H, W, CI, CO, R, S, stride, pad)");

@@ -37,6 +37,7 @@ struct WgradArgs {
   int B, GH, GW, CI, OH, OW, CO, R, S, stride, pad;
   long long P;
   int p_chunk;      // rows of P per block (multiple of BP)
+  float* dbias;     // optional fp32 [CO] += sum_p dY[p][co] (linear / conv bias grad)
 };
 
 __device__ __forceinline__ f32x4 mfma16w(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -197,6 +198,16 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
         (__attribute__((address_space(3))) s16x4_t*)(img + wg_off<BNW>(row + 4, col0 + 4 * pc)));
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
+  // bias gradient from the dY tiles already staged for the weight gradient:
+  // one extra MFMA per fragment with an all-ones B operand (column sums), by
+  // the wn == 0 waves of the blocks of the first k tile only
+  const bool do_bias = a.dbias != nullptr && blockIdx.x == 0 && wn == 0;
+  f32x4 accb[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ones.v[k] = 0x3f80;   // bf16 1.0
   auto compute = [&](int buf) {
     const u16* As = lds + buf * STAGE;
     const u16* Bs = As + A_EL;
@@ -211,6 +222,10 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16w(af[i], bf[j], acc[i][j]);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) accb[i] = mfma16w(af[i], ones, accb[i]);
+      }
     }
   };
 
@@ -231,6 +246,13 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
     fill_rows(it + NS);                 // table slot it % NS: stage `it` already issued
   }
   wait_vm<0>();
+  if (do_bias && (lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        atomicAdd(a.dbias + co0 + wm * (BMW / WM) + i * 16 + 4 * (lane >> 4) + rr, accb[i][rr]);
+  }
   // D layout: lane holds rows co = 4*(lane>>4)+r of column k = lane & 15
   const long long K = (long long)a.R * a.S * a.CI;
 #pragma unroll
@@ -489,9 +511,10 @@ static void launch_wgrad_variant(const WgradArgs& a, dim3 grid, int bp, int ns, 
 
 void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int W, int CI,
                        int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                       hipStream_t s) {
-  WgradArgs a{dy, x, dw, B, H, W, CI, OH, OW, CO, R, S, stride, pad, (long long)B * OH * OW, 0};
-  if (cfg >= kWhBase) {
+                       hipStream_t s, float* dbias) {
+  WgradArgs a{dy, x, dw, B, H, W, CI, OH, OW, CO, R, S, stride, pad, (long long)B * OH * OW, 0,
+              dbias};
+  if (cfg >= kWhBase && dbias == nullptr) {
     WgradHaloGeom g;
     int bm, sp;
     size_t lds;
@@ -503,6 +526,7 @@ void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int
     }
     cfg = -1;   // not applicable: gather kernel, heuristic variant
   }
+  if (cfg >= kWhBase) cfg = -1;   // halo cfg with a bias gradient: gather kernel
   const long long K = (long long)R * S * CI;
   const int sel = cfg < 0 ? 0 : (cfg & 3);
   int bnw = sel == 1 ? 64 : (sel == 2 ? 128 : (sel == 3 ? 192 : 0));

@@ -104,9 +104,10 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int
                        hipStream_t s, const uint16_t* addend = nullptr);
 void launch_conv_weight_transpose(const uint16_t* w, uint16_t* wt, int CO, int RS, int CI,
                                   hipStream_t s);
+// dbias: optional fp32 [CO] += column sums of dY (gather kernel only; halo cfgs fall back)
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int B, int H, int W,
                        int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                       hipStream_t s);
+                       hipStream_t s, float* dbias = nullptr);
 
 // conv_small.hip: few-input-channel (stem) convolutions, VALU
 int conv_small_max_k();

@@ -60,12 +60,14 @@ def _native_wgrad_ok(dy2, x2) -> bool:
             and dy2.is_contiguous() and x2.is_contiguous())
 
 
-def _native_wgrad(dy2, x2, g):
+def _native_wgrad(dy2, x2, g, gb=None):
     """g[N, K] += dy2^T @ x2 as a 1x1 convolution weight gradient on the native
     MFMA wgrad kernel (csrc/conv_wgrad.hip): fp32 atomics straight into the
     arena.  Measured against hipBLASLt's fp32-output addmm on the ViT-B/16
     shapes (scripts/linear_vs_conv1x1.py, profiles/linear_vs_conv1x1_r1.txt):
-    1.1-2x faster; forward / dgrad stay on hipBLASLt (it wins those)."""
+    1.1-2x faster; forward / dgrad stay on hipBLASLt (it wins those).
+    ``gb``: optional fp32 [N] bias gradient, accumulated by the same kernel from
+    the dY tiles it already stages (no separate column-sum pass over dY)."""
     from .conv import _wgrad_cfg
 
     M, N = dy2.shape
@@ -74,7 +76,7 @@ def _native_wgrad(dy2, x2, g):
     x4 = x2.view(M, 1, 1, K).permute(0, 3, 1, 2)
     g4 = g.view(N, K, 1, 1)
     cfg = _wgrad_cfg(dy4, x4, (N, K, 1, 1), 1, 0)
-    native().conv_wgrad(dy4, x4, g4, 1, 0, cfg)
+    native().conv_wgrad(dy4, x4, g4, 1, 0, cfg, gb)
 
 
 class _ArenaLinear(Function):
@@ -94,9 +96,12 @@ class _ArenaLinear(Function):
         dx = (dy2 @ w16).view(x.shape) if ctx.needs_input_grad[0] else None
         gw = gb = None
         g = _arena_grad(w)
+        bias_done = False
         if g is not None:
             if _native_wgrad_ok(dy2, x2):
-                _native_wgrad(dy2, x2, g)
+                gbias = _arena_grad(b) if (b is not None and b.requires_grad) else None
+                _native_wgrad(dy2, x2, g, gbias)
+                bias_done = gbias is not None
             else:
                 torch.ops.aten.addmm.dtype_out(g, dy2.t(), x2, torch.float32, out=g)
             _notify(w)
@@ -106,7 +111,9 @@ class _ArenaLinear(Function):
             g = _arena_grad(b)
             vec = dy2.dtype == torch.bfloat16 and N % 8 == 0    # 16-B column chunks
             if g is not None:
-                if vec:
+                if bias_done:
+                    pass                         # summed by the weight-gradient kernel
+                elif vec:
                     bias_grad_acc(dy2, g)        # one pass straight into the arena
                 else:
                     g.add_(dy2.sum(0, dtype=torch.float32))

@@ -38,3 +38,25 @@ def test_arena_linear_grads(M, K, N, bias):
         assert rel(lin.bias.grad, 2 * b16.grad) < 1e-2
     assert rel(x.grad.float(), 2 * xr.grad) < 2e-2
     assert 0 in ready
+
+
+@pytest.mark.parametrize("M,K,N", [(1000, 768, 256), (394, 192, 128)])
+def test_wgrad_fused_bias_every_config(M, K, N):
+    """The bias gradient summed inside the weight-gradient kernel (ones-operand
+    MFMA on the staged dY tiles), for every tile configuration the tuner may pick."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+    from distributed_ml_pytorch_amd.ops.conv import _wgrad_candidates
+
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    x4 = x.view(M, 1, 1, K).permute(0, 3, 1, 2)
+    dy4 = dy.view(M, 1, 1, N).permute(0, 3, 1, 2)
+    ref_w = dy.float().t() @ x.float()
+    ref_b = dy.float().sum(0)
+    for cfg in _wgrad_candidates(K, N):
+        g = torch.zeros(N, K, device="cuda")
+        b = torch.full((N,), 0.5, device="cuda")
+        native().conv_wgrad(dy4, x4, g.view(N, K, 1, 1), 1, 0, cfg, b)
+        assert float((g - ref_w).norm() / ref_w.norm()) < 1e-2, cfg
+        torch.testing.assert_close(b, ref_b + 0.5, rtol=1e-4, atol=1e-2)
