@@ -5,10 +5,10 @@ Not in the reference (no sequence models there).  ViT-B/16 at
 1000-class head.  LayerNorm and tanh-GELU are native kernels
 (``csrc/transformer.hip``), multi-head attention is one fused MFMA kernel per
 direction on the qkv rows (``csrc/attention.hip``); the projection / MLP GEMMs
-are plain library GEMMs (hipBLASLt through ``F.linear``) whose weight gradients
-accumulate in fp32 straight into the grad arena (``ops.linear``) and whose bias
-gradients are one native column-sum pass (``csrc/linear.hip``).
-Patch embedding is a stride-16 conv.
+run forward / dgrad on hipBLASLt (``F.linear``) and their weight + bias
+gradients on the native MFMA wgrad kernel, accumulating fp32 straight into the
+grad arena (``ops.linear``).  Patch embedding is a stride-16 conv computed as
+one GEMM over gathered patch rows (``ops.linear.patch_embed``).
 """
 from __future__ import annotations
 
@@ -21,6 +21,7 @@ import torch.nn.functional as F
 from ..ops import layers as L
 from ..ops import functional as DF
 from ..ops.functional import compute_weight
+from ..ops.linear import patch_embed, patch_embed_ok
 
 
 class LayerNorm(nn.LayerNorm):
@@ -40,6 +41,17 @@ class LayerNorm(nn.LayerNorm):
     def add_forward(self, x, r):
         """(h, LayerNorm(h)) with h = x + r, fused (pre-norm residual add)."""
         return DF.add_layer_norm(x, r, self.weight, self.bias, self.eps, self._slots(x))
+
+
+class PatchEmbed(L.Conv2d):
+    """Stride = kernel conv returning tokens ``[B, N, D]``; a GEMM on patch rows
+    when the weight is arena-backed (parameter layout unchanged: a Conv2d)."""
+
+    def forward(self, x):
+        p = self.kernel_size[0]
+        if self.training and patch_embed_ok(x, self.weight, self.bias, p):
+            return patch_embed(x, self.weight, self.bias, p)
+        return super().forward(x).flatten(2).transpose(1, 2)
 
 
 class Attention(nn.Module):
@@ -90,7 +102,7 @@ class VisionTransformer(nn.Module):
         assert image_size % patch == 0
         self.patch = patch
         self.num_patches = (image_size // patch) ** 2
-        self.patch_embed = L.Conv2d(in_chans, dim, kernel_size=patch, stride=patch)
+        self.patch_embed = PatchEmbed(in_chans, dim, kernel_size=patch, stride=patch)
         self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
         self.pos_embed = nn.Parameter(torch.zeros(1, self.num_patches + 1, dim))
         self.blocks = nn.ModuleList(Block(dim, heads, mlp_ratio) for _ in range(depth))
@@ -107,8 +119,7 @@ class VisionTransformer(nn.Module):
         nn.init.uniform_(w, -1 / math.sqrt(w[0].numel()), 1 / math.sqrt(w[0].numel()))
 
     def forward(self, x):
-        h = self.patch_embed(x)                       # [B, D, H/p, W/p]
-        h = h.flatten(2).transpose(1, 2)              # [B, N, D]
+        h = self.patch_embed(x)                       # [B, N, D]
         cls = compute_weight(self.cls_token, h.dtype).expand(h.shape[0], -1, -1)
         h = torch.cat([cls, h], dim=1) + compute_weight(self.pos_embed, h.dtype)
         pending = None

@@ -6,9 +6,11 @@ cast.  The weight gradient is ONE bf16 x bf16 -> fp32 GEMM that accumulates
 straight into the fp32 arena gradient view -- the native MFMA wgrad kernel
 (a 1x1 convolution's weight gradient) when the dims are multiples of 64,
 else ``addmm`` with an fp32 ``out_dtype`` and ``beta = 1``: no bf16
-weight-gradient tensor, no mixed-dtype add kernel, no AccumulateGrad.  The bias gradient is one native column-sum
-pass (``csrc/linear.hip``) adding straight into the fp32 arena view.  Both fire the parameter's grad-ready hook (bucketed all-reduce in
-sync DP) as soon as they land.
+weight-gradient tensor, no mixed-dtype add kernel, no AccumulateGrad.  On the
+native path the bias gradient is summed by the same kernel from the dY tiles it
+already stages; otherwise it is one native column-sum pass (``csrc/linear.hip``)
+adding straight into the fp32 arena view.  Both fire the parameter's grad-ready
+hook (bucketed all-reduce in sync DP) as soon as they land.
 
 Parity: the reference's ``nn.Linear`` layers (/root/reference/example/models.py
 LeNet/AlexNet/MLP heads) in fp32; here bf16 compute with fp32 master weights.
@@ -49,7 +51,12 @@ def _arena_grad(p):
     if p is None or not p.requires_grad or not getattr(p, "_dmp_arena", False):
         return None
     g = p.grad
-    return g if g is not None and g.is_contiguous() else None
+    if g is None:
+        return None
+    if g.dim() == 4 and g.is_contiguous(memory_format=torch.channels_last):
+        # conv weight used as a GEMM (patch embedding): [Cout, kh*kw*Cin] view
+        return g.permute(0, 2, 3, 1).reshape(g.shape[0], -1)
+    return g if g.is_contiguous() else None
 
 
 def _native_wgrad_ok(dy2, x2) -> bool:
@@ -107,6 +114,8 @@ class _ArenaLinear(Function):
             _notify(w)
         elif w is not None and w.requires_grad:
             gw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).to(w.dtype)
+            if w.dim() == 4:                     # patch embedding: (kh, kw, Cin) columns
+                gw = gw.view(w.shape[0], w.shape[2], w.shape[3], w.shape[1]).permute(0, 3, 1, 2)
         if b is not None and b.requires_grad:
             g = _arena_grad(b)
             vec = dy2.dtype == torch.bfloat16 and N % 8 == 0    # 16-B column chunks
@@ -142,3 +151,33 @@ def linear(x, w, b):
     w16 = w._dmp_w16
     b16 = b._dmp_w16 if b is not None else None
     return _ArenaLinear.apply(x, w16, b16, w, b)
+
+
+def patch_embed_ok(x, w, b, patch: int) -> bool:
+    """Non-overlapping ``patch`` x ``patch`` conv whose weight lives in an arena
+    with a channels-last bf16 shadow: computable as one GEMM on patch rows."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and torch.is_grad_enabled()
+            and x.dim() == 4 and x.shape[2] % patch == 0 and x.shape[3] % patch == 0):
+        return False
+    w16 = getattr(w, "_dmp_w16", None)
+    if w16 is None or w16.dtype != x.dtype or not w16.is_contiguous(
+            memory_format=torch.channels_last):
+        return False
+    return b is None or getattr(b, "_dmp_w16", None) is not None
+
+
+def patch_embed(x, w, b, patch: int):
+    """ViT patch embedding (stride = kernel = ``patch`` conv) as one GEMM:
+    ``[B, C, H, W] -> [B, (H/p)(W/p), Cout]`` tokens.  The patch rows are
+    gathered in the weight's physical (kh, kw, Cin) order, so the channels-last
+    arena shadow is the GEMM's [Cout, K] operand as-is, and the weight gradient
+    lands in the arena through the native wgrad kernel like any linear layer.
+    No input gradient (pixels), so no dgrad GEMM.  Replaces a library conv
+    forward + backward-weights pair."""
+    B, C, H, W = x.shape
+    gh, gw = H // patch, W // patch
+    xp = (x.reshape(B, C, gh, patch, gw, patch).permute(0, 2, 4, 3, 5, 1)
+          .reshape(B, gh * gw, patch * patch * C))
+    w16 = w._dmp_w16.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+    b16 = b._dmp_w16 if b is not None else None
+    return _ArenaLinear.apply(xp, w16, b16, w, b)

@@ -60,3 +60,30 @@ def test_wgrad_fused_bias_every_config(M, K, N):
         native().conv_wgrad(dy4, x4, g.view(N, K, 1, 1), 1, 0, cfg, b)
         assert float((g - ref_w).norm() / ref_w.norm()) < 1e-2, cfg
         torch.testing.assert_close(b, ref_b + 0.5, rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("B,C,H,P,D", [(4, 3, 224, 16, 768), (3, 3, 32, 4, 128)])
+def test_patch_embed_gemm_matches_conv(B, C, H, P, D):
+    """ViT patch embedding as one GEMM on gathered patch rows (channels-last
+    arena weight as the [D, kh*kw*C] operand) vs an fp32 stride-P conv."""
+    from distributed_ml_pytorch_amd.models.vit import PatchEmbed
+    from distributed_ml_pytorch_amd.parallel.arena import FlatArena
+
+    torch.manual_seed(0)
+    pe = PatchEmbed(C, D, kernel_size=P, stride=P).cuda()
+    arena = FlatArena(pe, device="cuda")
+    x = torch.randn(B, C, H, H, device="cuda").to(torch.bfloat16)
+    n = (H // P) ** 2
+    c = torch.randn(B, n, D, device="cuda")
+    y = pe(x)
+    assert y.shape == (B, n, D) and y.dtype == torch.bfloat16
+    (y.float() * c).sum().backward()
+    w = pe.weight._dmp_w16.float().detach().requires_grad_(True)
+    b = pe.bias._dmp_w16.float().detach().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(x.float(), w, b, stride=P).flatten(2).transpose(1, 2)
+    (yr * c).sum().backward()
+    rel = lambda a, r: float((a - r).norm() / (r.norm() + 1e-12))
+    assert rel(y.float(), yr) < 1e-2
+    assert rel(pe.weight.grad, w.grad) < 1e-2
+    assert rel(pe.bias.grad, b.grad) < 1e-2
+    assert pe.weight.grad.data_ptr() == arena.g32.data_ptr() + 4 * arena.slots[0].offset
