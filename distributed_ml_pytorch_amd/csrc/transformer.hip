@@ -141,6 +141,7 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(
     const long long r = ok ? row : 0;
     const float mean = mean_in[r], rstd = rstd_in[r];
     float xh[MAXC][8], dv[MAXC][8];
+    bf16x8 ad[MAXC];   // residual-stream gradient, raw: issued with x / dy, not after the reductions
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
@@ -149,6 +150,7 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(
         float gm[8];
         ld8(x + r * D + e0, xh[c]);
         ld8(dy + r * D + e0, dv[c]);
+        if (dadd) ad[c] = *reinterpret_cast<const bf16x8*>(dadd + r * D + e0);
         if (gamma) ld8f(gamma + e0, gm);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -175,10 +177,8 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(
           for (int k = 0; k < 8; ++k)
             o[k] = rstd * (dv[c][k] * (gamma ? gm[k] : 1.f) - m1 - xh[c][k] * m2);
           if (dadd) {
-            float t[8];
-            ld8(dadd + r * D + e0, t);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) o[k] += t[k];
+            for (int k = 0; k < 8; ++k) o[k] += bf2f(ad[c].v[k]);
           }
           st8(dx + r * D + e0, o);
         }
@@ -401,7 +401,10 @@ void launch_layernorm_bwd(const u16* x, const u16* dy, const float* gamma, const
   const int lr = ln_lanes(D), nc = D / 8 / lr;
   const long long rows_per_block = 4LL * (64 / lr);
   long long blocks = (rows + rows_per_block - 1) / rows_per_block;
-  if (blocks > 1024) blocks = 1024;   // <= 32 blocks add into each slot row
+  // the per-block param-grad epilogue (LDS fold + 2*D slot atomics) costs about
+  // as much as a row group, so fewer, longer-lived blocks (ViT-B/16 bs64, 25
+  // LayerNorms: 1024 blocks 601 us, 1576 blocks 741 us)
+  if (blocks > 512) blocks = 512;   // <= 16 blocks add into each slot row
   const bool grads = slots != nullptr && (dgamma != nullptr || dbeta != nullptr);
   const size_t lds = grads ? (size_t)8 * D * sizeof(float) : 0;
   DMP_LN_BY_LR(layernorm_bwd_kernel, lr, nc, dim3((unsigned)blocks), lds, x, dy, gamma, mean, rstd,
