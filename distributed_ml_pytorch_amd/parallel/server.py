@@ -99,6 +99,7 @@ class ParameterServer:
         self.staleness: list[int] = []
         self.last_seen = {w: time.monotonic() for w in self.workers}
         self.worker_timeout = worker_timeout
+        self.dropped: list[int] = []   # workers declared dead by the liveness check
         self.checkpoint_path = checkpoint_path
         self.checkpoint_every = checkpoint_every
         self._tracker = M.SendTracker()
@@ -209,6 +210,7 @@ class ParameterServer:
                         _LOG.warning("PS: worker %d silent for %.1fs, dropping", w,
                                      now - self.last_seen[w])
                         alive.discard(w)
+                        self.dropped.append(w)
         self.finish()
         return self.stats()
 
@@ -237,6 +239,7 @@ class ParameterServer:
             "bytes_out": self.bytes_out,
             "staleness_mean": (sum(st) / len(st)) if st else 0.0,
             "staleness_max": max(st) if st else 0,
+            "dropped": list(self.dropped),
         }
 
     def save_checkpoint(self, path: str | None = None):

@@ -246,3 +246,45 @@ def test_bench_two_ranks_sharded_ps_cpu():
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["value"] > 0
     assert out["config"]["global_batch"] == 32
     assert "sharded" in out["config"]["parallelism"]
+
+
+# ------------------------------------------------------ PS worker liveness
+def _liveness(rank, world):
+    import time
+
+    from distributed_ml_pytorch_amd.parallel import messaging as M
+    from distributed_ml_pytorch_amd.parallel.server import ParameterServer
+
+    n = 64
+    if rank == 0:
+        ps = ParameterServer(numel=n, worker_timeout=1.0)
+        t0 = time.monotonic()
+        st = ps.run()
+        st["secs"] = time.monotonic() - t0
+        st["shard"] = ps.parameters()[:4].tolist()
+        return st
+    tr = M.SendTracker()
+    M.send_message(M.MessageCode.ParameterUpdate, torch.zeros(n), tracker=tr)
+    if rank == 2:
+        # hangs from the PS's point of view: one push, then silence, no Shutdown
+        M.send_message(M.MessageCode.GradientUpdate, torch.ones(n), tracker=tr)
+        tr.drain()
+        return "silent"
+    for i in range(8):
+        time.sleep(0.3)
+        M.send_message(M.MessageCode.GradientUpdate, torch.full((n,), 0.5), step=i, tracker=tr)
+    M.send_message(M.MessageCode.Shutdown, tracker=tr)
+    tr.drain()
+    return "ok"
+
+
+def test_ps_drops_silent_worker_and_keeps_serving():
+    """a worker that goes silent (no Shutdown) is dropped after
+    ``worker_timeout`` while the PS keeps applying the live worker's pushes and
+    then exits cleanly -- the reference's PS would block in recv forever."""
+    out = _run(_liveness, 3)
+    ps = out[0]
+    assert ps["dropped"] == [2]
+    assert ps["counts"]["GradientUpdate"] == 9 and ps["version"] == 9
+    assert ps["shard"] == [5.0] * 4          # 0 + 1 (silent worker) + 8 x 0.5
+    assert ps["secs"] < 60
