@@ -180,6 +180,97 @@ class LocalPSClient(PSClient):
         self.bytes_recv += snap.numel() * snap.element_size()
 
 
+class SharedPS:
+    """One fp32 master vector served to several in-process workers.
+
+    Backs the "virtual workers" mode: K model replicas in ONE
+    process on one GPU, each stepping on its own HIP stream, all pushing to and
+    pulling from this master - the reference's 1 PS + N workers topology
+    (``Makefile:13-20``) without a second device.  Every apply and snapshot runs
+    on the PS's own stream, so concurrent pushes from different worker streams
+    are serialised exactly as the central PS serialises its receive loop, and a
+    pull observes every push enqueued before it.
+    """
+
+    def __init__(self):
+        self.master = None
+        self.version = 0
+        self.stream = None
+        self.nat = None
+
+    def adopt_or_set(self, p32: torch.Tensor) -> bool:
+        """First caller seeds the master (the worker's init ParameterUpdate,
+        ``Asynchronous.py:34``); later callers get ``False`` and copy it."""
+        if self.master is not None:
+            return False
+        self.master = p32.detach().to(torch.float32).clone()
+        if self.master.device.type == "cuda":
+            from ..ops._ext import native
+
+            self.nat = native()
+            self.stream = torch.cuda.Stream(self.master.device)
+            self.stream.wait_stream(torch.cuda.current_stream())
+        return True
+
+    def apply(self, delta: torch.Tensor):
+        """``master += delta`` after the caller's stream reaches this point;
+        returns the event marking the apply done (``None`` on CPU)."""
+        self.version += 1
+        if self.stream is None:
+            self.master.add_(delta.to(torch.float32))
+            return None
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            self.nat.ps_apply(self.master, delta, None, 1.0)
+            done = torch.cuda.Event()
+            done.record()
+        return done
+
+    def snapshot(self, wire_dtype: torch.dtype):
+        """Copy of the master as of every apply enqueued so far -> (buf, event)."""
+        if self.stream is None:
+            return self.master.clone() if wire_dtype == torch.float32 else \
+                self.master.to(wire_dtype), None
+        caller = torch.cuda.current_stream()
+        with torch.cuda.stream(self.stream):
+            buf = self.master.clone() if wire_dtype == torch.float32 else \
+                self.master.to(wire_dtype)
+            ev = torch.cuda.Event()
+            ev.record()
+        buf.record_stream(caller)    # landed (read) on the worker's stream
+        return buf, ev
+
+
+class SharedPSClient(PSClient):
+    """Worker side of :class:`SharedPS` (virtual workers on one device)."""
+
+    def __init__(self, shared: SharedPS, **kw):
+        super().__init__(**kw)
+        self.shared = shared
+
+    def init(self):
+        if not self.shared.adopt_or_set(self.arena.p32):
+            if self.shared.stream is not None:
+                torch.cuda.current_stream().wait_stream(self.shared.stream)
+            with torch.no_grad():
+                self.arena.p32.copy_(self.shared.master)
+            self.arena.refresh_shadow()
+
+    def push(self, step: int):
+        buf = self._handoff()
+        done = self.shared.apply(buf)
+        if done is not None:
+            # the send buffer is reused two pushes later: wait for this apply first
+            self._send_work[self._cur_slot] = _EventWork(done)
+        self.pushes += 1
+        self.bytes_sent += buf.numel() * buf.element_size()
+
+    def request_pull(self, step: int):
+        buf, ev = self.shared.snapshot(self.wire_dtype)
+        self.pending.append(_Pending(step, buf, event=ev, version=self.shared.version))
+        self.bytes_recv += buf.numel() * buf.element_size()
+
+
 class GlooPSClient(PSClient):
     """Reference topology over gloo: ``send_message`` to the PS, reply on TAG_REPLY."""
 

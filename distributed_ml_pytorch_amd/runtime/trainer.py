@@ -89,7 +89,9 @@ def _dtype(name: str) -> torch.dtype:
 class Worker:
     """One training process: model + arena + optimizer + step function."""
 
-    def __init__(self, cfg: TrainConfig, info: DistInfo, ps_groups=None):
+    def __init__(self, cfg: TrainConfig, info: DistInfo, ps_groups=None, client=None):
+        """``client``: an explicit PS client for ``mode='asgd'`` (e.g. a
+        :class:`~..parallel.clients.SharedPSClient` of the virtual-worker runner)."""
         self.cfg = cfg
         self.info = info
         torch.manual_seed(cfg.seed + info.rank)
@@ -105,7 +107,7 @@ class Worker:
         self.ddp = None
         params = list(self.model.parameters())
         if cfg.mode == "asgd":
-            client = self._make_client(ps_groups)
+            client = client if client is not None else self._make_client(ps_groups)
             self.opt = Asynchronous(params, lr=cfg.lr, n_push=cfg.n_push, n_pull=cfg.n_pull,
                                     model=self.model, client=client, momentum=cfg.momentum,
                                     weight_decay=cfg.weight_decay)
