@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="resnet18")
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=512,
+                    help="per-GPU batch (sweep: profiles/batch_sweep_r1.txt)")
     ap.add_argument("--mode", default="asgd", choices=["asgd", "sync", "single"])
     ap.add_argument("--ps", default="auto", choices=["auto", "local", "sharded", "central"])
     ap.add_argument("--n-push", type=int, default=10)
