@@ -94,17 +94,19 @@ def test_native_rejects_bad_shapes(nat):
 
 
 # --------------------------------------------------------------- cross entropy
-@pytest.mark.parametrize("B,C,dtype", [(64, 10, torch.bfloat16), (256, 10, torch.float32),
-                                       (1000, 1000, torch.bfloat16), (3, 130, torch.float32)])
-def test_softmax_xent(B, C, dtype):
+@pytest.mark.parametrize("B,C,dtype,ls", [(64, 10, torch.bfloat16, 0.0), (256, 10, torch.float32, 0.0),
+                                          (1000, 1000, torch.bfloat16, 0.0), (3, 130, torch.float32, 0.0),
+                                          (2500, 10, torch.bfloat16, 0.0), (512, 32, torch.float32, 0.1),
+                                          (300, 33, torch.float32, 0.1), (77, 1, torch.float32, 0.0)])
+def test_softmax_xent(B, C, dtype, ls):
     from distributed_ml_pytorch_amd.ops.functional import softmax_cross_entropy
 
     logits = (torch.randn(B, C, device="cuda") * 3).to(dtype).requires_grad_(True)
     y = torch.randint(0, C, (B,), device="cuda")
-    loss, hits = softmax_cross_entropy(logits, y)
+    loss, hits = softmax_cross_entropy(logits, y, ls)
     loss.backward()
     ref_in = logits.detach().float().requires_grad_(True)
-    ref = F.cross_entropy(ref_in, y)
+    ref = F.cross_entropy(ref_in, y, label_smoothing=ls)
     ref.backward()
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
     torch.testing.assert_close(loss.float(), ref, rtol=tol, atol=tol)
