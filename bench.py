@@ -6,12 +6,27 @@ Config: ResNet-18 (CIFAR stem, 11,173,962 params, random init), synthetic
 CIFAR-10-shaped batches resident in HBM, bf16 compute / fp32 master params,
 Downpour SGD with n_push = n_pull = 10 (reference defaults, main.py:146-147).
 
-* N = 1: one worker with an in-process PS on the same GPU (push = PS apply
-  kernel, pull = snapshot + land), i.e. every ASGD operation still runs.
-* N > 1: every rank is a worker; the PS is sharded across all ranks (each
-  owns 1/N of the fp32 master): push = reduce-scatter of the accumulated
-  deltas + apply, pull = all-gather, both on a side stream over RCCL/xGMI,
-  landed with staleness <= 1 step.  Per-GPU batch is fixed (weak scaling).
+Topologies (``--ps``):
+
+* ``local``   (N = 1 default): one worker with an in-process PS on the same GPU
+  (push = PS apply kernel, pull = snapshot + land): every ASGD operation runs.
+* ``sharded`` (N > 1 default): every rank is a worker and owns 1/N of the fp32
+  master; push = reduce-scatter of the accumulated deltas + apply, pull =
+  all-gather, both on a side HIP stream over RCCL/xGMI, landed with
+  staleness <= 1 step.  Simultaneous pushes are SUMMED, as a central Downpour
+  PS adds every worker's delta (``--delta-scale mean`` averages instead).
+* ``central``: the reference topology (/root/reference/Makefile:13-20,
+  example/main.py:135-138): rank 0 is the parameter server (fp32 master on its
+  GPU, payloads over one RCCL communicator per (PS, worker) pair, headers on a
+  gloo control group), ranks 1..N-1 are workers.  Whole-node samples/s counts
+  the workers' samples only (the PS GPU trains nothing).
+
+Per-GPU batch is fixed as N grows (weak scaling).
+
+Launch: ``python bench.py --gpus N`` with N > 1 and no launcher environment
+starts ``torch.distributed.run`` with N ranks as a CHILD process (this parent
+never touches the GPU) and relays rank 0's line; under a launcher
+(RANK/WORLD_SIZE set) ``--gpus`` must equal WORLD_SIZE.
 
 Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
 ``torch.cuda.synchronize()`` on both sides; the max elapsed over ranks is used.
@@ -22,24 +37,17 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-
-def _sync():
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-
 
 METRIC = "samples/sec (whole node) ResNet-18 ASGD at 1/2/4/8 MI355X; time-to-target-loss"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -47,14 +55,20 @@ def parse():
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--batch", type=int, default=512,
                     help="per-GPU batch (sweep: profiles/batch_sweep_r1.txt)")
+    ap.add_argument("--ref-batch", type=int, default=64,
+                    help="also time K steps at the reference's default batch "
+                         "(/root/reference/example/main.py:142); 0 skips")
     ap.add_argument("--mode", default="asgd", choices=["asgd", "sync", "single"])
     ap.add_argument("--ps", default="auto", choices=["auto", "local", "sharded", "central"])
+    ap.add_argument("--delta-scale", default="sum",
+                    help="sharded PS: 'sum' of simultaneous pushes (Downpour PS), 'mean', or x")
     ap.add_argument("--n-push", type=int, default=10)
     ap.add_argument("--n-pull", type=int, default=10)
     ap.add_argument("--staleness", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--momentum", type=float, default=0.0)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--bucket-mb", type=float, default=32.0, help="sync mode all-reduce bucket")
     ap.add_argument("--graph", type=int, default=1, help="capture fwd+bwd+update in a hipGraph")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra steps after timing, for rocprofv3 windows")
@@ -62,26 +76,146 @@ def parse():
                     help="after the throughput run: train a FRESH model on learnable synthetic "
                          "data until the mean loss of 10 steps <= target and report the "
                          "wall time (the metric's time-to-target-loss half); 0 skips")
-    ap.add_argument("--ttl-max-steps", type=int, default=1500)
-    return ap.parse_args()
+    ap.add_argument("--ttl-max-steps", type=int, default=3000)
+    ap.add_argument("--ttl-signal", type=float, default=0.5,
+                    help="class-template amplitude of the time-to-target images")
+    ap.add_argument("--ttl-batches", type=int, default=32, help="distinct TTL batches per rank")
+    ap.add_argument("--ttl-compare-sync", type=int, default=0,
+                    help="also measure time-to-target of sync all-reduce DP at the same N")
+    return ap.parse_args(argv)
 
 
-def time_to_target(a, cfg, info):
+# ----------------------------------------------------------------------- spawn
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(a, argv) -> int:
+    """Start N ranks under torch.distributed.run as a child process.  Nothing in
+    this parent initialises the GPU (no torch.cuda call), so the children own it."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    return subprocess.run(cmd, env=env).returncode
+
+
+# -------------------------------------------------------------------- helpers
+class _Ctx:
+    """Groups and roles of one benchmark process."""
+
+    def __init__(self, a, info):
+        import torch.distributed as dist
+
+        self.info = info
+        self.world = info.world_size
+        self.cpu_group = None
+        self.worker_group = None
+        self.ps_groups = None
+        self.central = a.mode == "asgd" and a.ps == "central"
+        if info.is_distributed:
+            # host-side result exchange + stop decisions never ride on RCCL
+            self.cpu_group = dist.new_group(backend="gloo") if info.backend != "gloo" else None
+            if self.central:
+                from distributed_ml_pytorch_amd.parallel.server import make_ps_groups
+
+                payload = "rccl" if info.backend == "nccl" else "gloo"
+                self.ps_groups = make_ps_groups(0, payload)
+                self.worker_group = dist.new_group(list(range(1, self.world)))
+        self.is_ps = self.central and info.rank == 0
+        self.n_workers = self.world - 1 if self.central else self.world
+
+    def worker_barrier(self):
+        import torch.distributed as dist
+
+        if not self.info.is_distributed:
+            return
+        if self.info.backend == "nccl":
+            dist.barrier(group=self.worker_group, device_ids=[self.info.device.index])
+        else:
+            dist.barrier(group=self.worker_group)
+
+    def host_reduce(self, vals, op="max"):
+        """Element-wise MAX (or SUM) of a float list over every rank, on the CPU."""
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor(vals, dtype=torch.float64)
+        if self.info.is_distributed:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM,
+                            group=self.cpu_group)
+        return t.tolist()
+
+    def worker_mean(self, t):
+        """Mean of a device scalar over the workers (a TTL stop decision)."""
+        import torch.distributed as dist
+
+        if self.info.is_distributed and self.n_workers > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.worker_group)
+            t /= self.n_workers
+        return t
+
+
+def _sync():
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def _serve(a, cfg, ctx, sessions: int):
+    """Rank 0 of the central topology: one PS run per worker session."""
+    from distributed_ml_pytorch_amd.runtime.trainer import run_server
+
+    stats = None
+    for _ in range(sessions):
+        st = run_server(cfg, ctx.info, ctx.ps_groups)
+        stats = stats or st      # the throughput session's counts
+    return stats
+
+
+def _timed_steps(w, pool, steps, warmup, ctx):
+    for _ in range(warmup):
+        x, y = pool.next()
+        loss, _ = w.train_step(x, y)
+    ctx.worker_barrier()
+    _sync()
+    w.timer.reset()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        x, y = pool.next()
+        loss, _ = w.train_step(x, y)
+    _sync()
+    ctx.worker_barrier()
+    return time.perf_counter() - t0, loss
+
+
+def time_to_target(a, cfg, ctx, mode=None):
     """Wall time for a freshly initialised model (same engine, same config) to
     bring the mean training loss over 10 steps down to ``--ttl-target`` on
     class-template synthetic images (learnable, unlike the noise batches of the
     throughput run).  Includes graph capture and the first (tuning) step."""
-    from distributed_ml_pytorch_amd.runtime.dist import barrier
+    from dataclasses import replace
+
+    import torch
+
     from distributed_ml_pytorch_amd.runtime.trainer import Worker
     from distributed_ml_pytorch_amd.utils.data import DeviceBatchPool
 
+    info = ctx.info
+    cfg = replace(cfg, mode=mode or cfg.mode, seed=1000)
     torch.manual_seed(1000 + info.rank)
-    w = Worker(cfg, info)
-    if a.mode != "sync":
+    w = Worker(cfg, info, ctx.ps_groups)
+    if cfg.mode != "sync":
         w.enable_graph(bool(a.graph))
-    pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device, n_batches=32,
-                           dtype=w.compute_dtype, seed=100 + info.rank, learnable=True)
-    barrier(info)
+    pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device,
+                           n_batches=a.ttl_batches, dtype=w.compute_dtype,
+                           seed=100 + info.rank, learnable=True, signal=a.ttl_signal)
+    ctx.worker_barrier()
     _sync()
     t0 = time.perf_counter()
     steps, reached, window = 0, False, []
@@ -91,73 +225,101 @@ def time_to_target(a, cfg, info):
         window.append(loss.detach().float())
         steps += 1
         if steps % 10 == 0:
-            m = torch.stack(window).mean().reshape(1)
+            # every worker takes the same stop decision, or the ones that keep
+            # training would block in a push the others never join
+            m = ctx.worker_mean(torch.stack(window).mean().reshape(1))
             window.clear()
-            if info.is_distributed:
-                # every rank must take the same stop decision, or the ranks that keep
-                # training would block in a push collective the others never join
-                dist.all_reduce(m, op=dist.ReduceOp.SUM)
-                m /= info.world_size
-            mean = float(m.item())
-            if mean <= a.ttl_target:
+            if float(m.item()) <= a.ttl_target:
                 reached = True
                 break
     _sync()
     t = time.perf_counter() - t0
     w.finish()
-    return {"time_to_target_s": round(t, 3), "ttl_target_loss": a.ttl_target,
-            "ttl_steps": steps, "ttl_reached": reached,
-            "ttl_data": "synthetic class-template images (signal 0.5 + N(0,1) noise), "
-                        "32 distinct batches per rank"}
+    return {"time_to_target_s": round(t, 3), "ttl_steps": steps, "ttl_reached": reached}
 
 
-def main():
-    a = parse()
-    from distributed_ml_pytorch_amd.runtime.dist import init_distributed, barrier, shutdown
+def run(a):
+    import torch
+
+    from distributed_ml_pytorch_amd.runtime.dist import init_distributed, shutdown
     from distributed_ml_pytorch_amd.runtime.trainer import TrainConfig, Worker
     from distributed_ml_pytorch_amd.utils.data import DeviceBatchPool
 
-    info = init_distributed(use_cuda=torch.cuda.is_available())
+    cuda = torch.cuda.is_available()
+    info = init_distributed(use_cuda=cuda)
     world = info.world_size
-    ps = a.ps
-    if ps == "auto":
-        ps = "sharded" if world > 1 else "local"
+    if a.mode == "asgd" and a.ps == "auto":
+        a.ps = "sharded" if world > 1 else "local"
+    if a.mode == "asgd" and a.ps == "local" and world > 1:
+        raise SystemExit("--ps local is the 1-GPU in-process PS; with N > 1 use sharded/central")
+    if a.mode == "asgd" and a.ps == "central" and world < 2:
+        raise SystemExit("--ps central needs >= 2 ranks (rank 0 = PS, ranks 1.. = workers)")
+    ctx = _Ctx(a, info)
     cfg = TrainConfig(model=a.model, batch_size=a.batch, lr=a.lr, momentum=a.momentum,
                       n_push=a.n_push, n_pull=a.n_pull, staleness=a.staleness, mode=a.mode,
-                      ps=ps, dtype=a.dtype, cuda=True, evaluate=False, verbose=False)
-    w = Worker(cfg, info)
-    graphed = w.enable_graph(bool(a.graph)) if a.mode != "sync" else False
-    pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device, n_batches=4,
-                           dtype=w.compute_dtype, seed=info.rank)
-    for _ in range(a.warmup):
-        x, y = pool.next()
-        loss, _ = w.train_step(x, y)
-    barrier(info)
-    _sync()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        x, y = pool.next()
-        loss, _ = w.train_step(x, y)
-    _sync()
-    barrier(info)
-    elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], device=w.device, dtype=torch.float64)
-    if info.is_distributed:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-    final_loss = float(loss.float().item())
-    for _ in range(a.profile_steps):
-        x, y = pool.next()
-        w.train_step(x, y)
-    _sync()
-    in_shape = tuple(w.input_shape)
-    w.finish()
-    ttl = time_to_target(a, cfg, info) if a.ttl_target > 0 else None
+                      ps=a.ps if a.mode == "asgd" else "local", dtype=a.dtype, cuda=True,
+                      evaluate=False, verbose=False, bucket_mb=a.bucket_mb,
+                      delta_scale=a.delta_scale, payload="auto")
+    res = {}
+    ps_stats = None
+    if ctx.is_ps:
+        ps_stats = _serve(a, cfg, ctx, 2 if a.ttl_target > 0 else 1)
+        elapsed = ref_elapsed = 0.0
+        final_loss = 0.0
+        graphed = False
+        in_shape = None
+        dev_name = str(info.device)
+    else:
+        w = Worker(cfg, info, ctx.ps_groups)
+        graphed = w.enable_graph(bool(a.graph)) if a.mode != "sync" else False
+        pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device, n_batches=4,
+                               dtype=w.compute_dtype, seed=info.rank)
+        elapsed, loss = _timed_steps(w, pool, a.steps, a.warmup, ctx)
+        final_loss = float(loss.float().item())
+        res["phases_host_ms"] = {k: v["mean_ms"] for k, v in w.timer.summary().items()}
+        for _ in range(a.profile_steps):
+            x, y = pool.next()
+            w.train_step(x, y)
+        ref_elapsed = 0.0
+        if a.ref_batch:
+            pool64 = DeviceBatchPool(a.ref_batch, w.input_shape, w.num_classes, w.device,
+                                     n_batches=4, dtype=w.compute_dtype, seed=info.rank + 7)
+            ref_elapsed, _ = _timed_steps(w, pool64, a.steps, max(a.warmup, 3), ctx)
+        _sync()
+        in_shape = tuple(w.input_shape)
+        dev_name = str(w.device)
+        if hasattr(w.opt, "client"):
+            res["comm"] = {k: v for k, v in w.opt.client.stats().items() if "device_ms" in k}
+        w.finish()
+        del w
+    ttl = ttl_sync = None
+    if a.ttl_target > 0:
+        ttl = time_to_target(a, cfg, ctx) if not ctx.is_ps else None
+        if a.ttl_compare_sync and not ctx.central and a.mode == "asgd":
+            ttl_sync = time_to_target(a, cfg, ctx, mode="sync")
+    # -------- reduce over ranks (host side; the PS contributes zeros) --------
+    ttl_vals = [ttl["time_to_target_s"], ttl["ttl_steps"], float(ttl["ttl_reached"])] \
+        if ttl else [0.0, 0.0, 0.0]
+    red = ctx.host_reduce([elapsed, -elapsed if elapsed else -1e30, ref_elapsed, final_loss,
+                           *ttl_vals])
+    elapsed, min_elapsed, ref_elapsed, final_loss = red[0], -red[1], red[2], red[3]
+    if ttl is not None or ctx.is_ps:
+        ttl = {"time_to_target_s": round(red[4], 3), "ttl_steps": int(red[5]),
+               "ttl_reached": bool(red[6])} if a.ttl_target > 0 else None
+    if ctx.is_ps:
+        shape_src = ctx.host_reduce([0.0, 0.0, 0.0])      # matched by workers below
+    else:
+        shape_src = ctx.host_reduce(list(map(float, in_shape)))
+    in_shape = tuple(int(v) for v in shape_src)
     if info.rank == 0:
-        global_batch = a.batch * world
+        nw = ctx.n_workers
+        global_batch = a.batch * nw
         value = global_batch * a.steps / elapsed
-        par = {"asgd": f"asgd-{ps}-ps x{world}", "sync": f"dp{world}",
+        par = {"asgd": f"asgd-{a.ps}-ps x{world}", "sync": f"dp{world}",
                "single": "single"}[a.mode]
+        if ctx.central:
+            par = f"asgd-central-ps 1ps+{nw}w"
+        on_gpu = cuda
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -169,22 +331,60 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": a.dtype,
-            "data": f"synthetic ({'x'.join(map(str, in_shape))} images, random labels, "
-                    "HBM-resident); random-init weights",
+            "dtype": a.dtype if on_gpu else "fp32 (CPU run: no bf16 compute)",
+            "data": ("synthetic ({} images, random labels, {}); random-init weights".format(
+                "x".join(map(str, in_shape)), "HBM-resident" if on_gpu else "host memory")),
             "config": {"model": (f"{a.model} ({'CIFAR' if in_shape[-1] <= 64 else 'ImageNet'} stem)"
                                  if a.model.startswith("resnet") else a.model),
                        "global_batch": global_batch, "per_gpu_batch": a.batch,
                        "seq_len": None, "image": "x".join(map(str, in_shape)),
                        "parallelism": par, "n_push": a.n_push, "n_pull": a.n_pull,
-                       "staleness": a.staleness, "lr": a.lr, "hip_graph": bool(graphed),
-                       "master_dtype": "fp32"},
+                       "staleness": a.staleness, "lr": a.lr,
+                       "push_combine": a.delta_scale if a.ps == "sharded" else "sum",
+                       "hip_graph": bool(graphed), "master_dtype": "fp32"},
+            "world_size": world,
+            "backend": info.backend,
+            "rccl_ranks": world if info.backend == "nccl" else 0,
+            "workers": nw,
+            "device": dev_name if on_gpu else "cpu",
+            "ms_per_step_fastest_rank": round(1e3 * min_elapsed / a.steps, 4),
             "final_loss": round(final_loss, 4),
         }
+        if res.get("phases_host_ms"):
+            out["phases_host_ms"] = res["phases_host_ms"]
+        if res.get("comm"):
+            out["comm_rank0"] = res["comm"]
+        if a.ref_batch and ref_elapsed > 0:
+            out["reference_batch"] = {
+                "per_gpu_batch": a.ref_batch, "global_batch": a.ref_batch * nw,
+                "ms_per_step": round(1e3 * ref_elapsed / a.steps, 4),
+                "value": round(a.ref_batch * nw * a.steps / ref_elapsed, 2)}
+        if ps_stats:
+            out["ps"] = {k: ps_stats[k] for k in ("version", "counts", "staleness_mean",
+                                                  "staleness_max", "bytes_in", "bytes_out")
+                         if k in ps_stats}
         if ttl is not None:
             out.update(ttl)
+            out.update({"ttl_target_loss": a.ttl_target,
+                        "ttl_data": f"synthetic class-template images (signal {a.ttl_signal} "
+                                    f"+ N(0,1) noise), {a.ttl_batches} distinct batches per "
+                                    "worker"})
+        if ttl_sync is not None:
+            out["ttl_sync_dp"] = ttl_sync
         print(json.dumps(out), flush=True)
     shutdown()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = parse(argv)
+    launched = "RANK" in os.environ and "WORLD_SIZE" in os.environ
+    if not launched and a.gpus > 1:
+        sys.exit(_spawn(a, argv))
+    if launched and int(os.environ["WORLD_SIZE"]) != a.gpus:
+        raise SystemExit(f"bench.py --gpus {a.gpus} but the launcher started "
+                         f"WORLD_SIZE={os.environ['WORLD_SIZE']} ranks")
+    run(a)
 
 
 if __name__ == "__main__":

@@ -61,7 +61,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--label-smoothing", type=float, default=0.0)
     p.add_argument("--checkpoint", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
-    p.add_argument("--resume", default=None)
+    p.add_argument("--resume", default=None,
+                   help="checkpoint base: workers load <base>.worker<rank>.pt, the PS <base>")
+    p.add_argument("--ps-resume", default=None, help="explicit parameter-server checkpoint")
+    p.add_argument("--delta-scale", default="sum",
+                   help="sharded PS: combine simultaneous pushes by 'sum' (Downpour), 'mean' or x")
+    p.add_argument("--ps-worker-timeout", type=float, default=0.0,
+                   help="central PS drops a worker silent for this many seconds (0 = never)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--log-dir", default="log")
     p.add_argument("--no-eval", action="store_true", default=False)
@@ -81,7 +87,9 @@ def config_from_args(a) -> TrainConfig:
         wire_dtype=a.wire_dtype, mode=mode, ps=a.ps, payload=a.payload, dtype=a.dtype,
         cuda=a.cuda, log_interval=a.log_interval, evaluate=not a.no_eval, seed=a.seed,
         log_dir=a.log_dir, checkpoint=a.checkpoint, checkpoint_every=a.checkpoint_every,
-        resume=a.resume, bucket_mb=a.bucket_mb, label_smoothing=a.label_smoothing)
+        resume=a.resume, ps_resume=a.ps_resume, delta_scale=a.delta_scale,
+        ps_worker_timeout=a.ps_worker_timeout, bucket_mb=a.bucket_mb,
+        label_smoothing=a.label_smoothing)
 
 
 def main(argv=None):

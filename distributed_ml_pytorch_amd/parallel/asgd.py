@@ -69,6 +69,7 @@ class Asynchronous(Optimizer):
         self.acc = torch.zeros(arena.numel, dtype=torch.float32, device=dev)
         self.mom = torch.zeros_like(self.acc) if momentum else None
         self.idx = 0
+        self.timer = _NO_TIMER      # a utils.metrics.StepTimer when the trainer wires one
         self.client = client if client is not None else default_client(
             staleness=staleness, pull_mode=pull_mode, wire_dtype=wire_dtype)
         self.client.attach(self)
@@ -128,11 +129,15 @@ class Asynchronous(Optimizer):
     @torch.no_grad()
     def comm_step(self):
         """Host-scheduled half: push / pull / land on the reference cadence."""
+        t = self.timer
         if self.idx % self.n_push == 0:
-            self.client.push(self.idx)
+            with t.time("push"):
+                self.client.push(self.idx)
         if self.idx % self.n_pull == 0:
-            self.client.request_pull(self.idx)
-        self.client.land_due(self.idx)
+            with t.time("pull_issue"):
+                self.client.request_pull(self.idx)
+        with t.time("land"):
+            self.client.land_due(self.idx)
         self.idx += 1
 
     def finish(self):
@@ -141,6 +146,23 @@ class Asynchronous(Optimizer):
 
     def stats(self) -> dict:
         return {"steps": self.idx, **self.client.stats()}
+
+
+class _NoTimer:
+    class _Ctx:
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+    _ctx = _Ctx()
+
+    def time(self, name):
+        return self._ctx
+
+
+_NO_TIMER = _NoTimer()
 
 
 # The reference's package exports this name (asgd/optim/__init__.py:1) while its

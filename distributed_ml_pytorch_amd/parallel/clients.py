@@ -34,10 +34,12 @@ _LOG = logging.getLogger(__name__)
 
 
 class _Pending:
-    __slots__ = ("step", "buf", "work", "event", "version")
+    __slots__ = ("step", "buf", "work", "event", "version", "vsrc")
 
-    def __init__(self, step, buf, work=None, event=None, version=0):
+    def __init__(self, step, buf, work=None, event=None, version=0, vsrc=None):
         self.step, self.buf, self.work, self.event, self.version = step, buf, work, event, version
+        # central PS replies carry the PS version as one trailing fp32 element
+        self.vsrc = vsrc
 
 
 class PSClient:
@@ -136,8 +138,30 @@ class PSClient:
                 if arena.w16 is not None:
                     arena.w16.copy_(arena.p32)
         self.version = max(self.version, pend.version)
+        if pend.vsrc is not None:
+            self._note_version(pend.vsrc)
         self.pulls += 1
         arena.bump()
+
+    def _note_version(self, vsrc: torch.Tensor):
+        """Record the PS version a landed reply was taken at, without a host sync
+        on GPU (pinned async copy, read once its event has completed)."""
+        if vsrc.device.type == "cpu":
+            self.version = max(self.version, int(vsrc.item()))
+            return
+        if not hasattr(self, "_vq"):
+            self._vq = deque()
+        host = torch.empty(1, dtype=torch.float32, pin_memory=True)
+        host.copy_(vsrc.reshape(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._vq.append((host, ev))
+
+    def _resolve_versions(self):
+        vq = getattr(self, "_vq", None)
+        while vq and vq[0][1].query():
+            host, _ = vq.popleft()
+            self.version = max(self.version, int(host.item()))
 
     def land_due(self, step: int, force: bool = False):
         while self.pending and (force or self.pending[0].step <= step - self.staleness):
@@ -151,8 +175,34 @@ class PSClient:
         M.SENDS.drain()
 
     def stats(self) -> dict:
-        return {"pushes": self.pushes, "pulls": self.pulls, "bytes_sent": self.bytes_sent,
-                "bytes_recv": self.bytes_recv, "version": self.version}
+        st = {"pushes": self.pushes, "pulls": self.pulls, "bytes_sent": self.bytes_sent,
+              "bytes_recv": self.bytes_recv, "version": self.version}
+        st.update(self.comm_times())
+        return st
+
+    # -- device-side timing of the communication (side stream) --------------
+    def _timed(self, kind: str):
+        """Context recording start/end events on the CURRENT stream around a
+        communication phase; resolved lazily by :meth:`comm_times` (no sync)."""
+        return _EventSpan(self, kind) if self.cuda else _NULL_SPAN
+
+    def comm_times(self) -> dict:
+        spans = getattr(self, "_spans", None)
+        if not spans:
+            return {}
+        out = {}
+        for kind, evs in spans.items():
+            ms = [a.elapsed_time(b) for a, b in evs if b.query()]
+            if ms:
+                out[f"{kind}_device_ms"] = round(sum(ms) / len(ms), 4)
+        return out
+
+    # -- checkpoint state of the PS side held by this client ----------------
+    def state_dict(self) -> dict:
+        return {}
+
+    def load_state_dict(self, sd: dict):
+        pass
 
 
 class LocalPSClient(PSClient):
@@ -178,6 +228,17 @@ class LocalPSClient(PSClient):
             self.master.to(self.wire_dtype)
         self.pending.append(_Pending(step, snap, version=self.ps_version))
         self.bytes_recv += snap.numel() * snap.element_size()
+
+    def state_dict(self) -> dict:
+        return {"kind": "local", "master": self.master.detach().cpu(),
+                "ps_version": int(self.ps_version)}
+
+    def load_state_dict(self, sd: dict):
+        if sd.get("kind") != "local":
+            return
+        with torch.no_grad():
+            self.master.copy_(sd["master"].to(self.master.device))
+        self.ps_version = int(sd["ps_version"])
 
 
 class SharedPS:
@@ -284,29 +345,41 @@ class GlooPSClient(PSClient):
 
     def init(self):
         self.used = self.arena.numel
-        M.send_message(M.MessageCode.ParameterUpdate, self._cpu(self.arena.p32), self.ps_rank,
-                       step=0, group=self.group)
+        # a snapshot: gloo reads a CPU send buffer only when the PS posts its receive,
+        # by which time the local steps may have moved the live parameters
+        snap = self.arena.p32.detach().clone() if not self.cuda else self._cpu(self.arena.p32)
+        M.send_message(M.MessageCode.ParameterUpdate, snap, self.ps_rank, step=0,
+                       group=self.group)
 
     def push(self, step: int):
         buf = self._handoff()
-        M.send_message(M.MessageCode.GradientUpdate, self._cpu(buf), self.ps_rank, step=step,
-                       version=self.version, group=self.group)
+        self._resolve_versions()
+        works = M.send_message(M.MessageCode.GradientUpdate, self._cpu(buf), self.ps_rank,
+                               step=step, version=self.version, group=self.group)
+        if not self.cuda:
+            # gloo reads an unbound CPU send buffer only when the PS posts its recv:
+            # the slot must not be refilled (two pushes later) before that happens
+            self._send_work[self._cur_slot] = works[-1]
         self.pushes += 1
         self.bytes_sent += buf.numel() * buf.element_size()
 
     def request_pull(self, step: int):
         M.send_message(M.MessageCode.ParameterRequest, None, self.ps_rank, step=step,
                        group=self.group)
-        buf = torch.empty(self.arena.numel, dtype=torch.float32)
+        n = self.arena.numel
+        buf = torch.empty(n + 1, dtype=torch.float32)
         work = dist.irecv(buf, self.ps_rank, group=self.group, tag=M.TAG_REPLY)
-        self.pending.append(_Pending(step, buf, work=work))
+        self.pending.append(_Pending(step, buf, work=M.OnceWork(work), vsrc=buf[n]))
         self.bytes_recv += buf.numel() * 4
 
     def _land(self, pend):
         if self.cuda:
             pend.work.wait()
             pend.work = None
-            pend.buf = pend.buf.to(self.device, non_blocking=False)
+            n = self.arena.numel
+            self.version = max(self.version, int(pend.buf[n].item()))
+            pend.vsrc = None
+            pend.buf = pend.buf[:n].to(self.device, non_blocking=False)
         super()._land(pend)
 
     def finish(self):
@@ -339,6 +412,7 @@ class RcclPSClient(PSClient):
 
     def push(self, step: int):
         buf = self._handoff()
+        self._resolve_versions()
         header = M.make_header(M.MessageCode.GradientUpdate, dist.get_rank(), step, self.version,
                                buf.numel(), buf.dtype)
         M.SENDS.add(dist.isend(header, self.ps_rank, group=self.ctrl, tag=M.TAG_HEADER), header)
@@ -349,10 +423,11 @@ class RcclPSClient(PSClient):
     def request_pull(self, step: int):
         header = M.make_header(M.MessageCode.ParameterRequest, dist.get_rank(), step, 0, 0)
         M.SENDS.add(dist.isend(header, self.ps_rank, group=self.ctrl, tag=M.TAG_HEADER), header)
+        n = self.arena.numel
         buf = self._pull_bufs.popleft() if len(self._pull_bufs) > self.staleness else \
-            torch.empty(self.arena.numel, dtype=torch.float32, device=self.device)
-        work = dist.irecv(buf[: self.arena.numel], self.ps_rank, group=self.pair)
-        self.pending.append(_Pending(step, buf, work=work))
+            torch.empty(n + 1, dtype=torch.float32, device=self.device)
+        work = dist.irecv(buf, self.ps_rank, group=self.pair)
+        self.pending.append(_Pending(step, buf, work=work, vsrc=buf[n]))
         self.bytes_recv += buf.numel() * 4
 
     def _land(self, pend):
@@ -377,11 +452,18 @@ class ShardedPSClient(PSClient):
     the pull is due (``staleness`` steps later).
     """
 
-    def __init__(self, group=None, force_collectives: bool = False, **kw):
+    def __init__(self, group=None, force_collectives: bool = False, delta_scale: str | float = "sum",
+                 **kw):
+        """``delta_scale``: how the W simultaneous pushes combine in the master.
+        ``"sum"`` (default) is what a central Downpour PS does - it adds every
+        worker's delta (/root/reference/asgd/optim/Asynchronous.py:58-59, SURVEY
+        C7) - so the effective step grows with W; ``"mean"`` scales the summed
+        delta by 1/W (model averaging); a float is used as is."""
         super().__init__(**kw)
         self.group = group
         # run the RCCL path even at world size 1 (single-GPU validation)
         self.force = force_collectives
+        self.delta_scale = delta_scale
 
     def init(self):
         self.world = dist.get_world_size(self.group) if dist.is_initialized() else 1
@@ -390,6 +472,12 @@ class ShardedPSClient(PSClient):
         if n % self.world:
             raise ValueError(f"arena length {n} not divisible by world size {self.world}")
         self.shard_n = n // self.world
+        if self.delta_scale == "sum":
+            self.scale = 1.0
+        elif self.delta_scale == "mean":
+            self.scale = 1.0 / self.world
+        else:
+            self.scale = float(self.delta_scale)
         if self.world > 1 or self.force:
             # identical starting point everywhere (the reference let every worker
             # start from its own random init and converge through pulls)
@@ -404,9 +492,9 @@ class ShardedPSClient(PSClient):
 
     def _apply_delta(self):
         if self.cuda:
-            self.nat.ps_apply(self.master, self.delta_shard, None, 1.0)
+            self.nat.ps_apply(self.master, self.delta_shard, None, self.scale)
         else:
-            self.master.add_(self.delta_shard.to(torch.float32))
+            self.master.add_(self.delta_shard.to(torch.float32), alpha=self.scale)
 
     def push(self, step: int):
         buf = self._handoff()
@@ -423,10 +511,11 @@ class ShardedPSClient(PSClient):
             ev.record()
             with torch.cuda.stream(self.side):
                 self.side.wait_event(ev)
-                work = dist.reduce_scatter_tensor(self.delta_shard, buf, group=self.group,
-                                                  async_op=True)
-                work.wait()
-                self._apply_delta()
+                with self._timed("push"):
+                    work = dist.reduce_scatter_tensor(self.delta_shard, buf, group=self.group,
+                                                      async_op=True)
+                    work.wait()
+                    self._apply_delta()
                 done = torch.cuda.Event()
                 done.record()
             self._send_work[self._cur_slot] = _EventWork(done)
@@ -455,9 +544,10 @@ class ShardedPSClient(PSClient):
             with torch.cuda.stream(self.side):
                 if free_ev is not None:
                     self.side.wait_event(free_ev)   # previous land kernel done reading buf
-                work = dist.all_gather_into_tensor(buf, self.master, group=self.group,
-                                                   async_op=True)
-                work.wait()
+                with self._timed("pull"):
+                    work = dist.all_gather_into_tensor(buf, self.master, group=self.group,
+                                                       async_op=True)
+                    work.wait()
                 ev = torch.cuda.Event()
                 ev.record()
             self.pending.append(_Pending(step, buf, event=ev))
@@ -484,6 +574,67 @@ class ShardedPSClient(PSClient):
         super().finish()
         if self.cuda:
             self.side.synchronize()
+
+    def state_dict(self) -> dict:
+        if self.cuda:
+            self.side.synchronize()
+        return {"kind": "sharded", "rank": self.rank, "world": self.world,
+                "master": self.master.detach().cpu()}
+
+    def load_state_dict(self, sd: dict):
+        """Restore this rank's master shard, then re-sync the live parameters
+        from the restored shards (a forced pull)."""
+        if sd.get("kind") != "sharded":
+            return
+        if sd["world"] != self.world or sd["rank"] != self.rank:
+            raise ValueError(f"sharded PS checkpoint is for rank {sd['rank']}/{sd['world']}, "
+                             f"this is rank {self.rank}/{self.world}")
+        with torch.no_grad():
+            self.master.copy_(sd["master"].to(self.master.device))
+            if self.world > 1 or self.force:
+                if dist.get_backend(self.group) == "gloo":
+                    self._gloo_all_gather(self.arena.p32).wait()
+                else:
+                    dist.all_gather_into_tensor(self.arena.p32, self.master, group=self.group)
+            else:
+                self.arena.p32.copy_(self.master)
+        self.arena.refresh_shadow()
+        self.arena.bump()
+
+
+class _EventSpan:
+    """Start/end CUDA events on the current stream; kept (bounded) on the client."""
+
+    KEEP = 64
+
+    def __init__(self, client, kind):
+        self.client, self.kind = client, kind
+
+    def __enter__(self):
+        self.a = torch.cuda.Event(enable_timing=True)
+        self.a.record()
+        return self
+
+    def __exit__(self, *exc):
+        b = torch.cuda.Event(enable_timing=True)
+        b.record()
+        spans = self.client.__dict__.setdefault("_spans", {})
+        lst = spans.setdefault(self.kind, [])
+        lst.append((self.a, b))
+        if len(lst) > self.KEEP:
+            del lst[0]
+        return False
+
+
+class _NullSpan:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL_SPAN = _NullSpan()
 
 
 class _EventWork:

@@ -48,17 +48,56 @@ class MessageCode(enum.IntEnum):
     Checkpoint = 5
 
 
-class SendTracker:
-    """Keeps in-flight ``Work`` handles (and their buffers) alive until done."""
+class OnceWork:
+    """A ``Work`` whose ``wait()`` may be called any number of times.
 
-    def __init__(self):
+    gloo's p2p ``Work`` reports ``is_completed() == False`` until ``wait()`` has
+    been called, and a SECOND ``wait()`` on a completed send blocks forever
+    (both measured on torch 2.10).  Every tracked send is wrapped, so the tracker
+    and a client's buffer-reuse guard can both wait on it safely.
+    """
+
+    __slots__ = ("work", "done")
+
+    def __init__(self, work):
+        self.work = work
+        self.done = False
+
+    def wait(self):
+        if not self.done:
+            self.work.wait()
+            self.done = True
+        return True
+
+    def is_completed(self) -> bool:
+        return self.done or self.work.is_completed()
+
+
+class SendTracker:
+    """Keeps in-flight ``Work`` handles (and their buffers) alive until done.
+
+    Completion cannot be polled on gloo (see :class:`OnceWork`), so the tracker
+    is bounded instead: beyond ``max_inflight`` entries the oldest are waited
+    for (long since received by then), which caps the payload memory it pins.
+    """
+
+    def __init__(self, max_inflight: int = 32):
         self._q: deque = deque()
         self._lock = threading.Lock()
+        self.max_inflight = max_inflight
 
     def add(self, work, *keepalive):
+        w = work if isinstance(work, OnceWork) else OnceWork(work)
         with self._lock:
-            self._q.append((work, keepalive))
+            self._q.append((w, keepalive))
             self._reap_locked()
+        while True:
+            with self._lock:
+                if len(self._q) <= self.max_inflight:
+                    break
+                old, _ = self._q.popleft()
+            old.wait()
+        return w
 
     def _reap_locked(self):
         while self._q and self._q[0][0].is_completed():
@@ -109,13 +148,10 @@ def send_message(message_code, payload: torch.Tensor | None = None, dst: int = 0
     nelem = 0 if payload is None else payload.numel()
     dt = torch.float32 if payload is None else payload.dtype
     header = make_header(message_code, rank, step, version, nelem, dt)
-    works = [dist.isend(header, dst, group=group, tag=TAG_HEADER)]
-    tracker.add(works[0], header)
+    works = [tracker.add(dist.isend(header, dst, group=group, tag=TAG_HEADER), header)]
     if nelem:
         buf = payload.detach().contiguous()
-        w = dist.isend(buf, dst, group=group, tag=TAG_PAYLOAD)
-        tracker.add(w, buf)
-        works.append(w)
+        works.append(tracker.add(dist.isend(buf, dst, group=group, tag=TAG_PAYLOAD), buf))
     return works
 
 

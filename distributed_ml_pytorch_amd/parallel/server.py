@@ -23,6 +23,8 @@ from __future__ import annotations
 
 import logging
 import os
+import queue
+import threading
 import time
 from collections import Counter, defaultdict
 
@@ -103,6 +105,7 @@ class ParameterServer:
         self.checkpoint_path = checkpoint_path
         self.checkpoint_every = checkpoint_every
         self._tracker = M.SendTracker()
+        self._hq = None
         self._send_bufs: dict[int, torch.Tensor] = {}
         self._send_work: dict[int, object] = {}
         self._recv_bufs = defaultdict(dict)
@@ -136,6 +139,10 @@ class ParameterServer:
         return buf
 
     def _reply(self, dst: int):
+        """ParameterUpdate to ``dst``: the shard followed by one fp32 element holding
+        the PS version (number of applied deltas) the snapshot was taken at, so
+        the worker can report its staleness on its next push."""
+        n = self.numel
         if self.payload == "rccl":
             with torch.cuda.stream(self.stream):
                 prev = self._send_work.pop(dst, None)
@@ -143,15 +150,18 @@ class ParameterServer:
                     prev.wait()
                 buf = self._send_bufs.get(dst)
                 if buf is None:
-                    buf = torch.empty_like(self.shard)
+                    buf = torch.empty(n + 1, dtype=torch.float32, device=self.device)
                     self._send_bufs[dst] = buf
-                buf.copy_(self.shard)   # snapshot: later applies never tear the reply
-                self._send_work[dst] = dist.isend(buf[: self.numel], dst, group=self.pairs[dst])
+                buf[:n].copy_(self.shard[:n])   # snapshot: later applies never tear the reply
+                buf[n:].fill_(float(self.version))
+                self._send_work[dst] = dist.isend(buf, dst, group=self.pairs[dst])
         else:
-            snap = self.shard[: self.numel].clone()
+            snap = torch.empty(n + 1, dtype=torch.float32)
+            snap[:n].copy_(self.shard[:n])
+            snap[n] = float(self.version)
             w = dist.isend(snap, dst, group=self.ctrl, tag=M.TAG_REPLY)
             self._tracker.add(w, snap)
-        self.bytes_out += self.numel * 4
+        self.bytes_out += (n + 1) * 4
 
     def _apply(self, delta: torch.Tensor):
         if self._native is not None:
@@ -187,30 +197,76 @@ class ParameterServer:
         elif code == M.MessageCode.Heartbeat:
             pass
 
+    def _check_liveness(self, alive: set):
+        if not self.worker_timeout:
+            return
+        now = time.monotonic()
+        for w in list(alive):
+            if now - self.last_seen[w] > self.worker_timeout:
+                _LOG.warning("PS: worker %d silent for %.1fs, dropping", w,
+                             now - self.last_seen[w])
+                alive.discard(w)
+                self.dropped.append(w)
+
+    def _header_pump(self, q):
+        """Receive thread: any-source headers into ``q`` until every worker has
+        sent Shutdown.  Only headers (TAG_HEADER) are received here; payloads and
+        replies use their own tags on the main thread."""
+        remaining = set(self.workers)
+        try:
+            while remaining:
+                hdr = M.recv_header(None, self.ctrl)
+                q.put(hdr)
+                if hdr[0] == M.MessageCode.Shutdown:
+                    remaining.discard(hdr[1])
+        except BaseException as e:   # surfaced to run()
+            q.put(e)
+
+    def _next_header(self, alive: set):
+        """Any-source header receive.  With a ``worker_timeout`` headers arrive
+        through a receive thread and the main loop waits on its queue with a
+        timeout, so liveness is enforced even when NO message arrives (every
+        remaining worker hung): returns ``None`` once nobody is left alive.
+        (gloo work cannot be polled and a timed ``wait`` closes the connection.)"""
+        if not self.worker_timeout:
+            return M.recv_header(None, self.ctrl)
+        if self._hq is None:
+            self._hq = queue.Queue()
+            threading.Thread(target=self._header_pump, args=(self._hq,), daemon=True,
+                             name="ps-headers").start()
+        tick = min(self.worker_timeout / 4, 0.5)
+        while True:
+            try:
+                item = self._hq.get(timeout=tick)
+            except queue.Empty:
+                self._check_liveness(alive)
+                if not alive:
+                    return None
+                continue
+            if isinstance(item, BaseException):
+                raise RuntimeError(f"PS header receive failed: {item!r}")
+            return item
+
     def run(self):
         alive = set(self.workers)
         _LOG.info("PS rank %d serving workers %s (%s payload, %d params)", self.rank,
                   sorted(alive), self.payload, self.numel)
         while alive:
             try:
-                code, sender, step, version, nelem, dtype = M.recv_header(None, self.ctrl)
+                hdr = self._next_header(alive)
             except RuntimeError as e:
                 # A worker died (connection closed / timeout): keep what we have.
                 _LOG.warning("PS: control receive failed (%r); stopping with %d live workers",
                              e, len(alive))
                 break
+            if hdr is None:
+                break
+            code, sender, step, version, nelem, dtype = hdr
             if code == M.MessageCode.Shutdown:
                 alive.discard(sender)
                 continue
             self.handle(code, sender, step, version, nelem, dtype)
-            if self.worker_timeout:
-                now = time.monotonic()
-                for w in list(alive):
-                    if now - self.last_seen[w] > self.worker_timeout:
-                        _LOG.warning("PS: worker %d silent for %.1fs, dropping", w,
-                                     now - self.last_seen[w])
-                        alive.discard(w)
-                        self.dropped.append(w)
+            self._check_liveness(alive)
         self.finish()
         return self.stats()
 

@@ -36,7 +36,7 @@ from ..parallel.ddp import BucketedAllReduce, FusedSGD
 from ..parallel.server import ParameterServer, make_ps_groups
 from ..utils import checkpoint as ckpt
 from ..utils.data import get_datasets, make_loaders
-from ..utils.metrics import IterationLog, Throughput
+from ..utils.metrics import IterationLog, StepTimer, Throughput, classification_report
 from .dist import DistInfo
 
 _LOG = logging.getLogger(__name__)
@@ -74,7 +74,10 @@ class TrainConfig:
     log_dir: str = "log"
     checkpoint: str | None = None
     checkpoint_every: int = 0
-    resume: str | None = None
+    resume: str | None = None         # base path: workers read <base>.worker<rank>.pt, the PS <base>
+    ps_resume: str | None = None      # explicit PS checkpoint (overrides <base> for the PS)
+    delta_scale: str = "sum"          # sharded PS: "sum" (Downpour PS semantics) | "mean" | float
+    ps_worker_timeout: float = 0.0    # central PS: drop a worker silent this long (0 = never)
     bucket_mb: float = 32.0
     label_smoothing: float = 0.0
     verbose: bool = True
@@ -105,6 +108,13 @@ class Worker:
         self.arena = attach_arena(self.model, shadow_dtype=shadow,
                                   channels_last=True)
         self.ddp = None
+        self.timer = StepTimer()
+        self.step_idx = 0
+        # resume the parameters BEFORE the optimizer exists: its PS client seeds the
+        # master (local / sharded) or the central PS from the live parameters
+        resume = _worker_resume_path(cfg.resume, info.rank) if cfg.resume else None
+        if resume:
+            self.step_idx = ckpt.load_worker_model(resume, self.model)
         params = list(self.model.parameters())
         if cfg.mode == "asgd":
             client = client if client is not None else self._make_client(ps_groups)
@@ -124,9 +134,10 @@ class Worker:
                                 weight_decay=cfg.weight_decay)
         else:
             raise ValueError(f"unknown mode {cfg.mode!r}")
-        self.step_idx = 0
-        if cfg.resume:
-            self.step_idx = ckpt.load_worker_checkpoint(cfg.resume, self.model, self.opt)
+        if isinstance(self.opt, Asynchronous):
+            self.opt.timer = self.timer
+        if resume:
+            ckpt.load_worker_optimizer(resume, self.opt)
 
     def _make_client(self, ps_groups):
         cfg, info = self.cfg, self.info
@@ -135,7 +146,7 @@ class Worker:
         if cfg.ps == "local" or not info.is_distributed:
             return LocalPSClient(**kw)
         if cfg.ps == "sharded":
-            return ShardedPSClient(**kw)
+            return ShardedPSClient(delta_scale=cfg.delta_scale, **kw)
         if cfg.ps == "central":
             ctrl, pairs = ps_groups if ps_groups is not None else (None, {})
             if pairs and self.device.type == "cuda" and _payload(cfg, info) == "rccl":
@@ -196,9 +207,10 @@ class Worker:
         key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
         if self.graph is None or key != self._graph_key:
             return self._capture(x, y)
-        self._gx.copy_(x, non_blocking=True)
-        self._gy.copy_(y, non_blocking=True)
-        self.graph.replay()
+        with self.timer.time("compute_launch"):
+            self._gx.copy_(x, non_blocking=True)
+            self._gy.copy_(y, non_blocking=True)
+            self.graph.replay()
         self.opt.comm_step()
         self.step_idx += 1
         # the captured outputs are overwritten by the next replay
@@ -208,24 +220,38 @@ class Worker:
         """One fwd+bwd+update. Returns (loss, hits) as device tensors (no sync)."""
         if getattr(self, "use_graph", False):
             return self._graph_step(x, y)
-        self.opt.zero_grad()
-        logits = self.model(x)
-        loss, hits = softmax_cross_entropy(logits, y, self.cfg.label_smoothing)
-        loss.backward()
+        with self.timer.time("compute_launch"):
+            self.opt.zero_grad()
+            logits = self.model(x)
+            loss, hits = softmax_cross_entropy(logits, y, self.cfg.label_smoothing)
+            loss.backward()
         if self.ddp is not None:
-            self.ddp.synchronize()
-        self.opt.step()
+            with self.timer.time("allreduce_wait"):
+                self.ddp.synchronize()
+        if isinstance(self.opt, Asynchronous):
+            self.opt.local_step()
+            self.opt.comm_step()
+        else:
+            with self.timer.time("update"):
+                self.opt.step()
         self.step_idx += 1
         return loss.detach(), hits
 
     @torch.no_grad()
-    def evaluate(self, loader, max_batches: int | None = None):
+    def evaluate(self, loader, max_batches: int | None = None, per_class: bool = False):
         """Mean loss and accuracy over ALL test batches (reference used the last batch
-        only, main.py:127); restores train mode afterwards (D6)."""
+        only, main.py:127); restores train mode afterwards (D6).
+
+        ``per_class``: also return the [C, C] confusion matrix (rows = true class),
+        from which :func:`~..utils.metrics.classification_report` prints the
+        reference's verbose per-class precision/recall/F1 table (main.py:127-131).
+        """
         was = self.model.training
         self.model.eval()
         tot_loss = torch.zeros((), device=self.device)
         tot_hits = torch.zeros((), device=self.device, dtype=torch.int64)
+        c = self.num_classes
+        conf = torch.zeros(c * c, device=self.device, dtype=torch.int64) if per_class else None
         n = 0
         nb = 0
         for xb, yb in loader:
@@ -234,14 +260,21 @@ class Worker:
             loss, hits = softmax_cross_entropy(out, yb)
             tot_loss += loss.float() * yb.numel()
             tot_hits += hits.to(torch.int64)
+            if conf is not None:
+                pred = out.float().argmax(1)
+                conf += torch.bincount(yb * c + pred, minlength=c * c)
             n += yb.numel()
             nb += 1
             if max_batches and nb >= max_batches:
                 break
         self.model.train(was)
         if n == 0:
-            return float("nan"), float("nan")
-        return (tot_loss / n).item(), tot_hits.item() / n
+            res = (float("nan"), float("nan"))
+        else:
+            res = ((tot_loss / n).item(), tot_hits.item() / n)
+        if per_class:
+            return (*res, conf.view(c, c).cpu())
+        return res
 
     def set_lr(self, lr: float):
         for g in self.opt.param_groups:
@@ -267,12 +300,13 @@ def run_server(cfg: TrainConfig, info: DistInfo, ps_groups):
                              payload=payload,
                              device=info.device if payload == "rccl" else "cpu",
                              checkpoint_path=cfg.checkpoint,
-                             checkpoint_every=cfg.checkpoint_every)
-    if cfg.resume and os.path.exists(cfg.resume):
-        try:
-            server.load_checkpoint(cfg.resume)
-        except ValueError:
-            pass
+                             checkpoint_every=cfg.checkpoint_every,
+                             worker_timeout=cfg.ps_worker_timeout or None)
+    ps_path = _ps_resume_path(cfg)
+    if ps_path:
+        server.load_checkpoint(ps_path)
+    elif cfg.ps_resume:
+        raise FileNotFoundError(f"--ps-resume {cfg.ps_resume}: no parameter-server checkpoint")
     stats = server.run()
     if cfg.verbose:
         print(f"[ps] finished: {stats}", flush=True)
@@ -298,6 +332,7 @@ def run_training(cfg: TrainConfig, info: DistInfo):
     train_loader, test_loader = make_loaders(tr, te, cfg.batch_size, cfg.test_batch_size,
                                              shuffle_seed=cfg.seed + info.rank)
     log = IterationLog()
+    log_phases = bool(cfg.log_interval)
     meter = Throughput(sync_cuda=w.device.type == "cuda")
     base_lr = cfg.lr
     done = False
@@ -325,14 +360,19 @@ def run_training(cfg: TrainConfig, info: DistInfo):
                               sps=row["samples_per_sec"], **row), flush=True)
             if cfg.checkpoint and cfg.checkpoint_every and w.step_idx % cfg.checkpoint_every == 0:
                 ckpt.save_worker_checkpoint(_worker_ckpt(cfg, info), w.model, w.opt, w.step_idx)
+            if log_phases and i % cfg.log_interval == 0 and i > 0:
+                row.update({f"{k}_ms": v["mean_ms"] for k, v in w.timer.summary().items()})
             if cfg.max_steps and w.step_idx >= cfg.max_steps:
                 done = True
                 break
         if cfg.evaluate and not done:
-            vl, va = w.evaluate(test_loader)
+            vl, va, conf = w.evaluate(test_loader, per_class=True)
             if cfg.verbose:
                 print(f"epoch {epoch}: lr {w.opt.param_groups[0]['lr']:.5g} "
                       f"test loss {vl:.4f} test accuracy {va:.4f}", flush=True)
+                # the reference's verbose eval prints sklearn's per-class report
+                # (/root/reference/example/main.py:127-131)
+                print(classification_report(conf), flush=True)
         if done:
             break
     w.finish()
@@ -350,15 +390,33 @@ def run_training(cfg: TrainConfig, info: DistInfo):
            "data": source, "log": path}
     if isinstance(w.opt, Asynchronous):
         res.update(w.opt.stats())
+    res["phases"] = w.timer.summary()
     if cfg.verbose:
         print(f"[worker {info.rank}] {res}", flush=True)
     return res
 
 
 def _worker_ckpt(cfg, info):
-    base = cfg.checkpoint
-    root, ext = os.path.splitext(base)
-    return f"{root}.worker{info.rank}{ext or '.pt'}"
+    return ckpt.worker_checkpoint_path(cfg.checkpoint, info.rank)
+
+
+def _worker_resume_path(base: str, rank: int) -> str | None:
+    """``<base>.worker<rank>.pt`` if present, else ``base`` when it is itself a worker
+    checkpoint, else ``None`` (e.g. only a PS checkpoint: the worker starts fresh
+    and adopts the PS parameters at its first pull)."""
+    cand = ckpt.worker_checkpoint_path(base, rank)
+    if os.path.exists(cand):
+        return cand
+    if os.path.exists(base) and ckpt.checkpoint_kind(base) == "worker":
+        return base
+    return None
+
+
+def _ps_resume_path(cfg) -> str | None:
+    for p in (cfg.ps_resume, cfg.resume):
+        if p and os.path.exists(p) and ckpt.checkpoint_kind(p) == "ps":
+            return p
+    return None
 
 
 def _fmt(v):

@@ -49,15 +49,29 @@ def save_worker_checkpoint(path: str, model: torch.nn.Module, optimizer=None, st
             "acc": acc.detach().cpu() if acc is not None else None,
             "mom": mom.detach().cpu() if mom is not None else None,
         }
+        client = getattr(optimizer, "client", None)
+        if client is not None:
+            # PS state held on this worker (in-process master / its sharded-PS shard)
+            sd["client"] = client.state_dict()
     if extra:
         sd["extra"] = extra
     _atomic_save(sd, path)
 
 
-def load_worker_checkpoint(path: str, model: torch.nn.Module, optimizer=None) -> int:
+def _load_worker_sd(path: str) -> dict:
     sd = torch.load(path, map_location="cpu", weights_only=True)
     if sd.get("kind") != "worker":
         raise ValueError(f"{path} is not a worker checkpoint")
+    return sd
+
+
+def load_worker_model(path: str, model: torch.nn.Module) -> int:
+    """Restore model parameters/buffers (into the arena views) and return the step.
+
+    Call BEFORE the optimizer is built: the PS client seeds its master (or the
+    central PS) from the live parameters in ``client.init()``.
+    """
+    sd = _load_worker_sd(path)
     with torch.no_grad():
         own = model.state_dict()
         for k, v in sd["model"].items():
@@ -67,14 +81,46 @@ def load_worker_checkpoint(path: str, model: torch.nn.Module, optimizer=None) ->
     arena = get_arena(model)
     if arena is not None:
         arena.refresh_shadow()
-    if optimizer is not None and "opt" in sd:
+        arena.bump()
+    return int(sd["step"])
+
+
+def load_worker_optimizer(path: str, optimizer) -> None:
+    """Restore the optimizer (step index, lr, push accumulator, momentum) and the
+    PS state its client holds (local master, sharded-PS shard)."""
+    sd = _load_worker_sd(path)
+    if "opt" in sd:
         o = sd["opt"]
         if hasattr(optimizer, "idx"):
             optimizer.idx = o["idx"]
         for g in optimizer.param_groups:
             g["lr"] = o["lr"]
-        if o.get("acc") is not None and getattr(optimizer, "acc", None) is not None:
-            optimizer.acc.copy_(o["acc"])
-        if o.get("mom") is not None and getattr(optimizer, "mom", None) is not None:
-            optimizer.mom.copy_(o["mom"])
-    return int(sd["step"])
+        with torch.no_grad():
+            if o.get("acc") is not None and getattr(optimizer, "acc", None) is not None:
+                optimizer.acc.copy_(o["acc"])
+            if o.get("mom") is not None and getattr(optimizer, "mom", None) is not None:
+                optimizer.mom.copy_(o["mom"])
+    client = getattr(optimizer, "client", None)
+    if client is not None and sd.get("client"):
+        client.load_state_dict(sd["client"])
+
+
+def load_worker_checkpoint(path: str, model: torch.nn.Module, optimizer=None) -> int:
+    step = load_worker_model(path, model)
+    if optimizer is not None:
+        load_worker_optimizer(path, optimizer)
+    return step
+
+
+def worker_checkpoint_path(base: str, rank: int) -> str:
+    """Per-rank worker file derived from one ``--checkpoint``/``--resume`` base
+    (the PS writes ``base`` itself)."""
+    root, ext = os.path.splitext(base)
+    return f"{root}.worker{rank}{ext or '.pt'}"
+
+
+def checkpoint_kind(path: str) -> str | None:
+    try:
+        return torch.load(path, map_location="cpu", weights_only=True).get("kind")
+    except (FileNotFoundError, RuntimeError, ValueError):
+        return None

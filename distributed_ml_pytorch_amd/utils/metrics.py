@@ -95,28 +95,78 @@ class Throughput:
         return self.samples / dt if dt > 0 else 0.0
 
 
+class _Phase:
+    __slots__ = ("timer", "name", "t")
+
+    def __init__(self, timer, name):
+        self.timer, self.name = timer, name
+
+    def __enter__(self):
+        self.t = time.perf_counter()
+        return self
+
+    def __exit__(self, *a):
+        dt = time.perf_counter() - self.t
+        tm = self.timer
+        tm.totals[self.name] = tm.totals.get(self.name, 0.0) + dt
+        tm.counts[self.name] = tm.counts.get(self.name, 0) + 1
+        return False
+
+
 class StepTimer:
-    """Accumulates named host-side phase times (compute, push, pull-wait, ...)."""
+    """Host-side time per named step phase (compute, push, pull-issue,
+    land).  The GPU work of these phases is asynchronous; the host times say how
+    long the CPU spends issuing them (what an eager step costs beyond the GPU), and
+    the PS clients add device-side span times of their side-stream collectives
+    (``push_device_ms`` / ``pull_device_ms`` in their stats)."""
 
     def __init__(self):
         self.totals: dict[str, float] = {}
         self.counts: dict[str, int] = {}
 
     def time(self, name: str):
-        timer = self
+        return _Phase(self, name)
 
-        class _Ctx:
-            def __enter__(self_inner):
-                self_inner.t = time.perf_counter()
-
-            def __exit__(self_inner, *a):
-                dt = time.perf_counter() - self_inner.t
-                timer.totals[name] = timer.totals.get(name, 0.0) + dt
-                timer.counts[name] = timer.counts.get(name, 0) + 1
-                return False
-
-        return _Ctx()
+    def reset(self):
+        self.totals.clear()
+        self.counts.clear()
 
     def summary(self) -> dict:
-        return {k: {"total_s": v, "mean_ms": 1e3 * v / max(self.counts[k], 1)}
+        return {k: {"total_s": round(v, 6), "count": self.counts[k],
+                    "mean_ms": round(1e3 * v / max(self.counts[k], 1), 4)}
                 for k, v in self.totals.items()}
+
+
+def classification_report(conf: torch.Tensor, names=None, digits: int = 2) -> str:
+    """Per-class precision / recall / F1 / support from a [C, C] confusion matrix
+    (rows = true class), laid out like sklearn's ``classification_report`` that the
+    reference prints on its verbose evaluation (/root/reference/example/main.py:127-131)."""
+    conf = conf.to(torch.float64)
+    c = conf.shape[0]
+    names = list(names) if names is not None else [str(i) for i in range(c)]
+    tp = conf.diag()
+    support = conf.sum(1)
+    predicted = conf.sum(0)
+    prec = torch.where(predicted > 0, tp / predicted.clamp_min(1), torch.zeros_like(tp))
+    rec = torch.where(support > 0, tp / support.clamp_min(1), torch.zeros_like(tp))
+    f1 = torch.where(prec + rec > 0, 2 * prec * rec / (prec + rec).clamp_min(1e-30),
+                     torch.zeros_like(tp))
+    total = float(support.sum())
+    width = max(max(len(n) for n in names), len("weighted avg"), digits)
+    head = " " * width + "".join(f"{h:>10}" for h in ("precision", "recall", "f1-score",
+                                                      "support"))
+    lines = [head, ""]
+    fmt = "{:>%d}" % width + ("{:>10.%df}" % digits) * 3 + "{:>10}"
+    for i in range(c):
+        lines.append(fmt.format(names[i], float(prec[i]), float(rec[i]), float(f1[i]),
+                                int(support[i])))
+    lines.append("")
+    acc = float(tp.sum()) / total if total else 0.0
+    lines.append(("{:>%d}" % width).format("accuracy") + " " * 20
+                 + ("{:>10.%df}" % digits).format(acc) + f"{int(total):>10}")
+    lines.append(fmt.format("macro avg", float(prec.mean()), float(rec.mean()),
+                            float(f1.mean()), int(total)))
+    w = support / total if total else support
+    lines.append(fmt.format("weighted avg", float((prec * w).sum()), float((rec * w).sum()),
+                            float((f1 * w).sum()), int(total)))
+    return "\n".join(lines)

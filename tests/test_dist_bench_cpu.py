@@ -1,0 +1,296 @@
+"""Multi-process CPU (gloo) tests of the round-2 distributed surface.
+
+* bench.py: self-spawned N ranks (``--gpus N`` without a launcher), the central
+  PS topology (rank 0 = PS, /root/reference/Makefile:13-20), launcher world-size
+  check;
+* PS liveness when EVERY worker hangs (no header ever arrives);
+* the gloo push double-buffer is not refilled before a lagging PS received it;
+* distributed resume (local / central / sharded PS state survives a restart);
+* 4-rank bucketed all-reduce == full-batch SGD; 8-rank central and sharded ASGD
+  convergence.
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from test_dist_cpu import ROOT, _ddp, _port, _run
+
+pytestmark = pytest.mark.slow
+
+
+def _bench(args, env_extra=None, timeout=300):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
+                       capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, lines
+
+
+def test_bench_self_spawns_n_ranks():
+    """``bench.py --gpus 4`` with no launcher env starts 4 ranks itself."""
+    r, lines = _bench(["--gpus", "4", "--steps", "2", "--warmup", "1", "--model", "mlp",
+                       "--batch", "8", "--ttl-target", "0", "--ref-batch", "0"])
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["world_size"] == 4 and out["workers"] == 4
+    assert out["config"]["global_batch"] == 32
+    assert out["backend"] == "gloo" and out["dtype"].startswith("fp32")
+    assert "sharded" in out["config"]["parallelism"]
+
+
+def test_bench_central_ps_three_ranks():
+    """``--ps central``: rank 0 serves, ranks 1-2 train; samples/s counts workers."""
+    r, lines = _bench(["--gpus", "3", "--ps", "central", "--steps", "6", "--warmup", "2",
+                       "--model", "mlp", "--batch", "8", "--n-push", "2", "--n-pull", "2",
+                       "--ttl-target", "0", "--ref-batch", "0"])
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 3 and out["workers"] == 2
+    assert out["config"]["global_batch"] == 16
+    assert out["config"]["parallelism"] == "asgd-central-ps 1ps+2w"
+    ps = out["ps"]
+    # 8 steps per worker, push/pull at idx 0,2,4,6
+    assert ps["counts"] == {"ParameterUpdate": 2, "GradientUpdate": 8, "ParameterRequest": 8}
+    assert ps["version"] == 8
+    assert 0 <= ps["staleness_mean"] <= 4
+
+
+def test_bench_central_ps_with_time_to_target():
+    """Two PS sessions (throughput, then a fresh model for time-to-target)."""
+    r, lines = _bench(["--gpus", "3", "--ps", "central", "--steps", "2", "--warmup", "1",
+                       "--model", "mlp", "--batch", "16", "--n-push", "2", "--n-pull", "2",
+                       "--ttl-target", "1.5", "--ttl-max-steps", "200", "--ttl-signal", "1.0",
+                       "--ref-batch", "0", "--lr", "0.05"])
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads(lines[0])
+    assert out["ttl_reached"] and out["ttl_steps"] <= 200
+
+
+def test_bench_rejects_world_size_mismatch():
+    r, _ = _bench(["--gpus", "3", "--steps", "1"],
+                  env_extra={"RANK": "0", "WORLD_SIZE": "2", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+# ------------------------------------------------- PS liveness: nobody talks
+def _all_silent(rank, world):
+    import time
+
+    from distributed_ml_pytorch_amd.parallel import messaging as M
+    from distributed_ml_pytorch_amd.parallel.server import ParameterServer
+
+    if rank == 0:
+        ps = ParameterServer(numel=16, worker_timeout=1.0)
+        t0 = time.monotonic()
+        st = ps.run()
+        return {"dropped": sorted(st["dropped"]), "secs": time.monotonic() - t0,
+                "version": st["version"]}
+    tr = M.SendTracker()
+    M.send_message(M.MessageCode.ParameterUpdate, torch.zeros(16), tracker=tr)
+    M.send_message(M.MessageCode.GradientUpdate, torch.ones(16), tracker=tr)
+    tr.drain()
+    return "hung"       # never sends Shutdown
+
+
+def test_ps_liveness_fires_when_every_worker_hangs():
+    out = _run(_all_silent, 3)
+    ps = out[0]
+    assert ps["dropped"] == [1, 2] and ps["version"] == 2
+    assert ps["secs"] < 30
+
+
+# ------------------------------------ gloo push buffer vs a lagging PS
+def _lagging_ps(rank, world):
+    import time
+
+    from distributed_ml_pytorch_amd.models import build_model
+    from distributed_ml_pytorch_amd.parallel.asgd import Asynchronous
+    from distributed_ml_pytorch_amd.parallel.clients import GlooPSClient
+    from distributed_ml_pytorch_amd.parallel.server import ParameterServer
+
+    torch.manual_seed(0)
+    m, _, _ = build_model("mlp")
+    if rank == 0:
+        ps = ParameterServer(model=m)
+        time.sleep(1.5)            # let the worker run several pushes ahead
+        ps.run()
+        return ps.parameters().clone().numpy()
+    opt = Asynchronous(m.parameters(), lr=0.1, n_push=1, n_pull=10 ** 6, model=m,
+                       client=GlooPSClient(ps_rank=0, staleness=10 ** 6))
+    init = opt.arena.p32.clone()
+    total = torch.zeros_like(init)
+    for k in range(5):
+        opt.zero_grad()
+        opt.arena.g32.fill_(float(k + 1))     # distinct delta per push
+        total += -0.1 * opt.arena.g32
+        opt.local_step()
+        opt.comm_step()
+    opt.finish()
+    return (init + total).numpy()
+
+
+def test_gloo_push_buffer_survives_lagging_ps():
+    """Five pushes queue up behind a PS that starts late; every delta must arrive
+    intact (the double-buffered send slot is not refilled while gloo still
+    holds it: ADVICE r1)."""
+    out = _run(_lagging_ps, 2)
+    got, exp = torch.from_numpy(out[0]), torch.from_numpy(out[1])
+    n = exp.numel()
+    assert torch.allclose(got[:n], exp, atol=1e-6)
+
+
+# ------------------------------------------------------------------ resume
+def _train_cfg(**kw):
+    from distributed_ml_pytorch_amd.runtime.trainer import TrainConfig
+
+    base = dict(model="mlp", n_train=256, n_test=64, test_batch_size=64, batch_size=32,
+                epochs=1, lr=0.05, n_push=2, n_pull=2, mode="asgd", cuda=False,
+                log_interval=0, evaluate=False, verbose=False, log_dir=tempfile.mkdtemp())
+    base.update(kw)
+    return TrainConfig(**base)
+
+
+def test_local_resume_keeps_weights_and_ps_master(tmp_path):
+    """after resume the first pull must not overwrite the restored
+    weights with the fresh-init PS master."""
+    from distributed_ml_pytorch_amd.runtime.dist import DistInfo
+    from distributed_ml_pytorch_amd.runtime.trainer import Worker
+    from distributed_ml_pytorch_amd.utils import checkpoint as ckpt
+
+    info = DistInfo()
+    cfg = _train_cfg(ps="local", n_push=1, n_pull=1, staleness=0)
+    w = Worker(cfg, info)
+    g = torch.Generator().manual_seed(3)
+    for _ in range(6):
+        w.train_step(torch.randn(32, 1, 28, 28, generator=g),
+                     torch.randint(0, 10, (32,), generator=g))
+    path = str(tmp_path / "ck.pt")
+    wpath = ckpt.worker_checkpoint_path(path, 0)
+    ckpt.save_worker_checkpoint(wpath, w.model, w.opt, w.step_idx)
+    saved = w.arena.p32.clone()
+    w2 = Worker(_train_cfg(ps="local", n_push=1, n_pull=1, staleness=0, resume=path,
+                           seed=99), info)
+    assert w2.step_idx == 6 and w2.opt.idx == w.opt.idx
+    assert torch.equal(w2.arena.p32, saved)
+    assert torch.equal(w2.opt.client.master, w.opt.client.master)
+    w2.train_step(torch.randn(32, 1, 28, 28, generator=g),
+                  torch.randint(0, 10, (32,), generator=g))
+    drift = float((w2.arena.p32 - saved).abs().max())
+    fresh = float((Worker(_train_cfg(ps="local", seed=99), info).arena.p32 - saved).abs().max())
+    assert drift < 0.1 * fresh, (drift, fresh)
+
+
+def _central_resume(rank, world, path, phase):
+    from distributed_ml_pytorch_amd.runtime.dist import DistInfo
+    from distributed_ml_pytorch_amd.runtime.trainer import run_training
+
+    cfg = _train_cfg(ps="central", checkpoint=path, max_steps=4,
+                     resume=path if phase == 2 else None)
+    res = run_training(cfg, DistInfo(rank, world, rank, "gloo", torch.device("cpu")))
+    return {k: v for k, v in res.items() if isinstance(v, (int, float, str, dict))}
+
+
+def test_central_resume_restores_ps_and_workers(tmp_path):
+    path = str(tmp_path / "central.pt")
+    first = _run(_central_resume, 3, path, 1)
+    v1 = first[0]["version"]
+    assert os.path.exists(path) and os.path.exists(str(tmp_path / "central.worker1.pt"))
+    second = _run(_central_resume, 3, path, 2)
+    # the PS continues from its checkpointed version; workers from their step
+    assert second[0]["version"] == v1 + second[0]["counts"]["GradientUpdate"]
+    for r in (1, 2):
+        assert second[r]["steps"] > first[r]["steps"]
+
+
+def _sharded_resume(rank, world, path, phase):
+    from distributed_ml_pytorch_amd.runtime.dist import DistInfo
+    from distributed_ml_pytorch_amd.runtime.trainer import Worker
+    from distributed_ml_pytorch_amd.utils import checkpoint as ckpt
+
+    info = DistInfo(rank, world, rank, "gloo", torch.device("cpu"))
+    if phase == 1:
+        w = Worker(_train_cfg(ps="sharded", staleness=0), info)
+        g = torch.Generator().manual_seed(rank)
+        for _ in range(5):
+            w.train_step(torch.randn(16, 1, 28, 28, generator=g),
+                         torch.randint(0, 10, (16,), generator=g))
+        w.finish()
+        ckpt.save_worker_checkpoint(ckpt.worker_checkpoint_path(path, rank), w.model, w.opt,
+                                    w.step_idx)
+        full = [torch.zeros_like(w.opt.client.master) for _ in range(world)]
+        dist.all_gather(full, w.opt.client.master)
+        return torch.cat(full).numpy()
+    w = Worker(_train_cfg(ps="sharded", staleness=0, resume=path, seed=7), info)
+    full = [torch.zeros_like(w.opt.client.master) for _ in range(world)]
+    dist.all_gather(full, w.opt.client.master)
+    return {"master": torch.cat(full).numpy(), "p32": w.arena.p32.clone().numpy(),
+            "step": w.step_idx}
+
+
+def test_sharded_resume_restores_master_shards(tmp_path):
+    path = str(tmp_path / "sharded.pt")
+    first = _run(_sharded_resume, 2, path, 1)
+    second = _run(_sharded_resume, 2, path, 2)
+    import numpy as np
+
+    for r in (0, 1):
+        assert np.array_equal(second[r]["master"], first[0])
+        assert second[r]["step"] == 5
+        # live parameters re-synced from the restored shards (a forced pull)
+        assert np.array_equal(second[r]["p32"], first[0])
+
+
+# --------------------------------------------------------------- 4 / 8 ranks
+def test_bucketed_allreduce_four_ranks():
+    out = _run(_ddp, 4)
+    for r, res in out.items():
+        assert res["err"] < 1e-5, (r, res)
+
+
+def _converge(rank, world, ps):
+    from distributed_ml_pytorch_amd.runtime.dist import DistInfo
+    from distributed_ml_pytorch_amd.runtime.trainer import run_training
+
+    cfg = _train_cfg(ps=ps, n_train=1024, n_test=256, test_batch_size=256, batch_size=32,
+                     lr=0.02, n_push=4, n_pull=4, evaluate=True, epochs=1,
+                     delta_scale="mean" if ps == "sharded" else "sum")
+    res = run_training(cfg, DistInfo(rank, world, rank, "gloo", torch.device("cpu")))
+    return {k: v for k, v in res.items() if isinstance(v, (int, float, str, dict))}
+
+
+@pytest.mark.parametrize("ps", ["central", "sharded"])
+def test_eight_rank_asgd_converges(ps):
+    """1 PS + 7 workers (reference topology at BASELINE config #3's size) and an
+    8-way sharded PS both learn the synthetic task."""
+    out = _run(_converge, 8, ps)
+    accs = [out[r]["test_accuracy"] for r in out if out[r].get("role") == "worker"]
+    assert len(accs) == (7 if ps == "central" else 8)
+    assert min(accs) > 0.5, accs
+    if ps == "central":
+        assert out[0]["counts"]["GradientUpdate"] == 7 * (1024 // 32 // 4)
+
+
+def test_classification_report_matches_sklearn():
+    sk = pytest.importorskip("sklearn.metrics")
+    from distributed_ml_pytorch_amd.utils.metrics import classification_report
+
+    g = torch.Generator().manual_seed(0)
+    y = torch.randint(0, 5, (400,), generator=g)
+    p = torch.where(torch.rand(400, generator=g) < 0.6, y, torch.randint(0, 5, (400,),
+                                                                         generator=g))
+    conf = torch.bincount(y * 5 + p, minlength=25).view(5, 5)
+    ours = classification_report(conf).split()
+    ref = sk.classification_report(y.numpy(), p.numpy()).split()
+    assert ours == ref
