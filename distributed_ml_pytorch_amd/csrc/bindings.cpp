@@ -617,6 +617,105 @@ void colsum_acc(Tensor dy, Tensor out, optional<Tensor> slots) {
                          out.data_ptr<float>(), sl.data_ptr<float>(), M, (int)N, cur_stream());
 }
 
+// ------------------------------------------------------------------- GEMM
+// 2-D operand with a unit inner stride: checked and its row stride returned
+int64_t mat_ld(const Tensor& t, at::ScalarType dt, int64_t rows, int64_t cols,
+               const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == dt && t.dim() == 2, name, " must be a 2-D ", dt,
+              " GPU tensor");
+  TORCH_CHECK(t.size(0) == rows && t.size(1) == cols, name, " is ", t.sizes(), ", expected [",
+              rows, ", ", cols, "]");
+  TORCH_CHECK(t.stride(1) == 1, name, " must have a unit inner stride");
+  const int64_t ld = rows <= 1 ? cols : t.stride(0);
+  TORCH_CHECK(ld >= cols, name, ": row stride smaller than the row");
+  TORCH_CHECK((int64_t)t.element_size() * rows * ld < (1LL << 31), name,
+              " exceeds the 2 GiB 32-bit offset range of the GEMM kernels");
+  return ld;
+}
+
+// C = epilogue(sum_k A(m, k) B(n, k)); see csrc/gemm.hip.  mode 0: a [M,K], b [N,K];
+// mode 1: a [M,K], b [K,N]; mode 2: a [K,M], b [K,N], c fp32 accumulated.
+void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
+          optional<Tensor> c2, optional<Tensor> bias, optional<Tensor> aux,
+          optional<Tensor> dbias, int64_t splits) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "gemm: mode must be 0 (fwd), 1 (dgrad) or 2 (wgrad)");
+  TORCH_CHECK(c.dim() == 2 && a.dim() == 2 && b.dim() == 2, "gemm: 2-D operands expected");
+  TORCH_CHECK((mode == 0 && (epi == 0 || epi == 1)) || (mode == 1 && (epi == 0 || epi == 2)) ||
+                  (mode == 2 && epi == 3),
+              "gemm: epilogue ", epi, " not available in mode ", mode);
+  TORCH_CHECK(dmp::gemm_config_ok((int)mode, (int)cfg), "gemm: config ", cfg,
+              " is not available in mode ", mode);
+  const int64_t M = c.size(0), N = c.size(1);
+  const int64_t K = mode == 2 ? a.size(0) : a.size(1);
+  const int64_t lda = mat_ld(a, at::kBFloat16, mode == 2 ? K : M, mode == 2 ? M : K, "a");
+  const int64_t ldb = mat_ld(b, at::kBFloat16, mode == 0 ? N : K, mode == 0 ? K : N, "b");
+  const int64_t ldc = mat_ld(c, mode == 2 ? at::kFloat : at::kBFloat16, M, N, "c");
+  if (M == 0 || N == 0) return;
+  auto same_as_c = [&](const Tensor& t, const char* name) {
+    TORCH_CHECK(mat_ld(t, at::kBFloat16, M, N, name) == ldc, name,
+                " must have the output's row stride");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name,
+                " must be 16-byte aligned");
+  };
+  uint16_t* c2p = nullptr;
+  if (epi == 1) {
+    TORCH_CHECK(c2.has_value() && c2->defined(), "gemm: GELU epilogue needs c2");
+    same_as_c(*c2, "c2");
+    c2p = reinterpret_cast<uint16_t*>(c2->data_ptr());
+  }
+  const uint16_t* auxp = nullptr;
+  if (aux.has_value() && aux->defined()) {
+    TORCH_CHECK(epi == 0 || epi == 2, "gemm: aux only with epilogues 0 / 2");
+    same_as_c(*aux, "aux");
+    auxp = reinterpret_cast<const uint16_t*>(aux->data_ptr());
+  }
+  TORCH_CHECK(epi != 2 || auxp != nullptr, "gemm: GELU-backward epilogue needs aux = h");
+  const uint16_t* biasp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(epi == 0 || epi == 1, "gemm: bias only in the forward epilogues");
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 &&
+                    bias->is_contiguous() && bias->numel() == N &&
+                    reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0,
+                "gemm: bias must be a contiguous 8-byte aligned bf16 [N] GPU tensor");
+    biasp = reinterpret_cast<const uint16_t*>(bias->data_ptr());
+  }
+  float* dbp = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(mode == 2, "gemm: dbias only in wgrad mode");
+    TORCH_CHECK(dbias->is_cuda() && dbias->scalar_type() == at::kFloat &&
+                    dbias->is_contiguous() && dbias->numel() == M,
+                "gemm: dbias must be a contiguous fp32 [M] GPU tensor");
+    dbp = dbias->data_ptr<float>();
+  }
+  if (cfg >= 0) {
+    // MFMA tiles: 16-B DMA pieces along k (row-major operand) or along the
+    // row (k-strided operand), 8-B bf16x4 output stores
+    for (const Tensor* t : {&a, &b, &c})
+      TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                  "gemm: operands must be 16-byte aligned for the MFMA kernels");
+    TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm: operand row strides must be multiples of 8");
+    if (mode == 0) TORCH_CHECK(K % 8 == 0, "gemm: K must be a multiple of 8 (else cfg -1)");
+    if (mode == 1) TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm: K, N must be multiples of 8");
+    if (mode == 2) TORCH_CHECK(M % 8 == 0 && N % 8 == 0, "gemm: M, N must be multiples of 8");
+    if (mode != 2)   // 16-B row-segment epilogue stores
+      TORCH_CHECK(N % 8 == 0 && ldc % 8 == 0, "gemm: N, ldc must be multiples of 8");
+  }
+  dmp::launch_gemm((int)mode, (int)epi, (int)cfg, reinterpret_cast<const uint16_t*>(a.data_ptr()),
+                   (int)lda, reinterpret_cast<const uint16_t*>(b.data_ptr()), (int)ldb,
+                   c.data_ptr(), (int)ldc, c2p, biasp, auxp, dbp, (int)M, (int)N, (int)K,
+                   (int)std::max<int64_t>(1, splits), cur_stream());
+}
+
+std::vector<std::vector<int64_t>> gemm_configs() {
+  std::vector<std::vector<int64_t>> out;
+  for (int i = 0; i < dmp::gemm_num_configs(); ++i) {
+    int info[5];
+    dmp::gemm_config_info(i, info);
+    out.push_back({i, info[0], info[1], info[2], info[3], info[4]});
+  }
+  return out;
+}
+
 // ------------------------------------------------------------- transformer
 void check_rows_bf16(const Tensor& t, const char* name) {
   check_gpu(t, name);
@@ -930,6 +1029,12 @@ PYBIND11_MODULE(_native, m) {
   m.def("colsum_acc", &colsum_acc, "bias gradient: out[n] += sum_m dy[m][n] (bf16 -> fp32)",
         py::arg("dy"), py::arg("out"), py::arg("slots") = py::none());
   m.def("colsum_num_slots", &dmp::colsum_num_slots, "slot rows of the colsum scratch");
+  m.def("gemm", &gemm, "bf16 MFMA GEMM (fwd / dgrad / wgrad modes, fused epilogues)",
+        py::arg("mode"), py::arg("epi"), py::arg("cfg"), py::arg("a"), py::arg("b"), py::arg("c"),
+        py::arg("c2") = py::none(), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
+        py::arg("dbias") = py::none(), py::arg("splits") = 1);
+  m.def("gemm_config_ok", &dmp::gemm_config_ok, "tile config usable in this mode");
+  m.def("gemm_configs", &gemm_configs, "[(id, BM, BN, threads, stages, BK)] of the GEMM tiles");
   m.def("attention_fwd", &attention_fwd, "fused MHSA forward on qkv rows -> (out, lse2)");
   m.def("attention_bwd", &attention_bwd, "fused MHSA backward -> dqkv (qkv layout)");
   m.def("attention_max_tokens", &dmp::attention_max_tokens, "max sequence length of the fused path");

@@ -40,6 +40,26 @@ __device__ __forceinline__ u16 f2bf(float f) {
   return __builtin_bit_cast(u16, static_cast<__bf16>(f));
 }
 
+// tanh(u) = 1 - 2 / (1 + e^{2u}): one v_exp_f32 + one v_rcp_f32 instead of
+// the ~30-instruction libm tanhf (the GELU pass was VALU-bound with it).
+__device__ __forceinline__ float fast_tanh(float u) {
+  const float e = __expf(2.f * u);
+  return 1.f - 2.f * __frcp_rn(1.f + e);
+}
+
+// tanh-approximated GELU; *dgelu (optional) receives d gelu / dx
+__device__ __forceinline__ float gelu_tanh(float x, float* dgelu) {
+  constexpr float c0 = 0.7978845608028654f, c1 = 0.044715f;
+  const float x2 = x * x;
+  const float u = c0 * x * (1.f + c1 * x2);
+  const float t = fast_tanh(u);
+  if (dgelu) {
+    const float du = c0 * (1.f + 3.f * c1 * x2);
+    *dgelu = 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+  }
+  return 0.5f * x * (1.f + t);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

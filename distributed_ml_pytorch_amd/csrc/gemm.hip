@@ -1,0 +1,590 @@
+// Dense bf16 GEMM on gfx950 MFMA (v_mfma_f32_16x16x32_bf16) for the Linear
+// layers (SURVEY §2.3 `addmm` / `mm` rows; the reference's nn.Linear heads,
+// /root/reference/example/models.py:11-13,43, and the ViT-B/16 projections):
+//
+//   C[m][n] (+)= epilogue( sum_k A(m, k) * B(n, k) )
+//
+// A(m, k) = A[m*lda + k] (AT = false: k contiguous) or A[k*lda + m] (AT = true),
+// B likewise.  The three passes of a linear layer Y = X W^T + b are:
+//   fwd   Y  = X W^T        AT=0 BT=0   epilogue: + bias [, + addend] or GELU
+//   dgrad dX = dY W          AT=0 BT=1   epilogue: plain, or * GELU'(h) (fused
+//                                        GELU backward of the layer before)
+//   wgrad dW += dY^T X       AT=1 BT=1   fp32 accumulate into the grad arena,
+//                                        bias grad = row sums of dY^T (one extra
+//                                        MFMA against an all-ones operand)
+//
+// Staging: every 64-deep k-tile of both operands is fetched by LDS DMA
+// (buffer_load_dwordx4 ... lds: 16 B per lane, no VGPR round trip) into an
+// NS-deep ring; one counted `s_waitcnt vmcnt` + one raw s_barrier per k-tile
+// (NS-1 tiles in flight).  A k-contiguous operand lands as a [rows][64] image
+// (128-B rows, 16-B chunk XOR swizzle applied on the SOURCE address) read with
+// ds_read_b128; a k-strided operand lands as a [64][rows] image (32-B granule
+// XOR swizzle) read with the gfx950 transposing ds_read_b64_tr_b16, which hands
+// each lane 4 consecutive k of one column -- two such reads are exactly one
+// MFMA operand fragment, in the same k order as the b128 fragment of the other
+// operand, so mixed layouts multiply correctly.  Tails (M, N, K not multiples of
+// the tile) read zeros through out-of-range buffer offsets and drop their
+// stores the same way: no per-element branches.
+//
+// Workgroup -> tile map is XCD-aware: consecutive tiles along N of one M panel
+// land on the same XCD (shared L2) under round-robin dispatch -- a speed
+// choice only, any placement is correct.
+#include "common.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace dmp {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr unsigned kOOBg = 0x80000000u;
+
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_ACC32 = 3 };
+
+// epilogues that may read an aux [M][N] operand (register slots reserved)
+constexpr bool has_aux_slots(int epi) { return epi == EPI_STORE || epi == EPI_DGELU; }
+
+struct GemmArgs {
+  const u16* a;
+  const u16* b;
+  void* c;            // bf16 [M][ldc] (EPI 0-2) or fp32 [M][ldc] (EPI_ACC32)
+  u16* c2;            // EPI_GELU: gelu(h) [M][ldc]  (h itself goes to c)
+  const u16* bias;    // EPI_STORE / EPI_GELU: bf16 [N] (optional)
+  const u16* aux;     // EPI_STORE: bf16 addend [M][ldc] (optional); EPI_DGELU: h [M][ldc]
+  float* dbias;       // EPI_ACC32: fp32 [M] += sum_k A(m, k) (optional)
+  int M, N, K;
+  int lda, ldb, ldc;
+  int k_chunk;        // reduction rows per blockIdx.y (split-K), multiple of BK
+  int tiles_n;
+};
+
+__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+
+// LDS DMA from inline asm (the builtin makes hipcc wait vmcnt(0) before the
+// next ds_read of ANY ring slot, serialising the pipeline); completion counted
+// by hand with wait_vm.
+__device__ __forceinline__ void gdma16(__amdgpu_buffer_rsrc_t rs, unsigned voff,
+                                       u16* lds_wave_base) {
+  const unsigned m0 = (unsigned)(size_t)(__attribute__((address_space(3))) void*)lds_wave_base;
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+               "{m0}"(m0));
+}
+
+template <int N>
+__device__ __forceinline__ void gwait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0070);
+}
+
+// [rows][BK] image, 16-B chunk c of row r holds logical chunk rswz(r, c) (an
+// involution): each ds_read_b128 lane group (16 rows, one chunk) hits 16
+// distinct slots.  BK = 64 (128-B rows, 2 per bank row): c ^= (r>>1)&7;
+// BK = 32 (64-B rows, 4 per bank row): c ^= (-(r>>2))&3.  Rows 16 apart share
+// the XOR.
+template <int BK>
+__device__ __forceinline__ int rswz(int row, int c) {
+  if constexpr (BK == 64) return c ^ ((row >> 1) & 7);
+  else return c ^ ((-(row >> 2)) & 3);
+}
+
+// [64][R] image (R >= 128 bf16 = whole bank rows): 32-B granule u of row r
+// holds logical granule u ^ tf(r).  One half-wave tr read touches rows
+// {8g + q : g = 0,1, q = 0..3} of one granule column; tf gives those 8 rows
+// 8 distinct granules of the 256-B bank row -> conflict-free.
+__device__ __forceinline__ int tf(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
+template <int R>
+__device__ __forceinline__ int toff(int row, int col) {
+  return row * R + (((col >> 4) ^ tf(row)) << 4) + (col & 15);
+}
+
+// One operand's per-lane DMA slots: PW 1-KiB wave-instructions per k-tile
+// (waves wid < INS % NW issue one more when NW does not divide INS).  The
+// per-lane byte offsets are computed once per block (recomputing them per
+// stage cost ~12 VALU per DMA and measured 15-25 % slower on the wgrad tiles).
+// 32-bit offsets; out-of-range pieces read zeros (kOOBg).
+template <int R, bool T, int NW, int BK>
+struct Stager {
+  static constexpr int EL = R * BK;
+  static constexpr int INS = EL / 512;
+  static constexpr int PW = (INS + NW - 1) / NW;
+  static constexpr int PW_MIN = INS / NW;
+  static_assert(EL % 512 == 0, "whole 1-KiB DMA pieces");
+  static_assert(!T || R % 128 == 0, "transposed image rows must be whole 256-B bank rows");
+  unsigned off[PW];   // byte offset of the piece at k = kbase (kOOBg: row/col out of range)
+  int kk[PW];         // k of the piece relative to the k-tile start
+
+  // r0: tile origin along the operand's rows
+  __device__ __forceinline__ void init(int wid, int lane, int r0, int rows, int ld, int kbase) {
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const int e = ((wid + j * NW) % INS) * 512 + lane * 8;
+      if constexpr (!T) {
+        const int row = e / BK;
+        const int kc = rswz<BK>(row, (e % BK) / 8) * 8;
+        kk[j] = kc;
+        off[j] = r0 + row < rows ? 2u * (unsigned)((r0 + row) * ld + kbase + kc) : kOOBg;
+      } else {
+        const int row = e / R, pch = (e % R) / 8;
+        const int col = (((pch >> 1) ^ tf(row)) << 4) + (pch & 1) * 8;
+        kk[j] = row;
+        off[j] = r0 + col < rows ? 2u * (unsigned)((kbase + row) * ld + r0 + col) : kOOBg;
+      }
+    }
+  }
+  // k0: k-tile start relative to kbase; kend: valid k count relative to kbase
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, u16* img, int wid, int k0,
+                                        int kend, int ld) {
+    const unsigned delta = T ? 2u * (unsigned)(k0 * ld) : 2u * (unsigned)k0;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      if (j < PW_MIN || wid + j * NW < INS) {
+        const bool ok = off[j] != kOOBg && k0 + kk[j] < kend;
+        gdma16(rs, ok ? off[j] + delta : kOOBg, img + (wid + j * NW) * 512);
+      }
+    }
+  }
+};
+
+// fragment of 16 rows/cols starting at `r` for k-step ks: row image via one
+// ds_read_b128, transposed image via two ds_read_b64_tr_b16
+template <int R, bool T, int BK>
+__device__ __forceinline__ bf16x8 frag(const u16* img, int r, int ks, int lane) {
+  if constexpr (!T) {
+    const int row = r + (lane & 15);
+    return *reinterpret_cast<const bf16x8*>(img + row * BK + rswz<BK>(row, ks * 4 + (lane >> 4)) * 8);
+  } else {
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int row = ks * 32 + 8 * g + q;
+    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4_t*)(img + toff<R>(row, r + 4 * p)));
+    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4_t*)(img + toff<R>(row + 4, r + 4 * p)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+}
+
+// One output tile per block (a persistent variant whose DMA ring ran across
+// tile boundaries measured no faster on the ViT shapes and 15-70 % slower on
+// the wgrad tiles: profiles/gemm_vs_hipblaslt_r2.txt).
+template <int BM, int BN, int BK, int WM, int WN, int NS, bool AT, bool BT, int EPI>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "wave tiles of 16x16 MFMAs");
+  using SA = Stager<BM, AT, NW, BK>;
+  using SB = Stager<BN, BT, NW, BK>;
+  constexpr int STAGE = SA::EL + SB::EL;
+  constexpr int INS_MIN = SA::PW_MIN + SB::PW_MIN;   // DMAs every wave issues per stage
+  static_assert(NS >= 2 && (NS - 2) * INS_MIN < 64, "pipeline depth");
+  constexpr bool TRANS_OUT = EPI != EPI_ACC32;   // lane owns 4 consecutive n of one m
+  __shared__ __attribute__((aligned(16))) u16 lds[NS * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+
+  // XCD-aware bijective remap of the tile id: blocks sharing an XCD take
+  // consecutive tiles (neighbouring N tiles of one M panel)
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tm = tile / g.tiles_n;
+  const int m0 = tm * BM, n0 = (tile - tm * g.tiles_n) * BN;
+  const int kbase = blockIdx.y * g.k_chunk;
+  const int kend = min(g.K, kbase + g.k_chunk) - kbase;
+  if (kend <= 0) return;
+  const int KT = (kend + BK - 1) / BK;
+
+  SA sa;
+  SB sb;
+  sa.init(wid, lane, m0, g.M, g.lda, kbase);
+  sb.init(wid, lane, n0, g.N, g.ldb, kbase);
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.a, 0, AT ? (int)(2LL * g.K * g.lda) : (int)(2LL * g.M * g.lda), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.b, 0, BT ? (int)(2LL * g.K * g.ldb) : (int)(2LL * g.N * g.ldb), 0x00020000);
+  auto stage = [&](int buf, int kt) {
+    u16* As = lds + buf * STAGE;
+    sa.issue(rsA, As, wid, kt * BK, kend, g.lda);
+    sb.issue(rsB, As + SA::EL, wid, kt * BK, kend, g.ldb);
+  };
+
+  f32x4 acc[TM][TN];
+  f32x4 accb[TM];
+  bf16x8 ones;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ones.v[k] = 0x3f80;   // bf16 1.0
+  const int ra = wm * (BM / WM), rb = wn * (BN / WN);
+  bool do_bias = false;
+
+  auto compute = [&](int buf) {
+    const u16* As = lds + buf * STAGE;
+    const u16* Bs = As + SA::EL;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag<BM, AT, BK>(As, ra + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = frag<BN, BT, BK>(Bs, rb + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = TRANS_OUT ? mfma_bf16(bf[j], af[i], acc[i][j])
+                                : mfma_bf16(af[i], bf[j], acc[i][j]);
+      if (EPI == EPI_ACC32 && do_bias) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) accb[i] = mfma_bf16(af[i], ones, accb[i]);
+      }
+    }
+  };
+
+  // tile start: accumulators = bias (fwd) or 0
+  auto tile_init = [&](int m0, int n0) {
+    if constexpr (EPI == EPI_ACC32) {
+      do_bias = g.dbias != nullptr && n0 == 0 && wn == 0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + rb + j * 16 + 4 * (lane >> 4);
+        f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+        if (EPI != EPI_DGELU && g.bias != nullptr && n < g.N) {
+          const uint2 raw = *reinterpret_cast<const uint2*>(g.bias + n);
+          bv = f32x4{__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
+                     __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][j] = bv;
+      }
+    }
+  };
+
+  auto epilogue = [&](int m0, int n0) {
+    if constexpr (EPI == EPI_ACC32) {
+      // D layout: lane holds rows m = 4*(lane>>4) + r of column n = lane & 15
+      float* C = reinterpret_cast<float*>(g.c);
+      const bool atomic = gridDim.y > 1;
+      if (do_bias && (lane & 15) == 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + ra + i * 16 + 4 * (lane >> 4) + r;
+            if (m < g.M) atomicAdd(g.dbias + m, accb[i][r]);
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + rb + j * 16 + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + ra + i * 16 + 4 * (lane >> 4) + r;
+            if (m < g.M && n < g.N) {
+              float* p = C + (long long)m * g.ldc + n;
+              if (atomic) atomicAdd(p, acc[i][j][r]);
+              else *p += acc[i][j][r];
+            }
+          }
+        }
+    } else {
+      // bf16 outputs: the D^T register layout (lane: 4 consecutive n of one m)
+      // would make every store / aux load touch 16 rows x 32 B.  Each wave
+      // stages its tile through LDS instead (free after the k-loop; row pitch
+      // padded by 16 B) and re-reads it as rows of 16-B chunks: the epilogue
+      // math, the aux load (GELU' pre-activation / addend) and the stores all
+      // move whole row segments.
+      constexpr int WROWS = BM / WM, WCOLS = BN / WN, CPR = WCOLS / 8, RPI = 64 / CPR;
+      // 16-B row padding when it fits, else (256x256 ring) an XOR swizzle of the
+      // 16-B chunks by row & 7 (needs 8 chunks per row)
+      constexpr bool SWZ = NW * WROWS * (WCOLS + 8) > NS * STAGE;
+      constexpr int PITCH = SWZ ? WCOLS : WCOLS + 8;
+      static_assert(NW * WROWS * PITCH <= NS * STAGE, "epilogue tile fits in the ring's LDS");
+      static_assert(!SWZ || CPR == 8, "swizzled epilogue tile needs 8 chunks per row");
+      auto pchunk = [](int row, int c) { return SWZ ? (c ^ (row & 7)) : c; };
+      constexpr int NR = (WROWS + RPI - 1) / RPI;   // row segments per lane
+      const int cbytes = (int)(2LL * g.M * g.ldc);
+      const __amdgpu_buffer_rsrc_t rsC =
+          __builtin_amdgcn_make_buffer_rsrc(g.c, 0, cbytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rsC2 = __builtin_amdgcn_make_buffer_rsrc(
+          EPI == EPI_GELU ? (void*)g.c2 : g.c, 0, cbytes, 0x00020000);
+      const bool has_aux = g.aux != nullptr;
+      const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
+          has_aux ? (void*)g.aux : g.c, 0, cbytes, 0x00020000);
+      const int lrow = lane / CPR, ch = lane - lrow * CPR;
+      const bool lane_on = lrow < RPI;
+      const int n = n0 + rb + ch * 8;
+      unsigned o[NR];
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        const int row = q * RPI + lrow, m = m0 + ra + row;
+        o[q] = (lane_on && row < WROWS && m < g.M && n < g.N) ? 2u * (unsigned)(m * g.ldc + n)
+                                                              : kOOBg;
+      }
+      // the aux row segments (GELU' pre-activation / addend) are fetched first,
+      // so their latency overlaps the LDS staging below
+      u32x4_t xa[has_aux_slots(EPI) ? NR : 1];
+      if (EPI == EPI_DGELU || (EPI == EPI_STORE && has_aux)) {
+#pragma unroll
+        for (int q = 0; q < (has_aux_slots(EPI) ? NR : 1); ++q)
+          xa[q] = __builtin_amdgcn_raw_buffer_load_b128(rsX, o[q], 0, 0);
+      }
+      __syncthreads();            // every wave is done reading the ring
+      u16* wl = lds + wid * (WROWS * PITCH);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = i * 16 + (lane & 15), c16 = 2 * j + (lane >> 5);
+          const int col = pchunk(row, c16) * 8 + 4 * ((lane >> 4) & 1);
+          uint2 pk;
+          pk.x = (u32)f2bf(acc[i][j][0]) | ((u32)f2bf(acc[i][j][1]) << 16);
+          pk.y = (u32)f2bf(acc[i][j][2]) | ((u32)f2bf(acc[i][j][3]) << 16);
+          *reinterpret_cast<uint2*>(wl + row * PITCH + col) = pk;
+        }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        const int row = min(q * RPI + lrow, WROWS - 1);   // idle lanes re-read a valid row
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(wl + row * PITCH + pchunk(row, ch) * 8);
+        bf16x8 xv;
+        if (has_aux_slots(EPI)) xv = __builtin_bit_cast(bf16x8, xa[has_aux_slots(EPI) ? q : 0]);
+        bf16x8 out, out2;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = bf2f(v.v[e]);
+          if constexpr (EPI == EPI_STORE) {
+            out.v[e] = has_aux ? f2bf(a + bf2f(xv.v[e])) : v.v[e];
+          } else if constexpr (EPI == EPI_GELU) {
+            out.v[e] = v.v[e];                                 // h (pre-activation)
+            out2.v[e] = f2bf(gelu_tanh(a, nullptr));           // gelu of the stored h
+          } else {   // EPI_DGELU: xv = pre-activation h
+            float d;
+            gelu_tanh(bf2f(xv.v[e]), &d);
+            out.v[e] = f2bf(a * d);
+          }
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, out), rsC, o[q], 0, 0);
+        if constexpr (EPI == EPI_GELU)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, out2), rsC2, o[q], 0,
+                                                 0);
+      }
+    }
+  };
+
+  // bias (fwd) into the accumulators before any DMA is in flight
+  tile_init(m0, n0);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < KT) stage(s, s);
+  for (int kt = 0; kt < KT; ++kt) {
+    // k-tile kt landed for this wave (younger ones may still fly) ...
+    if (kt + NS - 2 < KT) gwait_vm<(NS - 2) * INS_MIN>();
+    else gwait_vm<0>();
+    // ... and for every wave; everyone is done reading slot (kt-1) % NS
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NS - 1 < KT) stage((kt + NS - 1) % NS, kt + NS - 1);
+    compute(kt % NS);
+  }
+  epilogue(m0, n0);
+}
+
+// ------------------------------------------------------- any-shape fallback
+// Odd shapes the 16-B DMA tiles cannot take (a reduction length or output
+// width that is not a multiple of 8: LeNet's 84-wide layer, 10-class heads)
+// and tiny GEMMs: 64x64 output tile per 256-thread block, 4x4 outputs per
+// thread, k staged through LDS 16 at a time as fp32, same epilogues.
+template <bool AT, bool BT, int EPI>
+__global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
+  __shared__ float As[16][65], Bs[16][65];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int kbase = blockIdx.z * g.k_chunk;
+  const int kend = min(g.K, kbase + g.k_chunk);
+  const bool do_bias = EPI == EPI_ACC32 && g.dbias != nullptr && blockIdx.y == 0 && tx == 0;
+  float acc[4][4] = {};
+  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kbase; k0 < kend; k0 += 16) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, r = e >> 4, kk = e & 15, k = k0 + kk;
+      const int m = m0 + r, n = n0 + r;
+      float av = 0.f, bv = 0.f;
+      if (k < kend && m < g.M)
+        av = bf2f(AT ? g.a[(long long)k * g.lda + m] : g.a[(long long)m * g.lda + k]);
+      if (k < kend && n < g.N)
+        bv = bf2f(BT ? g.b[(long long)k * g.ldb + n] : g.b[(long long)n * g.ldb + k]);
+      As[kk][r] = av;
+      Bs[kk][r] = bv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float a4[4], b4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a4[i] = As[kk][ty + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b4[j] = Bs[kk][tx + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (do_bias) rsum[i] += a4[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a4[i], b4[j], acc[i][j]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + ty + 16 * i;
+    if (m >= g.M) continue;
+    if (do_bias) atomicAdd(g.dbias + m, rsum[i]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + tx + 16 * j;
+      if (n >= g.N) continue;
+      const long long o = (long long)m * g.ldc + n;
+      const float v = acc[i][j];
+      if constexpr (EPI == EPI_ACC32) {
+        float* C = reinterpret_cast<float*>(g.c);
+        if (gridDim.z > 1) atomicAdd(C + o, v);
+        else C[o] += v;
+      } else {
+        u16* C = reinterpret_cast<u16*>(g.c);
+        const float b = (EPI != EPI_DGELU && g.bias != nullptr) ? bf2f(g.bias[n]) : 0.f;
+        if constexpr (EPI == EPI_STORE) {
+          C[o] = f2bf(v + b + (g.aux != nullptr ? bf2f(g.aux[o]) : 0.f));
+        } else if constexpr (EPI == EPI_GELU) {
+          const u16 h = f2bf(v + b);
+          C[o] = h;
+          g.c2[o] = f2bf(gelu_tanh(bf2f(h), nullptr));
+        } else {
+          float d;
+          gelu_tanh(bf2f(g.aux[o]), &d);
+          C[o] = f2bf(v * d);
+        }
+      }
+    }
+  }
+}
+
+template <bool AT, bool BT, int EPI>
+void launch_small(const GemmArgs& g, int splits, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_small_kernel<AT, BT, EPI>),
+                     dim3((unsigned)((g.M + 63) / 64), (unsigned)((g.N + 63) / 64), (unsigned)splits),
+                     dim3(256), 0, s, g);
+}
+
+// ------------------------------------------------------------------ configs
+struct Cfg { int bm, bn, bk, wm, wn, ns; };
+// LDS = ns * (bm + bn) * bk * 2 B.  Tile heights 160 / 192 exist for tile
+// counts: M = 12608 tokens x N = 768 is 150 tiles of 256x256 (59 % of 256 CUs)
+// but 237 of 160x256.  A k-strided (transposed) operand needs a tile side that
+// is a multiple of 128 (whole 256-B LDS bank rows): gemm_config_ok().
+constexpr Cfg kCfgs[] = {
+    {256, 256, 64, 2, 4, 2},   // 0: 128 KiB, 8 waves (128x64 per wave), 1 block/CU
+    {256, 128, 64, 4, 2, 3},   // 1: 144 KiB, 8 waves (64x64)
+    {128, 256, 64, 2, 4, 3},   // 2: 144 KiB, 8 waves (64x64)
+    {192, 256, 64, 2, 4, 2},   // 3: 112 KiB, 8 waves (96x64)
+    {128, 128, 64, 2, 2, 2},   // 4:  64 KiB, 4 waves, 2 blocks/CU
+    {160, 256, 64, 2, 4, 2},   // 5: 104 KiB, 8 waves (80x64)
+    {256, 192, 64, 2, 4, 2},   // 6: 112 KiB, 8 waves (128x48)
+    {128, 128, 32, 2, 2, 4},   // 7:  64 KiB, 4 waves, 2 blocks/CU, 3 k-tiles in flight
+    {256, 128, 64, 2, 2, 3},   // 8: 144 KiB, 4 waves of 128x64 (1 wave / SIMD)
+};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+constexpr bool cfg_ok(const Cfg& c, bool at, bool bt) {
+  return (!at || c.bm % 128 == 0) && (!bt || c.bn % 128 == 0);
+}
+
+template <int C, bool AT, bool BT, int EPI>
+void launch_cfg(const GemmArgs& a, int splits, hipStream_t s) {
+  constexpr Cfg c = kCfgs[C];
+  if constexpr (!cfg_ok(c, AT, BT)) {
+    throw std::runtime_error("gemm: tile config not valid for a k-strided operand");
+  } else {
+    GemmArgs g = a;
+    g.tiles_n = (g.N + c.bn - 1) / c.bn;
+    const int tiles = ((g.M + c.bm - 1) / c.bm) * g.tiles_n;
+    hipLaunchKernelGGL((gemm_kernel<c.bm, c.bn, c.bk, c.wm, c.wn, c.ns, AT, BT, EPI>),
+                       dim3((unsigned)tiles, (unsigned)splits), dim3(64 * c.wm * c.wn), 0, s, g);
+  }
+}
+
+template <bool AT, bool BT, int EPI>
+void launch_mode(int cfg, const GemmArgs& a, int splits, hipStream_t s) {
+  switch (cfg) {
+    case -1: launch_small<AT, BT, EPI>(a, splits, s); break;
+    case 0: launch_cfg<0, AT, BT, EPI>(a, splits, s); break;
+    case 1: launch_cfg<1, AT, BT, EPI>(a, splits, s); break;
+    case 2: launch_cfg<2, AT, BT, EPI>(a, splits, s); break;
+    case 3: launch_cfg<3, AT, BT, EPI>(a, splits, s); break;
+    case 4: launch_cfg<4, AT, BT, EPI>(a, splits, s); break;
+    case 5: launch_cfg<5, AT, BT, EPI>(a, splits, s); break;
+    case 6: launch_cfg<6, AT, BT, EPI>(a, splits, s); break;
+    case 7: launch_cfg<7, AT, BT, EPI>(a, splits, s); break;
+    default: launch_cfg<8, AT, BT, EPI>(a, splits, s); break;
+  }
+}
+
+}  // namespace
+
+int gemm_num_configs() { return kNumCfgs; }
+
+bool gemm_config_ok(int mode, int cfg) {
+  if (cfg == -1) return true;
+  if (cfg < 0 || cfg >= kNumCfgs) return false;
+  return cfg_ok(kCfgs[cfg], mode == 2, mode >= 1);
+}
+
+void gemm_config_info(int cfg, int* info) {
+  const Cfg& c = kCfgs[cfg];
+  info[0] = c.bm;
+  info[1] = c.bn;
+  info[2] = 64 * c.wm * c.wn;
+  info[3] = c.ns;
+  info[4] = c.bk;
+}
+
+// mode 0: fwd (C = A B^T, EPI 0 or 1), 1: dgrad (A [M][K], B [K][N]; EPI 0 or 2),
+// 2: wgrad (A [K][M], B [K][N]; fp32 accumulate)
+void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
+                 int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
+                 const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
+                 hipStream_t s) {
+  GemmArgs g{};
+  g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.aux = aux; g.dbias = dbias;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  if (splits < 1 || mode != 2) splits = 1;   // split-K only for the fp32-accumulating pass
+  g.k_chunk = ((K + splits - 1) / splits + 63) / 64 * 64;   // whole k-tiles of any BK
+  splits = (K + g.k_chunk - 1) / g.k_chunk;
+  if (mode == 0) {
+    if (epi == EPI_GELU) launch_mode<false, false, EPI_GELU>(cfg, g, 1, s);
+    else launch_mode<false, false, EPI_STORE>(cfg, g, 1, s);
+  } else if (mode == 1) {
+    if (epi == EPI_DGELU) launch_mode<false, true, EPI_DGELU>(cfg, g, 1, s);
+    else launch_mode<false, true, EPI_STORE>(cfg, g, 1, s);
+  } else {
+    launch_mode<true, true, EPI_ACC32>(cfg, g, splits, s);
+  }
+}
+
+}  // namespace dmp

@@ -141,6 +141,19 @@ void launch_bn_fwd_partials(const uint16_t* x, const uint16_t* res, uint16_t* y,
                             float* stats, float* part, long long M, int C,
                             float momentum, float eps, bool relu, hipStream_t s);
 
+// gemm.hip: bf16 MFMA GEMM for linear layers.  mode 0 fwd C = A B^T (A [M][K],
+// B [N][K]); mode 1 dgrad (A [M][K], B [K][N]); mode 2 wgrad, fp32 C += (A [K][M],
+// B [K][N]), split-K over `splits`.  epi: 0 store (+bias, +aux addend),
+// 1 GELU (c = h, c2 = gelu(h)), 2 c = acc * gelu'(aux), 3 fp32 accumulate
+// (+ dbias row sums).  cfg -1: any-shape fallback kernel.
+int gemm_num_configs();
+bool gemm_config_ok(int mode, int cfg);   // tile shape usable for this pass
+void gemm_config_info(int cfg, int* info);   // {BM, BN, threads, stages, BK}
+void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
+                 int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
+                 const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
+                 hipStream_t s);
+
 // conv.hip: every conv weight of a flat bf16 shadow transposed in one launch
 void launch_conv_weight_transpose_batched(const uint16_t* src, uint16_t* dst,
                                           const long long* table, int n, long long max_elems,

@@ -238,24 +238,7 @@ __global__ void __launch_bounds__(256) layernorm_param_grad_kernel(float* __rest
 }
 
 // ----------------------------------------------------------------------- GELU
-// tanh(u) = 1 - 2 / (1 + e^{2u}): one v_exp_f32 + one v_rcp_f32 instead of
-// the ~30-instruction libm tanhf (the GELU pass was VALU-bound with it).
-__device__ __forceinline__ float fast_tanh(float u) {
-  const float e = __expf(2.f * u);
-  return 1.f - 2.f * __frcp_rn(1.f + e);
-}
-
-__device__ __forceinline__ float gelu_tanh(float x, float* dgelu) {
-  constexpr float c0 = 0.7978845608028654f, c1 = 0.044715f;
-  const float x2 = x * x;
-  const float u = c0 * x * (1.f + c1 * x2);
-  const float t = fast_tanh(u);
-  if (dgelu) {
-    const float du = c0 * (1.f + 3.f * c1 * x2);
-    *dgelu = 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
-  }
-  return 0.5f * x * (1.f + t);
-}
+// (gelu_tanh / fast_tanh live in common.h: the GEMM epilogues share them)
 
 __global__ void __launch_bounds__(256) gelu_fwd_kernel(const u16* __restrict__ x,
                                                        u16* __restrict__ y, long long nvec) {

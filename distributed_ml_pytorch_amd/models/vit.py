@@ -4,11 +4,12 @@ Not in the reference (no sequence models there).  ViT-B/16 at
 224x224 = 197 tokens, D=768, 12 heads, MLP 3072, 86,567,656 parameters with a
 1000-class head.  LayerNorm and tanh-GELU are native kernels
 (``csrc/transformer.hip``), multi-head attention is one fused MFMA kernel per
-direction on the qkv rows (``csrc/attention.hip``); the projection / MLP GEMMs
-run forward / dgrad on hipBLASLt (``F.linear``) and their weight + bias
-gradients on the native MFMA wgrad kernel, accumulating fp32 straight into the
-grad arena (``ops.linear``).  Patch embedding is a stride-16 conv computed as
-one GEMM over gathered patch rows (``ops.linear.patch_embed``).
+direction on the qkv rows (``csrc/attention.hip``); every projection / MLP GEMM
+(forward, data and weight gradient) runs on the native MFMA GEMM
+(``csrc/gemm.hip`` via ``ops.linear``), the MLP as one fused autograd op whose
+fc1 epilogue applies GELU and whose fc2 data-gradient epilogue applies GELU'.
+Patch embedding is a stride-16 conv computed as one GEMM over gathered patch
+rows (``ops.linear.patch_embed``).
 """
 from __future__ import annotations
 
@@ -21,7 +22,7 @@ import torch.nn.functional as F
 from ..ops import layers as L
 from ..ops import functional as DF
 from ..ops.functional import compute_weight
-from ..ops.linear import patch_embed, patch_embed_ok
+from ..ops.linear import mlp, mlp_ok, patch_embed, patch_embed_ok
 
 
 class LayerNorm(nn.LayerNorm):
@@ -77,9 +78,14 @@ class Block(nn.Module):
         self.fc1 = L.Linear(dim, hidden)
         self.fc2 = L.Linear(hidden, dim)
 
+    def mlp(self, y):
+        if self.training and mlp_ok(y, self.fc1, self.fc2):
+            return mlp(y, self.fc1, self.fc2)       # GELU fused into the GEMM epilogues
+        return self.fc2(DF.gelu(self.fc1(y)))
+
     def forward(self, x):
         x = x + self.attn(self.norm1(x))
-        return x + self.fc2(DF.gelu(self.fc1(self.norm2(x))))
+        return x + self.mlp(self.norm2(x))
 
     def forward_fused(self, h, pending=None):
         """Residual stream ``h`` plus the previous block's unadded MLP output
@@ -91,7 +97,7 @@ class Block(nn.Module):
         else:
             h, y = self.norm1.add_forward(h, pending)
         h, y = self.norm2.add_forward(h, self.attn(y))
-        return h, self.fc2(DF.gelu(self.fc1(y)))
+        return h, self.mlp(y)
 
 
 class VisionTransformer(nn.Module):

@@ -1,21 +1,30 @@
-"""Fully-connected layer with arena-direct fp32 weight gradients.
+"""Fully-connected layers on the native MFMA GEMM (``csrc/gemm.hip``).
 
-Forward and data gradient are plain bf16 GEMMs (hipBLASLt through
-``F.linear`` / ``matmul``) on the arena's bf16 weight shadow, so no per-step
-cast.  The weight gradient is ONE bf16 x bf16 -> fp32 GEMM that accumulates
-straight into the fp32 arena gradient view -- the native MFMA wgrad kernel
-(a 1x1 convolution's weight gradient) when the dims are multiples of 64,
-else ``addmm`` with an fp32 ``out_dtype`` and ``beta = 1``: no bf16
-weight-gradient tensor, no mixed-dtype add kernel, no AccumulateGrad.  On the
-native path the bias gradient is summed by the same kernel from the dY tiles it
-already stages; otherwise it is one native column-sum pass (``csrc/linear.hip``)
-adding straight into the fp32 arena view.  Both fire the parameter's grad-ready
-hook (bucketed all-reduce in sync DP) as soon as they land.
+Parity: the reference's ``nn.Linear`` layers (/root/reference/example/models.py:
+11-13 LeNet fc1-3, :43 AlexNet classifier; ATen ``addmm`` / ``mm`` / ``sum`` rows
+of SURVEY §2.3) in fp32; here bf16 compute with fp32 master weights.
 
-Parity: the reference's ``nn.Linear`` layers (/root/reference/example/models.py
-LeNet/AlexNet/MLP heads) in fp32; here bf16 compute with fp32 master weights.
+All three passes of a linear layer run on one hand-written gfx950 kernel family:
+
+* forward ``Y = X W^T + b``: bias folded into the accumulator init; the ViT MLP
+  runs fc1 with a GELU epilogue that writes both the pre-activation ``h`` (kept
+  for backward) and ``gelu(h)`` (fc2's input) -- no separate GELU pass;
+* data gradient ``dX = dY W``: W is read k-strided through transposed LDS reads
+  (no transposed weight copy); in the MLP the fc2 dgrad epilogue multiplies by
+  ``gelu'(h)`` so it produces fc1's output gradient directly;
+* weight gradient ``dW += dY^T X``: fp32 accumulated straight into the flat
+  grad arena (split-K with atomics when the output is small), the bias
+  gradient summed by the same kernel from the dY tiles it already stages.
+
+Tile shape (and split-K) are picked per (pass, shape) by measurement on first
+use (``ops.tuner``); shapes the 16-B DMA tiles cannot take (a dimension not a
+multiple of 8: 10-class heads, LeNet's 84-wide layer) run the any-shape
+fallback kernel of the same file.  ``DMP_GEMM=auto`` also lets hipBLASLt
+compete for the plain forward / data-gradient GEMMs (default ``native``).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
@@ -23,8 +32,11 @@ from torch.autograd import Function
 
 from ._ext import native
 from .functional import _notify
+from .tuner import TUNER
 
-
+_GEMM_MODE = os.environ.get("DMP_GEMM", "native")
+_BLAS = -1000          # candidate id of the library GEMM (DMP_GEMM=auto only)
+_SMALL = -1            # any-shape fallback kernel
 _COLSUM_SCRATCH: dict = {}
 
 
@@ -47,6 +59,108 @@ def bias_grad_acc(dy, out):
     native().colsum_acc(dy, out, colsum_scratch(dy.device, n))
 
 
+# ----------------------------------------------------------------- dispatcher
+def _mfma_ok(mode: int, M: int, N: int, K: int, *mats) -> bool:
+    """The MFMA tiles' layout constraints (mirrors the checks in bindings.cpp)."""
+    for t in mats:
+        if t is None:
+            continue
+        if t.stride(-1) != 1 or t.data_ptr() % 16 or (t.shape[0] > 1 and t.stride(0) % 8):
+            return False
+    if mode in (0, 1):
+        return K % 8 == 0 and N % 8 == 0
+    return M % 8 == 0 and N % 8 == 0
+
+
+def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bool):
+    if not ok:
+        return [_SMALL * 16 + 1]
+    cands = []
+    for c in native().gemm_configs():
+        cid = c[0]
+        if not native().gemm_config_ok(mode, cid):
+            continue
+        if mode == 2:
+            for s in (1, 2, 3, 4, 6, 8):
+                if s == 1 or K >= 256 * s:
+                    cands.append(cid * 16 + s)
+        else:
+            cands.append(cid * 16 + 1)
+    if M * N * K < (1 << 22):
+        cands.append(_SMALL * 16 + 1)
+    if _GEMM_MODE == "auto" and plain and mode in (0, 1):
+        cands.append(_BLAS)
+    return cands
+
+
+def _default(mode: int, M: int, N: int, K: int, ok: bool) -> int:
+    """Heuristic pick when tuning is off or a graph is being captured."""
+    if not ok:
+        return _SMALL * 16 + 1
+    if mode == 2:
+        return 4 * 16 + (4 if K >= 4096 else 1)
+    return 4 * 16 + 1
+
+
+def _blas(mode, a, b, c, bias):
+    if mode == 0:
+        if bias is not None:
+            torch.addmm(bias, a, b.t(), out=c)
+        else:
+            torch.mm(a, b.t(), out=c)
+    else:
+        torch.mm(a, b, out=c)
+
+
+def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None):
+    """C = epilogue(A(m,k) B(n,k)) on the native kernels (see csrc/gemm.hip):
+    mode 0 fwd (a [M,K], b [N,K]), 1 dgrad (a [M,K], b [K,N]), 2 wgrad (a [K,M],
+    b [K,N], fp32 c accumulated); epi 0 store(+bias,+aux), 1 GELU, 2 x gelu'(aux),
+    3 fp32 accumulate (+dbias)."""
+    M, N = c.shape
+    K = a.shape[0] if mode == 2 else a.shape[1]
+    if M == 0 or N == 0:
+        return
+    ok = _mfma_ok(mode, M, N, K, a, b, c, c2, aux)
+    plain = epi == 0 and aux is None
+    key = ("gemm", mode, epi, M, N, K, bias is not None, aux is not None, dbias is not None)
+    pick = TUNER.cache.get(key)
+    if pick is None:
+        cands = _candidates(mode, epi, M, N, K, plain, ok)
+        if len(cands) == 1:
+            pick = cands[0]
+        else:
+            if mode == 2:      # never time into the live grad arena
+                cs = torch.zeros_like(c)
+                ds = torch.zeros_like(dbias) if dbias is not None else None
+            else:
+                cs, ds = c, dbias
+
+            def run(e):
+                if e == _BLAS:
+                    _blas(mode, a, b, cs, bias)
+                else:
+                    native().gemm(mode, epi, e // 16 if e >= 0 else _SMALL, a, b, cs, c2, bias,
+                                  aux, ds, e % 16 if e >= 0 else 1)
+            pick = TUNER.best(key, run, cands)
+            if pick == -1:
+                pick = _default(mode, M, N, K, ok)
+    if pick == _BLAS:
+        _blas(mode, a, b, c, bias)
+        return
+    cfg, splits = (pick // 16, pick % 16) if pick >= 0 else (_SMALL, 1)
+    native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits)
+
+
+def _rows(t, k):
+    """[.., k] -> a [rows, k] operand with unit inner stride (copies only if needed)."""
+    t2 = t.reshape(-1, k)
+    if t2.stride(-1) != 1 or t2.data_ptr() % 16 or (t2.shape[0] > 1 and t2.stride(0) % 8):
+        t2 = t2.contiguous()
+    return t2
+
+
+# ------------------------------------------------------------ arena plumbing
 def _arena_grad(p):
     if p is None or not p.requires_grad or not getattr(p, "_dmp_arena", False):
         return None
@@ -59,81 +173,58 @@ def _arena_grad(p):
     return g if g.is_contiguous() else None
 
 
-def _native_wgrad_ok(dy2, x2) -> bool:
-    M, N = dy2.shape
-    K = x2.shape[1]
-    return (dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and N % 64 == 0
-            and K % 64 == 0 and M * max(N, K) * 2 < (1 << 30)
-            and dy2.is_contiguous() and x2.is_contiguous())
-
-
-def _native_wgrad(dy2, x2, g, gb=None):
-    """g[N, K] += dy2^T @ x2 as a 1x1 convolution weight gradient on the native
-    MFMA wgrad kernel (csrc/conv_wgrad.hip): fp32 atomics straight into the
-    arena.  Measured against hipBLASLt's fp32-output addmm on the ViT-B/16
-    shapes (scripts/linear_vs_conv1x1.py, profiles/linear_vs_conv1x1_r1.txt):
-    1.1-2x faster; forward / dgrad stay on hipBLASLt (it wins those).
-    ``gb``: optional fp32 [N] bias gradient, accumulated by the same kernel from
-    the dY tiles it already stages (no separate column-sum pass over dY)."""
-    from .conv import _wgrad_cfg
-
-    M, N = dy2.shape
-    K = x2.shape[1]
-    dy4 = dy2.view(M, 1, 1, N).permute(0, 3, 1, 2)     # NCHW view of NHWC memory
-    x4 = x2.view(M, 1, 1, K).permute(0, 3, 1, 2)
-    g4 = g.view(N, K, 1, 1)
-    cfg = _wgrad_cfg(dy4, x4, (N, K, 1, 1), 1, 0)
-    native().conv_wgrad(dy4, x4, g4, 1, 0, cfg, gb)
+def _weight_grads(dy2, x2, w, b):
+    """dW (+ db) of ``y = x W^T + b``: accumulated into the fp32 arena views
+    when the parameters live in one (grad-ready hooks fired), else returned."""
+    N, K = dy2.shape[1], x2.shape[1]
+    gw = gb = None
+    g = _arena_grad(w) if w is not None and w.requires_grad else None
+    gbias = _arena_grad(b) if b is not None and b.requires_grad else None
+    tmp_w = g is None and w is not None and w.requires_grad
+    tmp_b = gbias is None and b is not None and b.requires_grad
+    if g is None and (tmp_w or tmp_b or gbias is not None):
+        g = torch.zeros(N, K, dtype=torch.float32, device=dy2.device)
+    if tmp_b:
+        gbias = torch.zeros(N, dtype=torch.float32, device=dy2.device)
+    if g is not None:
+        gemm(2, 3, dy2, x2, g, dbias=gbias)
+    if tmp_w:
+        gw = g.to(w.dtype)
+        if w.dim() == 4:                     # patch embedding: (kh, kw, Cin) columns
+            gw = gw.view(w.shape[0], w.shape[2], w.shape[3], w.shape[1]).permute(0, 3, 1, 2)
+    elif w is not None and w.requires_grad:
+        _notify(w)
+    if tmp_b:
+        gb = gbias.to(b.dtype)
+    elif b is not None and b.requires_grad:
+        _notify(b)
+    return gw, gb
 
 
 class _ArenaLinear(Function):
     @staticmethod
     def forward(ctx, x, w16, b16, w, b):
-        ctx.save_for_backward(x, w16)
+        N, K = w16.shape
+        x2 = _rows(x, K)
+        y = torch.empty(x2.shape[0], N, dtype=x.dtype, device=x.device)
+        gemm(0, 0, x2, w16, y, bias=b16)
+        ctx.save_for_backward(x2, w16)
         ctx.params = (w, b)
-        return F.linear(x, w16, b16)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
-        x, w16 = ctx.saved_tensors
+        x2, w16 = ctx.saved_tensors
         w, b = ctx.params
-        K, N = x.shape[-1], dy.shape[-1]
-        dy2 = dy.reshape(-1, N)
-        x2 = x.reshape(-1, K)
-        dx = (dy2 @ w16).view(x.shape) if ctx.needs_input_grad[0] else None
-        gw = gb = None
-        g = _arena_grad(w)
-        bias_done = False
-        if g is not None:
-            if _native_wgrad_ok(dy2, x2):
-                gbias = _arena_grad(b) if (b is not None and b.requires_grad) else None
-                _native_wgrad(dy2, x2, g, gbias)
-                bias_done = gbias is not None
-            else:
-                torch.ops.aten.addmm.dtype_out(g, dy2.t(), x2, torch.float32, out=g)
-            _notify(w)
-        elif w is not None and w.requires_grad:
-            gw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).to(w.dtype)
-            if w.dim() == 4:                     # patch embedding: (kh, kw, Cin) columns
-                gw = gw.view(w.shape[0], w.shape[2], w.shape[3], w.shape[1]).permute(0, 3, 1, 2)
-        if b is not None and b.requires_grad:
-            g = _arena_grad(b)
-            vec = dy2.dtype == torch.bfloat16 and N % 8 == 0    # 16-B column chunks
-            if g is not None:
-                if bias_done:
-                    pass                         # summed by the weight-gradient kernel
-                elif vec:
-                    bias_grad_acc(dy2, g)        # one pass straight into the arena
-                else:
-                    g.add_(dy2.sum(0, dtype=torch.float32))
-                _notify(b)
-            else:
-                col = torch.zeros(N, dtype=torch.float32, device=dy.device)
-                if vec:
-                    bias_grad_acc(dy2, col)
-                else:
-                    col += dy2.sum(0, dtype=torch.float32)
-                gb = col.to(b.dtype)
+        N, K = w16.shape
+        dy2 = _rows(dy, N)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(dy2.shape[0], K, dtype=dy.dtype, device=dy.device)
+            gemm(1, 0, dy2, w16, dx)
+            dx = dx.view(ctx.xshape)
+        gw, gb = _weight_grads(dy2, x2, w, b)
         return dx, None, None, gw, gb
 
 
@@ -153,6 +244,58 @@ def linear(x, w, b):
     return _ArenaLinear.apply(x, w16, b16, w, b)
 
 
+# ------------------------------------------------------------ fused ViT MLP
+class _ArenaMLP(Function):
+    """``fc2(gelu_tanh(fc1(x)))`` as 4 + 1 native GEMMs with the GELU in the
+    epilogues: fc1 forward writes (h, gelu(h)); fc2's data gradient multiplies
+    by gelu'(h) and IS fc1's output gradient.  Replaces two library GEMMs + a
+    GELU pass forward and a GELU-backward pass."""
+
+    @staticmethod
+    def forward(ctx, x, w1_16, b1_16, w2_16, b2_16, w1, b1, w2, b2):
+        H, D = w1_16.shape
+        x2 = _rows(x, D)
+        M = x2.shape[0]
+        h = torch.empty(M, H, dtype=x.dtype, device=x.device)
+        g = torch.empty_like(h)
+        gemm(0, 1, x2, w1_16, h, c2=g, bias=b1_16)
+        y = torch.empty(M, w2_16.shape[0], dtype=x.dtype, device=x.device)
+        gemm(0, 0, g, w2_16, y, bias=b2_16)
+        ctx.save_for_backward(x2, h, g, w1_16, w2_16)
+        ctx.params = (w1, b1, w2, b2)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], y.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, g, w1_16, w2_16 = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        dy2 = _rows(dy, w2_16.shape[0])
+        gw2, gb2 = _weight_grads(dy2, g, w2, b2)
+        dh = torch.empty_like(h)
+        gemm(1, 2, dy2, w2_16, dh, aux=h)          # (dY W2) * gelu'(h)
+        gw1, gb1 = _weight_grads(dh, x2, w1, b1)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x2)
+            gemm(1, 0, dh, w1_16, dx)
+            dx = dx.view(ctx.xshape)
+        return dx, None, None, None, None, gw1, gb1, gw2, gb2
+
+
+def mlp_ok(x, fc1, fc2) -> bool:
+    return (arena_linear_ok(x, fc1.weight, fc1.bias)
+            and arena_linear_ok(x, fc2.weight, fc2.bias))
+
+
+def mlp(x, fc1, fc2):
+    """``fc2(gelu_tanh(fc1(x)))`` for two arena-backed linear layers."""
+    w1, b1, w2, b2 = fc1.weight, fc1.bias, fc2.weight, fc2.bias
+    return _ArenaMLP.apply(x, w1._dmp_w16, b1._dmp_w16 if b1 is not None else None,
+                           w2._dmp_w16, b2._dmp_w16 if b2 is not None else None, w1, b1, w2, b2)
+
+
+# ---------------------------------------------------------- patch embedding
 def patch_embed_ok(x, w, b, patch: int) -> bool:
     """Non-overlapping ``patch`` x ``patch`` conv whose weight lives in an arena
     with a channels-last bf16 shadow: computable as one GEMM on patch rows."""
@@ -171,9 +314,8 @@ def patch_embed(x, w, b, patch: int):
     ``[B, C, H, W] -> [B, (H/p)(W/p), Cout]`` tokens.  The patch rows are
     gathered in the weight's physical (kh, kw, Cin) order, so the channels-last
     arena shadow is the GEMM's [Cout, K] operand as-is, and the weight gradient
-    lands in the arena through the native wgrad kernel like any linear layer.
-    No input gradient (pixels), so no dgrad GEMM.  Replaces a library conv
-    forward + backward-weights pair."""
+    lands in the arena like any linear layer's.  No input gradient (pixels), so
+    no dgrad GEMM.  Replaces a library conv forward + backward-weights pair."""
     B, C, H, W = x.shape
     gh, gw = H // patch, W // patch
     xp = (x.reshape(B, C, gh, patch, gw, patch).permute(0, 2, 4, 3, 5, 1)
@@ -181,3 +323,8 @@ def patch_embed(x, w, b, patch: int):
     w16 = w._dmp_w16.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
     b16 = b._dmp_w16 if b is not None else None
     return _ArenaLinear.apply(xp, w16, b16, w, b)
+
+
+def plain_linear(x, w, b):
+    """Library fallback (CPU, fp32, no arena)."""
+    return F.linear(x, w, b)

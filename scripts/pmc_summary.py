@@ -7,15 +7,17 @@ from collections import defaultdict
 
 
 def main(paths):
+    show_all = "--all" in paths
+    paths = [p for p in paths if p != "--all"]
     for path in paths:
         rows = list(csv.DictReader(open(path)))
         per = defaultdict(lambda: defaultdict(list))
         for r in rows:
-            name = r["Kernel_Name"].split("(")[0][:90]
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:90]
             per[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
         print(f"== {path}")
         for k, cs in per.items():
-            if "conv" not in k and "wgrad" not in k:
+            if not show_all and "conv" not in k and "wgrad" not in k:
                 continue
             vals = {c: statistics.median(v) for c, v in cs.items()}
             print(f"  {k}")
@@ -25,6 +27,10 @@ def main(paths):
             if "SQ_INSTS_VALU" in vals and "SQ_INSTS_MFMA" in vals:
                 print(f"    VALU/MFMA = {vals['SQ_INSTS_VALU'] / max(vals['SQ_INSTS_MFMA'], 1):.2f}  "
                       f"LDS/MFMA = {vals.get('SQ_INSTS_LDS', 0) / max(vals['SQ_INSTS_MFMA'], 1):.2f}")
+            if "TCC_HIT_sum" in vals and "TCC_MISS_sum" in vals:
+                print(f"    L2 hit rate = {vals['TCC_HIT_sum'] / max(vals['TCC_HIT_sum'] + vals['TCC_MISS_sum'], 1):.3f}")
+            if "SQ_BUSY_CYCLES" in vals and "SQ_WAVE_CYCLES" in vals and "SQ_WAVES" in vals:
+                pass
             if "SQ_LDS_BANK_CONFLICT" in vals and "SQ_LDS_IDX_ACTIVE" in vals:
                 print(f"    LDS bank conflict / active = {vals['SQ_LDS_BANK_CONFLICT'] / max(vals['SQ_LDS_IDX_ACTIVE'], 1):.3f}")
 

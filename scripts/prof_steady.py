@@ -13,7 +13,7 @@ from collections import defaultdict
 
 
 def short(name):
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     return n[:110]
 
 

@@ -7,7 +7,7 @@ from collections import defaultdict
 
 
 def family(name):
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     n = re.sub(r"<.*", "", n)
     if n.startswith("igemm_") or "conv" in n.lower() and "dmp::" not in n:
         return "miopen:" + n.split("_")[0] + "_" + n.split("_")[1]

@@ -87,3 +87,55 @@ def test_patch_embed_gemm_matches_conv(B, C, H, P, D):
     assert rel(pe.weight.grad, w.grad) < 1e-2
     assert rel(pe.bias.grad, b.grad) < 1e-2
     assert pe.weight.grad.data_ptr() == arena.g32.data_ptr() + 4 * arena.slots[0].offset
+
+
+@pytest.mark.parametrize("M,D,H", [(394, 768, 3072), (130, 64, 256)])
+def test_fused_mlp_matches_fp32(M, D, H):
+    """fc2(gelu(fc1(x))) as the fused native op (GELU in the fc1 forward
+    epilogue, GELU' in the fc2 data-gradient epilogue) vs fp32 PyTorch on the
+    same bf16 weights: output, input gradient, all four parameter gradients."""
+    from distributed_ml_pytorch_amd.ops import layers as L
+    from distributed_ml_pytorch_amd.ops.linear import mlp, mlp_ok
+    from distributed_ml_pytorch_amd.parallel.arena import FlatArena
+
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(L.Linear(D, H), L.Linear(H, D)).cuda()
+    FlatArena(net, device="cuda")
+    fc1, fc2 = net[0], net[1]
+    x = torch.randn(M, D, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    assert mlp_ok(x, fc1, fc2)
+    c = torch.randn(M, D, device="cuda")
+    y = mlp(x, fc1, fc2)
+    (y.float() * c).sum().backward()
+    p = [t._dmp_w16.float().detach().requires_grad_(True)
+         for t in (fc1.weight, fc1.bias, fc2.weight, fc2.bias)]
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.gelu(xr @ p[0].t() + p[1], approximate="tanh") @ p[2].t() + p[3]
+    (yr * c).sum().backward()
+    rel = lambda a, b: float((a.float() - b).norm() / (b.norm() + 1e-12))
+    assert rel(y, yr) < 2e-2
+    assert rel(x.grad, xr.grad) < 3e-2
+    for t, r in zip((fc1.weight, fc1.bias, fc2.weight, fc2.bias), p):
+        assert rel(t.grad, r.grad) < 3e-2
+
+
+def test_linear_odd_head_native():
+    """10-class head (N % 8 != 0) and 84-wide reduction run the any-shape native
+    kernel in all three passes (LeNet fc3: 84 -> 10)."""
+    from distributed_ml_pytorch_amd.ops import layers as L
+    from distributed_ml_pytorch_amd.parallel.arena import FlatArena
+
+    torch.manual_seed(0)
+    lin = L.Linear(84, 10).cuda()
+    FlatArena(lin, device="cuda")
+    x = torch.randn(64, 84, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    c = torch.randn(64, 10, device="cuda")
+    (lin(x).float() * c).sum().backward()
+    w = lin.weight._dmp_w16.float().detach().requires_grad_(True)
+    b = lin.bias._dmp_w16.float().detach().requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    ((xr @ w.t() + b) * c).sum().backward()
+    rel = lambda a, r: float((a.float() - r).norm() / (r.norm() + 1e-12))
+    assert rel(lin.weight.grad, w.grad) < 1e-2
+    assert rel(lin.bias.grad, b.grad) < 1e-2
+    assert rel(x.grad, xr.grad) < 2e-2
