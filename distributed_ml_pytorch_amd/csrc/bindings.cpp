@@ -287,8 +287,8 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K, int64_t S, int64_t P) {
   check_nhwc_bf16(x, "x");
   TORCH_CHECK(x.dim() == 4, "maxpool expects 4-D input");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
-  TORCH_CHECK(C % 8 == 0 && K >= 1 && K <= 15 && S >= 1 && P >= 0 && 2 * P <= K,
-              "maxpool: C % 8 == 0, 1 <= K <= 15, S >= 1, 0 <= P <= K/2");
+  TORCH_CHECK(K >= 1 && K <= 15 && S >= 1 && P >= 0 && 2 * P <= K,
+              "maxpool: 1 <= K <= 15, S >= 1, 0 <= P <= K/2");
   const int Ho = dmp::maxpool_out(H, (int)K, (int)S, (int)P);
   const int Wo = dmp::maxpool_out(W, (int)K, (int)S, (int)P);
   TORCH_CHECK(Ho > 0 && Wo > 0, "maxpool: window larger than input");
@@ -319,6 +319,60 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t K, int64
   return dx;
 }
 
+// ----------------------------------------------------------- im2col / relu
+// x: bf16 channels_last [B, CI, H, W] -> [B*OH*OW, Kp] patch rows, k = (r, s, ci)
+Tensor im2col(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Kp) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4, "im2col: 4-D input");
+  const int B = (int)x.size(0), CI = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(R >= 1 && S >= 1 && stride >= 1 && pad >= 0, "im2col: bad geometry");
+  const int OH = (int)((H + 2 * pad - R) / stride + 1), OW = (int)((W + 2 * pad - S) / stride + 1);
+  TORCH_CHECK(OH > 0 && OW > 0, "im2col: window larger than the padded input");
+  const int64_t K = R * S * CI;
+  TORCH_CHECK(Kp >= K && Kp % 8 == 0, "im2col: Kp must be >= R*S*CI and a multiple of 8");
+  TORCH_CHECK(2LL * B * OH * OW * Kp < (1LL << 40), "im2col: patch matrix too large");
+  Tensor cols = at::empty({(int64_t)B * OH * OW, Kp}, x.options());
+  dmp::launch_im2col(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                     reinterpret_cast<uint16_t*>(cols.data_ptr()), B, H, W, CI, OH, OW, (int)R,
+                     (int)S, (int)stride, (int)pad, (int)K, (int)Kp, cur_stream());
+  return cols;
+}
+
+// dcols [B*OH*OW, Kp] -> dX bf16 channels_last [B, CI, H, W]
+Tensor col2im(Tensor dcols, int64_t B, int64_t CI, int64_t H, int64_t W, int64_t R, int64_t S,
+              int64_t stride, int64_t pad) {
+  check_gpu(dcols, "dcols");
+  TORCH_CHECK(dcols.scalar_type() == at::kBFloat16 && dcols.dim() == 2 && dcols.is_contiguous(),
+              "col2im: dcols must be a contiguous bf16 [M, Kp] tensor");
+  const int OH = (int)((H + 2 * pad - R) / stride + 1), OW = (int)((W + 2 * pad - S) / stride + 1);
+  TORCH_CHECK(dcols.size(0) == B * OH * OW && dcols.size(1) >= R * S * CI,
+              "col2im: dcols shape does not match the conv geometry");
+  Tensor dx = at::empty({B, CI, H, W}, dcols.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dmp::launch_col2im(reinterpret_cast<const uint16_t*>(dcols.data_ptr()),
+                     reinterpret_cast<uint16_t*>(dx.data_ptr()), (int)B, (int)H, (int)W, (int)CI,
+                     OH, OW, (int)R, (int)S, (int)stride, (int)pad, (int)dcols.size(1),
+                     cur_stream());
+  return dx;
+}
+
+// dx = y > 0 ? dy : 0 over dense bf16 tensors of one layout (out may alias dy)
+Tensor relu_bwd(Tensor dy, Tensor y, optional<Tensor> out) {
+  check_gpu(y, "y");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16, "relu_bwd: bf16 tensors");
+  const auto mf = y.dim() == 4 && y.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                          !y.is_contiguous()
+                      ? at::MemoryFormat::ChannelsLast
+                      : at::MemoryFormat::Contiguous;
+  dy = dy.contiguous(mf);
+  TORCH_CHECK(dy.sizes() == y.sizes() && dy.scalar_type() == at::kBFloat16, "relu_bwd: dy shape");
+  Tensor dx = out.has_value() && out->defined() ? *out : at::empty_like(dy);
+  TORCH_CHECK(dx.sizes() == y.sizes() && dx.is_contiguous(mf), "relu_bwd: out layout");
+  dmp::launch_relu_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(y.data_ptr()),
+                       reinterpret_cast<uint16_t*>(dx.data_ptr()), y.numel(), cur_stream());
+  return dx;
+}
+
 // ---------------------------------------------------------------- convolution
 // x: bf16 channels_last [B, CI, H, W]; w: bf16 channels_last [CO, CI, R, S].
 struct ConvGeom {
@@ -345,7 +399,8 @@ ConvGeom conv_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad
 }
 
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bool want_stats,
-                             int64_t cfg, optional<Tensor> slots, optional<Tensor> bias) {
+                             int64_t cfg, optional<Tensor> slots, optional<Tensor> bias,
+                             bool relu) {
   check_nhwc_bf16(x, "x");
   check_gpu(w, "w");
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -371,7 +426,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
                        reinterpret_cast<uint16_t*>(y.data_ptr()),
                        want_stats ? part.data_ptr<float>() : nullptr, g.B, g.H, g.W, g.CI, g.OH,
                        g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream(),
-                       bias ? bias->data_ptr<float>() : nullptr);
+                       bias ? bias->data_ptr<float>() : nullptr, relu);
   return {y, part, at::scalar_tensor(G, at::kLong)};
 }
 
@@ -637,7 +692,8 @@ int64_t mat_ld(const Tensor& t, at::ScalarType dt, int64_t rows, int64_t cols,
 // mode 1: a [M,K], b [K,N]; mode 2: a [K,M], b [K,N], c fp32 accumulated.
 void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
           optional<Tensor> c2, optional<Tensor> bias, optional<Tensor> aux,
-          optional<Tensor> dbias, int64_t splits) {
+          optional<Tensor> dbias, int64_t splits, bool relu) {
+  TORCH_CHECK(!relu || epi == 0, "gemm: relu only with the store epilogue");
   TORCH_CHECK(mode >= 0 && mode <= 2, "gemm: mode must be 0 (fwd), 1 (dgrad) or 2 (wgrad)");
   TORCH_CHECK(c.dim() == 2 && a.dim() == 2 && b.dim() == 2, "gemm: 2-D operands expected");
   TORCH_CHECK((mode == 0 && (epi == 0 || epi == 1)) || (mode == 1 && (epi == 0 || epi == 2)) ||
@@ -690,20 +746,30 @@ void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
   if (cfg >= 0) {
     // MFMA tiles: 16-B DMA pieces along k (row-major operand) or along the
     // row (k-strided operand), 8-B bf16x4 output stores
-    for (const Tensor* t : {&a, &b, &c})
+    for (const Tensor* t : {&a, &b})
       TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
                   "gemm: operands must be 16-byte aligned for the MFMA kernels");
+    if (mode != 2)   // bf16 output rows are stored as 16-B pieces when ldc allows
+      TORCH_CHECK(reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 == 0,
+                  "gemm: the bf16 output must be 16-byte aligned");
     TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm: operand row strides must be multiples of 8");
+    auto c8 = [](int64_t v) { return (v + 7) / 8 * 8; };
     if (mode == 0) TORCH_CHECK(K % 8 == 0, "gemm: K must be a multiple of 8 (else cfg -1)");
-    if (mode == 1) TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm: K, N must be multiples of 8");
-    if (mode == 2) TORCH_CHECK(M % 8 == 0 && N % 8 == 0, "gemm: M, N must be multiples of 8");
-    if (mode != 2)   // 16-B row-segment epilogue stores
-      TORCH_CHECK(N % 8 == 0 && ldc % 8 == 0, "gemm: N, ldc must be multiples of 8");
+    if (mode == 1)
+      TORCH_CHECK(K % 8 == 0 && (N % 8 == 0 || ldb >= c8(N)),
+                  "gemm: K must be a multiple of 8, N too unless padded in b's row stride");
+    // k-strided operands are fetched in 8-column pieces: a partial last piece
+    // may read into the row padding, never past the row stride
+    if (mode == 2)
+      TORCH_CHECK((M % 8 == 0 || lda >= c8(M)) && (N % 8 == 0 || ldb >= c8(N)),
+                  "gemm: wgrad M, N must be multiples of 8 or padded in the row stride");
+    // bf16 outputs: 16-B row segments, or element stores when N / ldc are not
+    // multiples of 8 (any width)
   }
   dmp::launch_gemm((int)mode, (int)epi, (int)cfg, reinterpret_cast<const uint16_t*>(a.data_ptr()),
                    (int)lda, reinterpret_cast<const uint16_t*>(b.data_ptr()), (int)ldb,
                    c.data_ptr(), (int)ldc, c2p, biasp, auxp, dbp, (int)M, (int)N, (int)K,
-                   (int)std::max<int64_t>(1, splits), cur_stream());
+                   (int)std::max<int64_t>(1, splits), cur_stream(), relu);
 }
 
 std::vector<std::vector<int64_t>> gemm_configs() {
@@ -983,7 +1049,8 @@ std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optio
 PYBIND11_MODULE(_native, m) {
   m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM conv forward (+BN partials)",
         py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
-        py::arg("cfg") = -1, py::arg("slots") = py::none(), py::arg("bias") = py::none());
+        py::arg("cfg") = -1, py::arg("slots") = py::none(), py::arg("bias") = py::none(),
+        py::arg("relu") = false);
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM conv data gradient", py::arg("dy"),
         py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"),
         py::arg("cfg") = -1, py::arg("wt") = py::none(), py::arg("addend") = py::none());
@@ -1032,7 +1099,14 @@ PYBIND11_MODULE(_native, m) {
   m.def("gemm", &gemm, "bf16 MFMA GEMM (fwd / dgrad / wgrad modes, fused epilogues)",
         py::arg("mode"), py::arg("epi"), py::arg("cfg"), py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("c2") = py::none(), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
-        py::arg("dbias") = py::none(), py::arg("splits") = 1);
+        py::arg("dbias") = py::none(), py::arg("splits") = 1, py::arg("relu") = false);
+  m.def("im2col", &im2col, "NHWC patch rows [B*OH*OW, Kp], k = (r, s, ci), zero-padded",
+        py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));
+  m.def("col2im", &col2im, "gather-form inverse of im2col -> channels_last dX", py::arg("dcols"),
+        py::arg("B"), py::arg("CI"), py::arg("H"), py::arg("W"), py::arg("R"), py::arg("S"),
+        py::arg("stride"), py::arg("pad"));
+  m.def("relu_bwd", &relu_bwd, "ReLU backward from the saved output", py::arg("dy"), py::arg("y"),
+        py::arg("out") = py::none());
   m.def("gemm_config_ok", &dmp::gemm_config_ok, "tile config usable in this mode");
   m.def("gemm_configs", &gemm_configs, "[(id, BM, BN, threads, stages, BK)] of the GEMM tiles");
   m.def("attention_fwd", &attention_fwd, "fused MHSA forward on qkv rows -> (out, lse2)");

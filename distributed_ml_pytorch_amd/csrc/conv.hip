@@ -47,6 +47,7 @@ struct ConvArgs {
   long long M;      // fwd: B*OH*OW; dgrad: rows of the largest parity class
   const float* bias;   // optional fp32 [CO] added in the fwd epilogue
   const u16* addend;   // dgrad: optional [B][H][W][CI] bf16 added to dX in the epilogue
+  int relu;            // fwd: max(0, .) in the epilogue (conv -> ReLU, AlexNet)
 };
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -350,7 +351,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        h[r] = f2bf(acc[i][j][r] + bj[j][r] + ad[r]);
+        float t = acc[i][j][r] + bj[j][r] + ad[r];
+        if (MODE == 0 && a.relu) t = fmaxf(t, 0.f);
+        h[r] = f2bf(t);
         v[r] = bf2f(h[r]);   // statistics of the stored (rounded) values
       }
       const u32x2_t packed = {(u32)h[0] | ((u32)h[1] << 16), (u32)h[2] | ((u32)h[3] << 16)};
@@ -614,7 +617,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        hv[r] = f2bf(acc[i][j][r] + bj[j][r] + ad[r]);
+        float t = acc[i][j][r] + bj[j][r] + ad[r];
+        if (!FLIP && a.relu) t = fmaxf(t, 0.f);
+        hv[r] = f2bf(t);
         v[r] = bf2f(hv[r]);
       }
       const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
@@ -867,9 +872,9 @@ int conv_fwd_num_mblocks(long long M, int CO, int cfg) {
 
 void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int H, int W,
                      int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                     hipStream_t s, const float* bias) {
+                     hipStream_t s, const float* bias, bool relu) {
   ConvArgs a{x, w, y, part, B, H, W, CI, OH, OW, CO, R, S, stride, pad,
-             (long long)B * OH * OW, bias, nullptr};
+             (long long)B * OH * OW, bias, nullptr, relu ? 1 : 0};
   if (cfg >= kHaloBase) {
     if (part ? launch_halo<false, true>(a, cfg, s) : launch_halo<false, false>(a, cfg, s)) return;
     cfg = -1;   // not applicable to this geometry: heuristic implicit-GEMM tile

@@ -61,6 +61,7 @@ struct GemmArgs {
   int lda, ldb, ldc;
   int k_chunk;        // reduction rows per blockIdx.y (split-K), multiple of BK
   int tiles_n;
+  int relu;           // EPI_STORE: max(0, .) after bias / addend (linear -> ReLU)
 };
 
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -330,6 +331,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
       const int lrow = lane / CPR, ch = lane - lrow * CPR;
       const bool lane_on = lrow < RPI;
       const int n = n0 + rb + ch * 8;
+      // an output width / row stride that is not whole 16-B pieces (10-class
+      // heads, LeNet's 84 / 6 / 16 columns) is stored element by element
+      const bool narrow = ((g.N | g.ldc) & 7) != 0;
       unsigned o[NR];
 #pragma unroll
       for (int q = 0; q < NR; ++q) {
@@ -340,7 +344,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
       // the aux row segments (GELU' pre-activation / addend) are fetched first,
       // so their latency overlaps the LDS staging below
       u32x4_t xa[has_aux_slots(EPI) ? NR : 1];
-      if (EPI == EPI_DGELU || (EPI == EPI_STORE && has_aux)) {
+      if (!narrow && (EPI == EPI_DGELU || (EPI == EPI_STORE && has_aux))) {
 #pragma unroll
         for (int q = 0; q < (has_aux_slots(EPI) ? NR : 1); ++q)
           xa[q] = __builtin_amdgcn_raw_buffer_load_b128(rsX, o[q], 0, 0);
@@ -364,13 +368,25 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
         const int row = min(q * RPI + lrow, WROWS - 1);   // idle lanes re-read a valid row
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(wl + row * PITCH + pchunk(row, ch) * 8);
         bf16x8 xv;
-        if (has_aux_slots(EPI)) xv = __builtin_bit_cast(bf16x8, xa[has_aux_slots(EPI) ? q : 0]);
+        if (has_aux_slots(EPI)) {
+          if (!narrow) {
+            xv = __builtin_bit_cast(bf16x8, xa[has_aux_slots(EPI) ? q : 0]);
+          } else if (has_aux) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              xv.v[e] = n + e < g.N ? (u16)__builtin_amdgcn_raw_buffer_load_b16(
+                                          rsX, o[q] == kOOBg ? kOOBg : o[q] + 2u * e, 0, 0)
+                                    : (u16)0;
+          }
+        }
         bf16x8 out, out2;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float a = bf2f(v.v[e]);
           if constexpr (EPI == EPI_STORE) {
-            out.v[e] = has_aux ? f2bf(a + bf2f(xv.v[e])) : v.v[e];
+            float t = has_aux ? a + bf2f(xv.v[e]) : a;
+            if (g.relu) t = fmaxf(t, 0.f);
+            out.v[e] = (has_aux || g.relu) ? f2bf(t) : v.v[e];
           } else if constexpr (EPI == EPI_GELU) {
             out.v[e] = v.v[e];                                 // h (pre-activation)
             out2.v[e] = f2bf(gelu_tanh(a, nullptr));           // gelu of the stored h
@@ -380,10 +396,22 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
             out.v[e] = f2bf(a * d);
           }
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, out), rsC, o[q], 0, 0);
-        if constexpr (EPI == EPI_GELU)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, out2), rsC2, o[q], 0,
+        if (!narrow) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, out), rsC, o[q], 0,
                                                  0);
+          if constexpr (EPI == EPI_GELU)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, out2), rsC2, o[q],
+                                                   0, 0);
+        } else if (o[q] != kOOBg) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            if (n + e < g.N) {
+              __builtin_amdgcn_raw_buffer_store_b16(out.v[e], rsC, o[q] + 2u * e, 0, 0);
+              if constexpr (EPI == EPI_GELU)
+                __builtin_amdgcn_raw_buffer_store_b16(out2.v[e], rsC2, o[q] + 2u * e, 0, 0);
+            }
+          }
+        }
       }
     }
   };
@@ -410,10 +438,12 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
 // Odd shapes the 16-B DMA tiles cannot take (a reduction length or output
 // width that is not a multiple of 8: LeNet's 84-wide layer, 10-class heads)
 // and tiny GEMMs: 64x64 output tile per 256-thread block, 4x4 outputs per
-// thread, k staged through LDS 16 at a time as fp32, same epilogues.
+// thread, k staged through LDS 32 at a time as fp32 with the next stage
+// prefetched into registers, same epilogues.
 template <bool AT, bool BT, int EPI>
 __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
-  __shared__ float As[16][65], Bs[16][65];
+  constexpr int KS = 32;                       // k per LDS stage
+  __shared__ float As[KS][65], Bs[KS][65];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
   const int kbase = blockIdx.z * g.k_chunk;
@@ -421,22 +451,46 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
   const bool do_bias = EPI == EPI_ACC32 && g.dbias != nullptr && blockIdx.y == 0 && tx == 0;
   float acc[4][4] = {};
   float rsum[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = kbase; k0 < kend; k0 += 16) {
+  // a lane's 8 staging elements of each operand: consecutive lanes walk the
+  // operand's contiguous dimension (k for a row-major operand, rows for a
+  // k-strided one); the next stage is fetched into registers while the
+  // current one is multiplied (the loop is load-latency bound otherwise)
+  auto coord = [&](int u, bool t, int& r, int& kk) {
+    const int e = tid + 256 * u;
+    if (t) { r = e & 63; kk = e >> 6; }
+    else { r = e / KS; kk = e % KS; }
+  };
+  float pa[8], pb[8];
+  auto fetch = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + 256 * u, r = e >> 4, kk = e & 15, k = k0 + kk;
-      const int m = m0 + r, n = n0 + r;
-      float av = 0.f, bv = 0.f;
-      if (k < kend && m < g.M)
-        av = bf2f(AT ? g.a[(long long)k * g.lda + m] : g.a[(long long)m * g.lda + k]);
-      if (k < kend && n < g.N)
-        bv = bf2f(BT ? g.b[(long long)k * g.ldb + n] : g.b[(long long)n * g.ldb + k]);
-      As[kk][r] = av;
-      Bs[kk][r] = bv;
+    for (int u = 0; u < 8; ++u) {
+      int r, kk;
+      coord(u, AT, r, kk);
+      const int k = k0 + kk, m = m0 + r;
+      pa[u] = (k < kend && m < g.M)
+                  ? bf2f(AT ? g.a[(long long)k * g.lda + m] : g.a[(long long)m * g.lda + k])
+                  : 0.f;
+      coord(u, BT, r, kk);
+      const int kb = k0 + kk, n = n0 + r;
+      pb[u] = (kb < kend && n < g.N)
+                  ? bf2f(BT ? g.b[(long long)kb * g.ldb + n] : g.b[(long long)n * g.ldb + kb])
+                  : 0.f;
+    }
+  };
+  if (kbase < kend) fetch(kbase);
+  for (int k0 = kbase; k0 < kend; k0 += KS) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      int r, kk;
+      coord(u, AT, r, kk);
+      As[kk][r] = pa[u];
+      coord(u, BT, r, kk);
+      Bs[kk][r] = pb[u];
     }
     __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
+    if (k0 + KS < kend) fetch(k0 + KS);
+#pragma unroll 8
+    for (int kk = 0; kk < KS; ++kk) {
       float a4[4], b4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) a4[i] = As[kk][ty + 16 * i];
@@ -470,7 +524,8 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
         u16* C = reinterpret_cast<u16*>(g.c);
         const float b = (EPI != EPI_DGELU && g.bias != nullptr) ? bf2f(g.bias[n]) : 0.f;
         if constexpr (EPI == EPI_STORE) {
-          C[o] = f2bf(v + b + (g.aux != nullptr ? bf2f(g.aux[o]) : 0.f));
+          const float t = v + b + (g.aux != nullptr ? bf2f(g.aux[o]) : 0.f);
+          C[o] = f2bf(g.relu ? fmaxf(t, 0.f) : t);
         } else if constexpr (EPI == EPI_GELU) {
           const u16 h = f2bf(v + b);
           C[o] = h;
@@ -569,8 +624,9 @@ void gemm_config_info(int cfg, int* info) {
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
-                 hipStream_t s) {
+                 hipStream_t s, bool relu) {
   GemmArgs g{};
+  g.relu = relu ? 1 : 0;
   g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.aux = aux; g.dbias = dbias;
   g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   if (splits < 1 || mode != 2) splits = 1;   // split-K only for the fp32-accumulating pass

@@ -98,7 +98,7 @@ bool conv_wgrad_halo_ok(int cfg, int B, int H, int W, int CI, int CO, int R, int
                         int pad);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int B, int H,
                      int W, int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
-                     int cfg, hipStream_t s, const float* bias = nullptr);
+                     int cfg, hipStream_t s, const float* bias = nullptr, bool relu = false);
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int B, int H, int W,
                        int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s, const uint16_t* addend = nullptr);
@@ -152,7 +152,16 @@ void gemm_config_info(int cfg, int* info);   // {BM, BN, threads, stages, BK}
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
-                 hipStream_t s);
+                 hipStream_t s, bool relu = false);
+
+// im2col.hip: patch matrix [B*OH*OW][Kp] (k = (r, s, ci), zero-padded) and its
+// gather-form inverse; ReLU backward from the saved output
+void launch_im2col(const uint16_t* x, uint16_t* cols, int B, int H, int W, int CI, int OH, int OW,
+                   int R, int S, int stride, int pad, int K, int Kp, hipStream_t st);
+void launch_col2im(const uint16_t* dcols, uint16_t* dx, int B, int H, int W, int CI, int OH,
+                   int OW, int R, int S, int stride, int pad, int Kp, hipStream_t st);
+void launch_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long long n,
+                     hipStream_t st);
 
 // conv.hip: every conv weight of a flat bf16 shadow transposed in one launch
 void launch_conv_weight_transpose_batched(const uint16_t* src, uint16_t* dst,

@@ -135,6 +135,65 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const u16* __restrict_
   }
 }
 
+// Any channel count (C % 8 != 0: LeNet's 6-channel pool): one element per
+// lane, same argmax / gather-form semantics as the 8-wide kernels above.
+__global__ void __launch_bounds__(256) maxpool_fwd_c1_kernel(const u16* __restrict__ x,
+                                                             u16* __restrict__ y,
+                                                             uint8_t* __restrict__ idx, int N,
+                                                             int H, int W, int C, int K, int S,
+                                                             int P, int Ho, int Wo) {
+  const long long total = (long long)N * Ho * Wo * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int c = (int)(t % C);
+    long long r = t / C;
+    const int wo = (int)(r % Wo); r /= Wo;
+    const int ho = (int)(r % Ho);
+    const long long n = r / Ho;
+    float best = -INFINITY;
+    uint8_t bi = 0;
+    const int h0 = ho * S - P, w0 = wo * S - P;
+    for (int i = 0; i < K; ++i) {
+      const int h = h0 + i;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int j = 0; j < K; ++j) {
+        const int w = w0 + j;
+        if ((unsigned)w >= (unsigned)W) continue;
+        const float f = bf2f(x[((n * H + h) * W + w) * C + c]);
+        if (f > best || (f != f)) { best = f; bi = (uint8_t)(i * K + j); }
+      }
+    }
+    y[t] = f2bf(best);
+    idx[t] = bi;
+  }
+}
+
+__global__ void __launch_bounds__(256) maxpool_bwd_c1_kernel(const u16* __restrict__ dy,
+                                                             const uint8_t* __restrict__ idx,
+                                                             u16* __restrict__ dx, int N, int H,
+                                                             int W, int C, int K, int S, int P,
+                                                             int Ho, int Wo) {
+  const long long total = (long long)N * H * W * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int c = (int)(t % C);
+    long long r = t / C;
+    const int w = (int)(r % W); r /= W;
+    const int h = (int)(r % H);
+    const long long n = r / H;
+    const int hlo = max(0, (h + P - K + S) / S), hhi = min(Ho - 1, (h + P) / S);
+    const int wlo = max(0, (w + P - K + S) / S), whi = min(Wo - 1, (w + P) / S);
+    float acc = 0.f;
+    for (int ho = hlo; ho <= hhi; ++ho)
+      for (int wo = wlo; wo <= whi; ++wo) {
+        const uint8_t me = (uint8_t)((h - (ho * S - P)) * K + (w - (wo * S - P)));
+        const long long o = ((n * Ho + ho) * Wo + wo) * C + c;
+        if (idx[o] == me) acc += bf2f(dy[o]);
+      }
+    dx[t] = f2bf(acc);
+  }
+}
+
 void launch_gap_fwd(const u16* x, u16* y, int N, int HW, int C, hipStream_t s) {
   const long long total = (long long)N * (C / 8);
   hipLaunchKernelGGL(gap_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, x, y, N, HW, C);
@@ -150,6 +209,12 @@ int maxpool_out(int H, int K, int S, int P) { return (H + 2 * P - K) / S + 1; }
 void launch_maxpool_fwd(const u16* x, u16* y, uint8_t* idx, int N, int H, int W, int C, int K,
                         int S, int P, hipStream_t s) {
   const int Ho = maxpool_out(H, K, S, P), Wo = maxpool_out(W, K, S, P);
+  if (C % 8) {
+    const long long n1 = (long long)N * Ho * Wo * C;
+    hipLaunchKernelGGL(maxpool_fwd_c1_kernel, dim3(stream_grid(n1, 256)), dim3(256), 0, s, x, y,
+                       idx, N, H, W, C, K, S, P, Ho, Wo);
+    return;
+  }
   const long long total = (long long)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, x, y, idx,
                      N, H, W, C, K, S, P, Ho, Wo);
@@ -158,6 +223,12 @@ void launch_maxpool_fwd(const u16* x, u16* y, uint8_t* idx, int N, int H, int W,
 void launch_maxpool_bwd(const u16* dy, const uint8_t* idx, u16* dx, int N, int H, int W, int C,
                         int K, int S, int P, hipStream_t s) {
   const int Ho = maxpool_out(H, K, S, P), Wo = maxpool_out(W, K, S, P);
+  if (C % 8) {
+    const long long n1 = (long long)N * H * W * C;
+    hipLaunchKernelGGL(maxpool_bwd_c1_kernel, dim3(stream_grid(n1, 256)), dim3(256), 0, s, dy,
+                       idx, dx, N, H, W, C, K, S, P, Ho, Wo);
+    return;
+  }
   const long long total = (long long)N * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy, idx,
                      dx, N, H, W, C, K, S, P, Ho, Wo);

@@ -3,15 +3,19 @@
 Architectures match /root/reference/example/models.py (LeNet :5-23,
 AlexNet :25-49) layer for layer, so parameter counts and the flat ravel order
 are identical (LeNet 62,006 params; AlexNet 2,472,266).  They are built from
-this package's layers so GPU runs go through the native kernels where a
-kernel exists (max-pool, cross-entropy, optimizer) and MIOpen otherwise.
+this package's layers, so every GPU op is a native kernel: the convs (implicit
+GEMM, or patch matrix + MFMA GEMM for AlexNet's 11x11 stem and both LeNet
+convs), the linears (MFMA GEMM), max-pool, dropout, cross-entropy, optimizer;
+each ReLU is fused into the epilogue of the conv / linear that produces its
+input (``L.fuse_relu``; ReLU commutes with max-pool and with dropout's
+non-negative scaling, so LeNet's pool -> ReLU is the same function).
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
+from ..ops import functional as DF
 from ..ops import layers as L
 
 
@@ -30,11 +34,12 @@ class LeNet(nn.Module):
         self.fc3 = L.Linear(84, num_classes)
 
     def forward(self, x):
-        h = F.relu(F.max_pool2d(self.conv1(x), 2))
-        h = F.relu(F.max_pool2d(self.conv2_drop(self.conv2(h)), 2))
+        # relu(pool(c)) == pool(relu(c)); relu(pool(drop(c))) == pool(drop(relu(c)))
+        h = DF.max_pool2d(self.conv1(x, relu=True), 2)
+        h = DF.max_pool2d(self.conv2_drop(self.conv2(h, relu=True)), 2)
         h = torch.flatten(h.contiguous(), 1)
-        h = self.fc1_drop(F.relu(self.fc1(h)))
-        h = F.relu(self.fc2(h))
+        h = self.fc1_drop(self.fc1(h, relu=True))
+        h = self.fc2(h, relu=True)
         return self.fc3(h)
 
 
@@ -62,7 +67,7 @@ class AlexNet(nn.Module):
         self.classifier = L.Linear(256, num_classes)
 
     def forward(self, x):
-        h = self.features(x)
+        h = L.fuse_relu(self.features, x)
         return self.classifier(torch.flatten(h.contiguous(), 1))
 
 
@@ -78,5 +83,5 @@ class MLP(nn.Module):
     def forward(self, x):
         h = torch.flatten(x, 1)
         for lin in self.layers:
-            h = F.relu(lin(h))
+            h = lin(h, relu=True)
         return self.head(h)

@@ -16,7 +16,11 @@ Few-input-channel convolutions (CIFAR-style stems: ``R*S*CI <= 32``,
 ``csrc/conv_small.hip`` with the same fused BN-statistics epilogue and direct
 fp32 arena weight-gradient accumulation.
 
-Everything else goes to ``F.conv2d`` (MIOpen) in channels_last.
+Every other bf16 GPU conv (few input / output channels, large windows:
+AlexNet's 11x11/s4 stem, the LeNet convs, the ResNet-50 7x7 stem) runs as a
+native patch matrix (``csrc/im2col.hip``) on the native MFMA GEMM
+(``csrc/gemm.hip``) with bias / ReLU in its epilogue.  ``F.conv2d`` only for
+CPU / fp32 inputs.
 """
 from __future__ import annotations
 
@@ -153,7 +157,8 @@ def _wgrad_cfg(dy, x, shape, stride, pad):
 
 class _NativeConv(Function):
     @staticmethod
-    def forward(ctx, x, w16, master, stride, pad, want_stats, slots=None, bias=None, alias=False):
+    def forward(ctx, x, w16, master, stride, pad, want_stats, slots=None, bias=None, alias=False,
+                relu=False):
         # the BN-partials output never receives a gradient: do not let autograd
         # materialise (zero-fill) one for it every backward
         ctx.set_materialize_grads(False)
@@ -164,8 +169,9 @@ class _NativeConv(Function):
             if b32.dtype != torch.float32 or not b32.is_contiguous():
                 b32 = b32.float().contiguous()
         ctx.bias = bias
-        y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats, cfg, slots, b32)
-        ctx.save_for_backward(x, w16)
+        y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats, cfg, slots, b32, relu)
+        # ReLU fused in the epilogue; its backward masks dY by the saved output
+        ctx.save_for_backward(x, w16, y if relu else None)
         ctx.master = master
         ctx.geom = (x.shape[2], x.shape[3], stride, pad)
         # alias: x handed back as a third output (a view whose gradient arrives
@@ -181,10 +187,12 @@ class _NativeConv(Function):
     @staticmethod
     def backward(ctx, dy, _dpart, dxa=None):
         if dy is None:
-            return None, None, None, None, None, None, None, None, dxa
-        x, w16 = ctx.saved_tensors
+            return None, None, None, None, None, None, None, None, dxa, None
+        x, w16, y = ctx.saved_tensors
         H, W, stride, pad = ctx.geom
         dy = dy.contiguous(memory_format=torch.channels_last)
+        if y is not None:
+            dy = native().relu_bwd(dy, y)
         dx = None
         master = ctx.master
         if ctx.needs_input_grad[0]:
@@ -229,7 +237,85 @@ class _NativeConv(Function):
                     cb(bias)
             else:
                 gb = dy.sum(dim=(0, 2, 3), dtype=torch.float32).to(bias.dtype)
-        return dx, None, gw, None, None, None, None, gb, None
+        return dx, None, gw, None, None, None, None, gb, None, None
+
+
+def _ceil8(v: int) -> int:
+    return (v + 7) // 8 * 8
+
+
+class _Im2colConv(Function):
+    """Any-geometry conv (few input or output channels, large windows: AlexNet's
+    11x11/s4 stem, the LeNet convs, the ResNet-50 7x7 stem) as a native patch
+    matrix (csrc/im2col.hip) times the weight on the native MFMA GEMM
+    (csrc/gemm.hip): bias / ReLU in the GEMM epilogue, weight (+ bias) gradient
+    fp32-accumulated into the arena by the wgrad GEMM, input gradient = dgrad
+    GEMM into patch space + gather-form col2im.  The patch matrix is kept for
+    the weight gradient (no second im2col)."""
+
+    @staticmethod
+    def forward(ctx, x, w16, master, b16, bias, stride, pad, relu):
+        from .linear import gemm
+
+        B, CI, H, W = x.shape
+        CO, _, R, S = master.shape
+        K = R * S * CI
+        Kp = _ceil8(K)
+        cols = native().im2col(x, R, S, stride, pad, Kp)
+        wmat = w16.permute(0, 2, 3, 1).reshape(CO, K)       # channels_last: [CO][R][S][CI]
+        if Kp != K:
+            wp = torch.zeros(CO, Kp, dtype=w16.dtype, device=w16.device)
+            wp[:, :K] = wmat
+        else:
+            wp = wmat
+        OH = (H + 2 * pad - R) // stride + 1
+        OW = (W + 2 * pad - S) // stride + 1
+        y2 = torch.empty(B * OH * OW, CO, dtype=x.dtype, device=x.device)
+        gemm(0, 0, cols, wp, y2, bias=b16, relu=relu)
+        ctx.save_for_backward(cols, wp, y2 if relu else None)
+        ctx.params = (master, bias)
+        ctx.geom = (B, CI, H, W, R, S, K, stride, pad)
+        return y2.view(B, OH, OW, CO).permute(0, 3, 1, 2)     # channels_last NCHW view
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .linear import _arena_grad, gemm
+        from .functional import _notify
+
+        cols, wp, y2 = ctx.saved_tensors
+        master, bias = ctx.params
+        B, CI, H, W, R, S, K, stride, pad = ctx.geom
+        CO = master.shape[0]
+        dy2 = dy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, CO)
+        if y2 is not None:
+            dy2 = native().relu_bwd(dy2, y2)
+        gw = gb = None
+        wants_w = master is not None and master.requires_grad
+        wants_b = bias is not None and bias.requires_grad
+        g = _arena_grad(master) if wants_w else None
+        gbias = _arena_grad(bias) if wants_b else None
+        tmp_w = wants_w and g is None
+        tmp_b = wants_b and gbias is None
+        if wants_w or wants_b:
+            gmat = (torch.zeros(CO, K, dtype=torch.float32, device=dy.device) if g is None
+                    else g)                                   # [CO, K] view of the arena grad
+            if tmp_b:
+                gbias = torch.zeros(CO, dtype=torch.float32, device=dy.device)
+            gemm(2, 3, dy2, cols[:, :K], gmat, dbias=gbias)
+            if tmp_w:
+                gw = gmat.view(CO, R, S, CI).permute(0, 3, 1, 2).to(master.dtype)
+            elif wants_w:
+                _notify(master)
+            if tmp_b:
+                gb = gbias.to(bias.dtype)
+            elif wants_b:
+                _notify(bias)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dcols = torch.empty(dy2.shape[0], wp.shape[1], dtype=dy2.dtype, device=dy2.device)
+            gemm(1, 0, dy2, wp, dcols)
+            dx = native().col2im(dcols, B, CI, H, W, R, S, stride, pad)
+        return dx, None, gw, None, gb, None, None, None
 
 
 class _SmallConv(Function):
@@ -310,8 +396,18 @@ def native_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
     return ci % 64 == 0 and co % 64 == 0
 
 
+def im2col_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
+    """Any other conv with a bf16 GPU input: patch matrix + native GEMM."""
+    if not (_NATIVE_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+        return False
+    if groups != 1 or _pair(dilation) != (1, 1):
+        return False
+    st, pd = _pair(stride), _pair(padding)
+    return st[0] == st[1] and pd[0] == pd[1] and isinstance(pd[0], int)
+
+
 def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=False,
-           slots=None, alias=False):
+           slots=None, alias=False, relu=False):
     """Returns ``y`` (with BN slot sums attached as ``y._dmp_bn_part`` when ``want_stats``).
 
     ``slots``: the layer's persistent ``[2][64][CO]`` fp32 BN slot buffer (zeroed;
@@ -328,12 +424,13 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
                 w16 = master.detach().to(torch.bfloat16).contiguous(
                     memory_format=torch.channels_last)
             y, part, xa = _NativeConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
-                                            bool(want_stats), slots if want_stats else None, b,
-                                            bool(alias))
+                                            bool(want_stats and not relu),
+                                            slots if want_stats and not relu else None, b,
+                                            bool(alias), bool(relu))
             if part is not None:
                 y._dmp_bn_part = part
             return (y, xa) if alias else y
-        if master is not None and b is None and small_conv_supported(
+        if master is not None and b is None and not relu and small_conv_supported(
                 x, master, stride, padding, dilation, groups):
             w16 = getattr(master, "_dmp_w16", None)
             if w16 is None or not w16.is_contiguous(memory_format=torch.channels_last):
@@ -344,5 +441,24 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
             if part is not None:
                 y._dmp_bn_part = part
             return (y, x) if alias else y
-    y = F.conv2d(x, w, b, stride, padding, dilation, groups)
+        if master is not None and im2col_conv_supported(x, master, stride, padding, dilation,
+                                                        groups):
+            w16 = getattr(master, "_dmp_w16", None)
+            if w16 is None or not w16.is_contiguous(memory_format=torch.channels_last):
+                w16 = master.detach().to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last)
+            b16 = None
+            if b is not None:
+                b16 = getattr(b, "_dmp_w16", None)
+                if b16 is None:
+                    b16 = b.detach().to(torch.bfloat16).contiguous()
+            y = _Im2colConv.apply(x, w16, master, b16, b, _pair(stride)[0], _pair(padding)[0],
+                                  bool(relu))
+            return (y, x) if alias else y
+        if w is None:
+            w = master.to(x.dtype)
+    y = F.conv2d(x, w, b if b is None or b.dtype == x.dtype else b.to(x.dtype), stride, padding,
+                 dilation, groups)
+    if relu:
+        y = F.relu(y)
     return (y, x) if alias else y

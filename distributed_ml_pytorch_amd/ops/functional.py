@@ -222,15 +222,38 @@ class _MaxPool(Function):
 
 
 def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0):
-    """Max pool (floor mode): native NHWC kernel for bf16 GPU input (any
-    window <= 15, stride, padding <= window/2), PyTorch otherwise."""
+    """Max pool (floor mode): native NHWC kernel for bf16 GPU input (any channel
+    count, window <= 15, stride, padding <= window/2), PyTorch otherwise."""
     stride = kernel_size if stride is None else stride
-    if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+    if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and 1 <= kernel_size <= 15 and stride >= 1 and 0 <= 2 * padding <= kernel_size
             and x.shape[2] + 2 * padding >= kernel_size
             and x.shape[3] + 2 * padding >= kernel_size):
         return _MaxPool.apply(x, int(kernel_size), int(stride), int(padding))
     return F.max_pool2d(x, kernel_size, stride, padding)
+
+
+# ----------------------------------------------------------------------- ReLU
+class _ReLU(Function):
+    """Standalone ReLU (where no producing GEMM / conv epilogue can take it):
+    forward and backward on the native mask kernel (csrc/im2col.hip)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        y = native().relu_bwd(x, x)          # x > 0 ? x : 0
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return native().relu_bwd(dy, y)
+
+
+def relu(x):
+    if x.is_cuda and x.dtype == torch.bfloat16:
+        return _ReLU.apply(x)
+    return F.relu(x)
 
 
 # -------------------------------------------------------------------- dropout

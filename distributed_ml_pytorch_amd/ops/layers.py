@@ -12,46 +12,51 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import functional as DF
-from .conv import bn_slot_buffer, conv2d as _conv2d, native_conv_supported, small_conv_supported
+from .conv import (bn_slot_buffer, conv2d as _conv2d, im2col_conv_supported,
+                   native_conv_supported, small_conv_supported)
 from .linear import arena_linear_ok, linear as _arena_linear
 
 
 class Conv2d(nn.Conv2d):
-    """Conv2d on the native NHWC implicit-GEMM kernels when the shape allows.
+    """Conv2d on the native kernels for bf16 GPU input (implicit GEMM / halo
+    tiles, the VALU stem kernel, or patch matrix + MFMA GEMM: ``ops.conv``).
 
     ``emit_bn_stats`` (set by models where a BatchNorm follows) makes the
     native forward also produce the BN partial sums in its epilogue.
+    ``relu=True`` fuses a following ReLU into the epilogue.
     """
 
     emit_bn_stats = False
 
-    def forward(self, x, alias: bool = False):
+    def forward(self, x, alias: bool = False, relu: bool = False):
         """``alias=True`` returns ``(y, x_alias)``: route the block's shortcut
         through ``x_alias`` and its gradient is added in this conv's dgrad."""
-        if (x.is_cuda and (self.bias is None or native_conv_supported(
-                x, self.weight, self.stride, self.padding, self.dilation, self.groups))
-                and (native_conv_supported(x, self.weight, self.stride, self.padding,
-                                           self.dilation, self.groups)
-                     or small_conv_supported(x, self.weight, self.stride, self.padding,
-                                             self.dilation, self.groups))):
-            want = self.emit_bn_stats and self.training
+        if x.is_cuda and x.dtype == torch.bfloat16 and (
+                native_conv_supported(x, self.weight, self.stride, self.padding, self.dilation,
+                                      self.groups)
+                or small_conv_supported(x, self.weight, self.stride, self.padding,
+                                        self.dilation, self.groups)
+                or im2col_conv_supported(x, self.weight, self.stride, self.padding,
+                                         self.dilation, self.groups)):
+            want = self.emit_bn_stats and self.training and not relu
             slots = bn_slot_buffer(self, "_dmp_slots", self.out_channels, x.device) if want else None
             return _conv2d(x, None, self.bias, self.stride, self.padding, self.dilation,
                            self.groups, master=self.weight, want_stats=want, slots=slots,
-                           alias=alias)
+                           alias=alias, relu=relu)
         w = DF.compute_weight(self.weight, x.dtype)
         b = DF.compute_weight(self.bias, x.dtype)
         return _conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups,
-                       alias=alias)
+                       alias=alias, relu=relu)
 
 
 class Linear(nn.Linear):
-    def forward(self, x):
+    def forward(self, x, relu: bool = False):
         if arena_linear_ok(x, self.weight, self.bias):
-            return _arena_linear(x, self.weight, self.bias)
+            return _arena_linear(x, self.weight, self.bias, relu)
         w = DF.compute_weight(self.weight, x.dtype)
         b = DF.compute_weight(self.bias, x.dtype)
-        return F.linear(x, w, b)
+        y = F.linear(x, w, b)
+        return DF.relu(y) if relu else y
 
 
 def _bn_slots(mod, x):
@@ -113,7 +118,29 @@ class GlobalAvgPool(nn.Module):
 
 
 class ReLU(nn.ReLU):
-    pass
+    """ReLU on the native mask kernel for bf16 GPU tensors (models fuse it into
+    the producing conv / linear epilogue where they can: ``fuse_relu``)."""
+
+    def forward(self, x):
+        return DF.relu(x)
+
+
+def fuse_relu(seq, x):
+    """Run an nn.Sequential, folding every ReLU that directly follows a Conv2d /
+    Linear of this package into that layer's epilogue (the ReLU modules stay in
+    the Sequential, so parameter names and state_dict keys are unchanged)."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        nxt = mods[i + 1] if i + 1 < len(mods) else None
+        if isinstance(m, (Conv2d, Linear)) and isinstance(nxt, nn.ReLU):
+            x = m(x, relu=True)
+            i += 2
+            continue
+        x = m(x)
+        i += 1
+    return x
 
 
 class _DropoutBase(nn.Module):

@@ -67,27 +67,66 @@ def _mfma_ok(mode: int, M: int, N: int, K: int, *mats) -> bool:
             continue
         if t.stride(-1) != 1 or t.data_ptr() % 16 or (t.shape[0] > 1 and t.stride(0) % 8):
             return False
-    if mode in (0, 1):
-        return K % 8 == 0 and N % 8 == 0
-    return M % 8 == 0 and N % 8 == 0
+    a, b = mats[0], mats[1]
+    c8 = lambda v: (v + 7) // 8 * 8                      # noqa: E731
+    if mode == 0:
+        return K % 8 == 0
+    if mode == 1:
+        return K % 8 == 0 and (N % 8 == 0 or b.stride(0) >= c8(N))
+    return ((M % 8 == 0 or a.stride(0) >= c8(M))          # pieces may run into row padding
+            and (N % 8 == 0 or b.stride(0) >= c8(N)))
+
+
+# candidate encoding: (cfg + 1) * 1024 + splits (cfg -1 = any-shape kernel);
+# _BLAS < 0; the tuner's "no pick" is -1
+def _enc(cfg: int, splits: int) -> int:
+    return (cfg + 1) * 1024 + splits
+
+
+def _dec(e: int):
+    return e // 1024 - 1, e % 1024
+
+
+def _wgrad_splits(M: int, N: int, K: int, bm: int, bn: int):
+    """Split-K counts worth timing for an fp32-accumulating weight gradient:
+    enough blocks to fill the chip (a conv stem's 64 x 147 output over 1.6M
+    pixels is 2 tiles), at least 256 reduction rows per split."""
+    tiles = -(-M // bm) * -(-N // bn)
+    out = []
+    for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512):
+        if s > 1 and K < 256 * s:
+            break
+        if s == 1 or tiles * s <= 2048:
+            out.append(s)
+    # keep the few counts around "one block per CU" plus the unsplit one
+    if len(out) > 6:
+        best = min(out, key=lambda s: abs(tiles * s - 384))
+        i = out.index(best)
+        out = sorted({1, *out[max(0, i - 2):i + 3]})
+    return out
+
+
+def _small_splits(mode: int, K: int) -> int:
+    """Split-K of the any-shape kernel in wgrad mode: its blocks cover only a
+    64x64 output tile, so a long reduction (a conv's B*OH*OW pixels) must be
+    spread over blocks (fp32 atomics), ~256 rows each."""
+    return max(1, min(1023, K // 256)) if mode == 2 else 1
 
 
 def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bool):
     if not ok:
-        return [_SMALL * 16 + 1]
+        return [_enc(_SMALL, _small_splits(mode, K))]
     cands = []
     for c in native().gemm_configs():
-        cid = c[0]
+        cid, bm, bn = c[0], c[1], c[2]
         if not native().gemm_config_ok(mode, cid):
             continue
         if mode == 2:
-            for s in (1, 2, 3, 4, 6, 8):
-                if s == 1 or K >= 256 * s:
-                    cands.append(cid * 16 + s)
+            cands += [_enc(cid, s) for s in _wgrad_splits(M, N, K, bm, bn)]
         else:
-            cands.append(cid * 16 + 1)
+            cands.append(_enc(cid, 1))
     if M * N * K < (1 << 22):
-        cands.append(_SMALL * 16 + 1)
+        cands.append(_enc(_SMALL, _small_splits(mode, K)))
     if _GEMM_MODE == "auto" and plain and mode in (0, 1):
         cands.append(_BLAS)
     return cands
@@ -96,10 +135,10 @@ def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bo
 def _default(mode: int, M: int, N: int, K: int, ok: bool) -> int:
     """Heuristic pick when tuning is off or a graph is being captured."""
     if not ok:
-        return _SMALL * 16 + 1
+        return _enc(_SMALL, _small_splits(mode, K))
     if mode == 2:
-        return 4 * 16 + (4 if K >= 4096 else 1)
-    return 4 * 16 + 1
+        return _enc(4, _wgrad_splits(M, N, K, 128, 128)[-1])
+    return _enc(4, 1)
 
 
 def _blas(mode, a, b, c, bias):
@@ -112,7 +151,7 @@ def _blas(mode, a, b, c, bias):
         torch.mm(a, b, out=c)
 
 
-def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None):
+def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None, relu=False):
     """C = epilogue(A(m,k) B(n,k)) on the native kernels (see csrc/gemm.hip):
     mode 0 fwd (a [M,K], b [N,K]), 1 dgrad (a [M,K], b [K,N]), 2 wgrad (a [K,M],
     b [K,N], fp32 c accumulated); epi 0 store(+bias,+aux), 1 GELU, 2 x gelu'(aux),
@@ -121,9 +160,11 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None)
     K = a.shape[0] if mode == 2 else a.shape[1]
     if M == 0 or N == 0:
         return
-    ok = _mfma_ok(mode, M, N, K, a, b, c, c2, aux)
-    plain = epi == 0 and aux is None
-    key = ("gemm", mode, epi, M, N, K, bias is not None, aux is not None, dbias is not None)
+    # outputs / aux of any row stride: the epilogues fall back to element access
+    ok = _mfma_ok(mode, M, N, K, a, b)
+    plain = epi == 0 and aux is None and not relu
+    key = ("gemm", mode, epi, M, N, K, bias is not None, aux is not None, dbias is not None,
+           bool(relu))
     pick = TUNER.cache.get(key)
     if pick is None:
         cands = _candidates(mode, epi, M, N, K, plain, ok)
@@ -140,16 +181,16 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None)
                 if e == _BLAS:
                     _blas(mode, a, b, cs, bias)
                 else:
-                    native().gemm(mode, epi, e // 16 if e >= 0 else _SMALL, a, b, cs, c2, bias,
-                                  aux, ds, e % 16 if e >= 0 else 1)
+                    cfg_e, split_e = _dec(e)
+                    native().gemm(mode, epi, cfg_e, a, b, cs, c2, bias, aux, ds, split_e, relu)
             pick = TUNER.best(key, run, cands)
             if pick == -1:
                 pick = _default(mode, M, N, K, ok)
     if pick == _BLAS:
         _blas(mode, a, b, c, bias)
         return
-    cfg, splits = (pick // 16, pick % 16) if pick >= 0 else (_SMALL, 1)
-    native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits)
+    cfg, splits = _dec(pick)
+    native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits, relu)
 
 
 def _rows(t, k):
@@ -203,29 +244,31 @@ def _weight_grads(dy2, x2, w, b):
 
 class _ArenaLinear(Function):
     @staticmethod
-    def forward(ctx, x, w16, b16, w, b):
+    def forward(ctx, x, w16, b16, w, b, relu=False):
         N, K = w16.shape
         x2 = _rows(x, K)
         y = torch.empty(x2.shape[0], N, dtype=x.dtype, device=x.device)
-        gemm(0, 0, x2, w16, y, bias=b16)
-        ctx.save_for_backward(x2, w16)
+        gemm(0, 0, x2, w16, y, bias=b16, relu=relu)      # ReLU fused in the epilogue
+        ctx.save_for_backward(x2, w16, y if relu else None)
         ctx.params = (w, b)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w16 = ctx.saved_tensors
+        x2, w16, y = ctx.saved_tensors
         w, b = ctx.params
         N, K = w16.shape
         dy2 = _rows(dy, N)
+        if y is not None:
+            dy2 = native().relu_bwd(dy2, y)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(dy2.shape[0], K, dtype=dy.dtype, device=dy.device)
             gemm(1, 0, dy2, w16, dx)
             dx = dx.view(ctx.xshape)
         gw, gb = _weight_grads(dy2, x2, w, b)
-        return dx, None, None, gw, gb
+        return dx, None, None, gw, gb, None
 
 
 def arena_linear_ok(x, w, b) -> bool:
@@ -238,10 +281,10 @@ def arena_linear_ok(x, w, b) -> bool:
     return b is None or getattr(b, "_dmp_w16", None) is not None
 
 
-def linear(x, w, b):
+def linear(x, w, b, relu: bool = False):
     w16 = w._dmp_w16
     b16 = b._dmp_w16 if b is not None else None
-    return _ArenaLinear.apply(x, w16, b16, w, b)
+    return _ArenaLinear.apply(x, w16, b16, w, b, bool(relu))
 
 
 # ------------------------------------------------------------ fused ViT MLP

@@ -1,0 +1,116 @@
+"""Native coverage of the reference's own models: patch-matrix convs (any CI /
+CO / window / stride, bias + fused ReLU), any-channel max-pool, native ReLU --
+each vs a plain fp32 PyTorch oracle on the same bf16 operands."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+@pytest.mark.parametrize("B,CI,H,CO,k,st,pd,bias,relu,xgrad", [
+    (16, 3, 32, 64, 11, 4, 5, True, True, False),    # AlexNet conv1
+    (16, 3, 32, 6, 5, 1, 0, True, True, False),      # LeNet conv1
+    (16, 6, 14, 16, 5, 1, 0, True, True, True),      # LeNet conv2 (input grad: col2im)
+    (4, 3, 64, 64, 7, 2, 3, False, False, False),    # ResNet-50 stem geometry
+    (8, 5, 9, 24, 3, 2, 1, True, False, True),       # odd everything
+])
+def test_im2col_conv_matches_fp32(B, CI, H, CO, k, st, pd, bias, relu, xgrad):
+    from distributed_ml_pytorch_amd.ops import layers as L
+    from distributed_ml_pytorch_amd.ops.conv import native_conv_supported
+    from distributed_ml_pytorch_amd.parallel.arena import FlatArena
+
+    torch.manual_seed(0)
+    conv = L.Conv2d(CI, CO, k, stride=st, padding=pd, bias=bias).cuda()
+    FlatArena(conv, device="cuda")
+    x = torch.randn(B, CI, H, H, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_(xgrad)
+    assert not native_conv_supported(x, conv.weight, st, pd, 1, 1)
+    y = conv(x, relu=relu)
+    c = torch.randn_like(y, dtype=torch.float32)
+    (y.float() * c).sum().backward()
+    w = conv.weight._dmp_w16.float().detach().requires_grad_(True)
+    b = conv.bias._dmp_w16.float().detach().requires_grad_(True) if bias else None
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, w, b, stride=st, padding=pd)
+    if relu:
+        yr = F.relu(yr)
+    (yr * c).sum().backward()
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 1e-2
+    assert _rel(conv.weight.grad, w.grad) < 1e-2
+    if bias:
+        assert _rel(conv.bias.grad, b.grad) < 1e-2
+    if xgrad:
+        assert _rel(x.grad, xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("C", [6, 16, 3])
+def test_maxpool_any_channels(C):
+    from distributed_ml_pytorch_amd.ops import functional as DF
+
+    torch.manual_seed(1)
+    x = torch.randn(4, C, 14, 14, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = DF.max_pool2d(x, 2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 2)
+    yr.backward(g.float())
+    torch.testing.assert_close(y.float(), yr)
+    torch.testing.assert_close(x.grad.float(), xr.grad)
+
+
+def test_native_relu():
+    from distributed_ml_pytorch_amd.ops import functional as DF
+
+    x = torch.randn(1000, 37, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    y = DF.relu(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    torch.testing.assert_close(y, torch.relu(x.detach()))
+    torch.testing.assert_close(x.grad, torch.where(x.detach() > 0, g, torch.zeros_like(g)))
+
+
+@pytest.mark.parametrize("name", ["lenet", "alexnet", "mlp"])
+def test_reference_models_step_matches_fp32(name):
+    """One training step of the reference models through the native kernels vs
+    the same model (same bf16-rounded weights) in fp32 PyTorch.  bf16
+    activations legitimately move the result (max-pool ties, rounding through 5
+    layers), so the oracle is relative: our error vs fp32 must stay within 2x
+    (+1e-2) of stock PyTorch's own bf16 error vs fp32 on the same step."""
+    import copy
+
+    from distributed_ml_pytorch_amd.models import build_model
+    from distributed_ml_pytorch_amd.parallel.arena import FlatArena
+
+    torch.manual_seed(2)
+    model, _, _ = build_model(name)
+    ref = copy.deepcopy(model).cuda().float()
+    model = model.cuda()
+    FlatArena(model, device="cuda")
+    for m in (model, ref):
+        m.eval() if name == "lenet" else m.train()      # LeNet: dropout off for parity
+    with torch.no_grad():
+        for p, q in zip(model.parameters(), ref.parameters()):
+            q.copy_(p._dmp_w16.float().view_as(q))
+    stock = copy.deepcopy(ref).to(torch.bfloat16)        # stock ATen / MIOpen in bf16
+    x = torch.randn(64, 784, device="cuda") if name == "mlp" else torch.randn(
+        64, 3, 32, 32, device="cuda")
+    x16 = x.to(torch.bfloat16)
+    y = torch.randint(0, 10, (64,), device="cuda")
+    losses = []
+    with torch.enable_grad():
+        for m, inp in ((model, x16), (ref, x16.float()), (stock, x16)):
+            loss = F.cross_entropy(m(inp).float(), y)
+            loss.backward()
+            losses.append(float(loss))
+    assert abs(losses[0] - losses[1]) <= 2 * abs(losses[2] - losses[1]) + 1e-2
+    for (n, p), q, r in zip(model.named_parameters(), ref.parameters(), stock.parameters()):
+        ours, theirs = _rel(p.grad, q.grad), _rel(r.grad, q.grad)
+        assert ours <= 2 * theirs + 1e-2, (n, ours, theirs)
