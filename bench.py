@@ -76,11 +76,12 @@ def parse(argv=None):
                     help="after the throughput run: train a FRESH model on learnable synthetic "
                          "data until the mean loss of 10 steps <= target and report the "
                          "wall time (the metric's time-to-target-loss half); 0 skips")
-    ap.add_argument("--ttl-max-steps", type=int, default=3000)
-    ap.add_argument("--ttl-signal", type=float, default=0.5,
-                    help="class-template amplitude of the time-to-target images")
-    ap.add_argument("--ttl-batches", type=int, default=32, help="distinct TTL batches per rank")
-    ap.add_argument("--ttl-compare-sync", type=int, default=0,
+    ap.add_argument("--ttl-max-steps", type=int, default=4000)
+    ap.add_argument("--ttl-signal", type=float, default=0.05,
+                    help="class-template amplitude of the time-to-target images (0.05: ~1000 "
+                         "steps to loss 0.5 at N=1, profiles/ttl_calibration_r2.txt)")
+    ap.add_argument("--ttl-batches", type=int, default=128, help="distinct TTL batches per rank")
+    ap.add_argument("--ttl-compare-sync", type=int, default=1,
                     help="also measure time-to-target of sync all-reduce DP at the same N")
     return ap.parse_args(argv)
 
@@ -210,8 +211,7 @@ def time_to_target(a, cfg, ctx, mode=None):
     cfg = replace(cfg, mode=mode or cfg.mode, seed=1000)
     torch.manual_seed(1000 + info.rank)
     w = Worker(cfg, info, ctx.ps_groups)
-    if cfg.mode != "sync":
-        w.enable_graph(bool(a.graph))
+    w.enable_graph(bool(a.graph))
     pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device,
                            n_batches=a.ttl_batches, dtype=w.compute_dtype,
                            seed=100 + info.rank, learnable=True, signal=a.ttl_signal)
@@ -271,11 +271,12 @@ def run(a):
         dev_name = str(info.device)
     else:
         w = Worker(cfg, info, ctx.ps_groups)
-        graphed = w.enable_graph(bool(a.graph)) if a.mode != "sync" else False
+        graphed = w.enable_graph(bool(a.graph))
         pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device, n_batches=4,
                                dtype=w.compute_dtype, seed=info.rank)
         elapsed, loss = _timed_steps(w, pool, a.steps, a.warmup, ctx)
         final_loss = float(loss.float().item())
+        graphed = bool(getattr(w, "use_graph", False) and w.graph is not None)
         res["phases_host_ms"] = {k: v["mean_ms"] for k, v in w.timer.summary().items()}
         for _ in range(a.profile_steps):
             x, y = pool.next()

@@ -60,6 +60,10 @@ class BucketedAllReduce:
         self.works = [None] * len(self.buckets)
         self.seen = set()
 
+    def reset(self):
+        """Forget launched-but-unwaited buckets (after an aborted step / capture)."""
+        self._reset()
+
     def _launch(self, b: int):
         if self.works[b] is not None or (self.world == 1 and not self.force):
             return

@@ -168,10 +168,19 @@ class Worker:
         """Replay forward+backward+fused update as ONE captured hipGraph per step.
 
         The push/pull/land half of the ASGD step (which depends on the step
-        index) stays eager between replays.  Not used for sync-DP (its RCCL
-        bucket all-reduces fire from inside backward).
+        index) stays eager between replays.  Sync DP is captured whole: the
+        bucket all-reduces that the grad-ready hooks launch during backward
+        (RCCL on the comm stream, ordered by events) and the wait before the
+        update are part of the graph.  Gloo collectives cannot be captured:
+        sync DP over gloo stays eager.
         """
-        self.use_graph = bool(enabled) and self.device.type == "cuda" and self.ddp is None
+        can = self.device.type == "cuda"
+        if self.ddp is not None and self.info.is_distributed:
+            # gloo collectives cannot be captured; RCCL ones can, but capturing
+            # them at N > 1 is opt-in (DMP_GRAPH_SYNC=1) until measured on a
+            # multi-GPU node -- eager bucket all-reduces otherwise
+            can = can and self.info.backend == "nccl" and os.environ.get("DMP_GRAPH_SYNC") == "1"
+        self.use_graph = bool(enabled) and can
         self.graph = None
         return self.use_graph
 
@@ -180,6 +189,8 @@ class Worker:
         logits = self.model(self._gx)
         loss, hits = softmax_cross_entropy(logits, self._gy, self.cfg.label_smoothing)
         loss.backward()
+        if self.ddp is not None:
+            self.ddp.synchronize()
         self.opt.local_step()
         return loss.detach(), hits
 
@@ -196,9 +207,17 @@ class Worker:
             self.step_idx += 1
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        # thread_local: RCCL's watchdog thread queries events while we capture
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            self._gloss, self._ghits = self._graph_body()
+        try:
+            # thread_local: RCCL's watchdog thread queries events while we capture
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._gloss, self._ghits = self._graph_body()
+        except RuntimeError as e:     # e.g. a collective backend that cannot be captured
+            if self.ddp is not None:
+                self.ddp.reset()
+            print(f"[trainer] hipGraph capture failed ({e}); stepping eagerly", flush=True)
+            self.use_graph = False
+            self.graph = None
+            return loss.clone(), hits.clone()
         self.graph = g
         self._graph_key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
         return loss.clone(), hits.clone()

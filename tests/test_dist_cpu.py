@@ -135,7 +135,7 @@ def test_sharded_ps_collective_push_pull():
 
 
 # ----------------------------------------------------------------- sync DP
-def _ddp(rank, world):
+def _ddp(rank, world, bucket_mb=0.25, steps=1, momentum=0.0):
     from distributed_ml_pytorch_amd.models import build_model
     from distributed_ml_pytorch_amd.parallel.arena import attach_arena
     from distributed_ml_pytorch_amd.parallel.ddp import BucketedAllReduce, FusedSGD
@@ -143,23 +143,26 @@ def _ddp(rank, world):
     torch.manual_seed(0)
     m, _, _ = build_model("mlp")
     arena = attach_arena(m, shadow_dtype=None)
-    ddp = BucketedAllReduce(arena, bucket_mb=0.25)
-    opt = FusedSGD(list(m.parameters()), arena, lr=0.1, grad_scale=1.0 / world)
+    ddp = BucketedAllReduce(arena, bucket_mb=bucket_mb)
+    opt = FusedSGD(list(m.parameters()), arena, lr=0.1, momentum=momentum,
+                   grad_scale=1.0 / world)
     g = torch.Generator().manual_seed(7)
-    xs = torch.randn(8 * world, 1, 28, 28, generator=g)
-    ys = torch.randint(0, 10, (8 * world,), generator=g)
-    x, y = xs[rank * 8:(rank + 1) * 8], ys[rank * 8:(rank + 1) * 8]
-    opt.zero_grad()
-    torch.nn.functional.cross_entropy(m(x), y).backward()
-    ddp.synchronize()
-    opt.step()
-    # single-process oracle on the full batch
+    batches = [(torch.randn(8 * world, 1, 28, 28, generator=g),
+                torch.randint(0, 10, (8 * world,), generator=g)) for _ in range(steps)]
+    for xs, ys in batches:
+        x, y = xs[rank * 8:(rank + 1) * 8], ys[rank * 8:(rank + 1) * 8]
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        ddp.synchronize()
+        opt.step()
+    # single-process oracle: stock torch.optim.SGD on the full batch
     torch.manual_seed(0)
     ref, _, _ = build_model("mlp")
-    torch.nn.functional.cross_entropy(ref(xs), ys).backward()
-    with torch.no_grad():
-        for p in ref.parameters():
-            p -= 0.1 * p.grad
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=momentum)
+    for xs, ys in batches:
+        ropt.zero_grad()
+        torch.nn.functional.cross_entropy(ref(xs), ys).backward()
+        ropt.step()
     got = arena.ravel()
     exp = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
     return {"err": float((got - exp).abs().max()), "buckets": ddp.num_buckets}
@@ -170,6 +173,17 @@ def test_bucketed_allreduce_matches_full_batch_sgd():
     for r, res in out.items():
         assert res["err"] < 1e-5, (r, res)
         assert res["buckets"] >= 2          # 0.25 MB buckets -> several per 2 MB model
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("bucket_mb", [0.1, 4.0])
+def test_bucketed_allreduce_4ranks_momentum_matches_full_batch(bucket_mb):
+    """4 gloo ranks, several steps with momentum, many small buckets vs one
+    bucket: identical to single-process SGD on the concatenated batch."""
+    out = _run(_ddp, 4, bucket_mb, 3, 0.9)
+    for r, res in out.items():
+        assert res["err"] < 2e-5, (r, res)
+        assert (res["buckets"] >= 3) == (bucket_mb < 1), res
 
 
 # --------------------------------------------------------------- messaging
