@@ -149,7 +149,9 @@ std::vector<Tensor> softmax_xent(Tensor logits, Tensor labels, bool want_grad, d
   auto row_hit = at::empty({B}, logits.options().dtype(at::kInt));
   Tensor dlogits;
   if (want_grad) dlogits = at::empty_like(logits);
-  const float grad_scale = 1.f / (float)std::max(B, 1);
+  // <= 0: the kernels count the non-ignored rows on device and scale the
+  // gradient by 1/#valid (the mean the reported loss uses)
+  const float grad_scale = -1.f;
   if (logits.scalar_type() == at::kBFloat16) {
     dmp::launch_softmax_xent_bf16(
         reinterpret_cast<const uint16_t*>(logits.data_ptr()), labels.data_ptr<int64_t>(),

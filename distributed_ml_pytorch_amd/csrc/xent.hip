@@ -5,8 +5,10 @@
 // -> _log_softmax_backward_data -> max that the reference runs per iteration
 // (/root/reference/example/main.py:71-75; op trace in SURVEY.md §2.3).
 //
-// dlogits = (softmax(x) - onehot(y)) * grad_scale  where grad_scale = 1/B for a
-// mean-reduced loss; the autograd wrapper rescales by the incoming grad_output.
+// dlogits = (softmax(x) - onehot(y)) * grad_scale  where grad_scale = 1/#valid
+// rows (grad_scale <= 0: counted on device) for the loss averaged over the
+// rows whose label is not ignore_index; the autograd wrapper rescales by the
+// incoming grad_output.
 #include "common.h"
 
 namespace dmp {
@@ -25,6 +27,28 @@ __device__ __forceinline__ void st<float>(float* p, long long i, float v) { p[i]
 template <>
 __device__ __forceinline__ void st<u16>(u16* p, long long i, float v) { p[i] = f2bf(v); }
 
+// Labels outside [0, C) are treated like ignore_index (no out-of-bounds read).
+__device__ __forceinline__ bool label_ok(long long y, int C, int ignore_index) {
+  return y != ignore_index && y >= 0 && y < C;
+}
+
+// 1 / (number of non-ignored labels), counted by every block over all B labels
+// (B <= a few thousand int64: cheaper than a separate pass): the gradient of a
+// mean over the valid rows, exactly as F.cross_entropy(ignore_index=...).
+__device__ float valid_grad_scale(const int64_t* __restrict__ labels, int B, int C,
+                                  int ignore_index) {
+  __shared__ int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  int c = 0;
+  for (int r = threadIdx.x; r < B; r += blockDim.x) c += label_ok(labels[r], C, ignore_index);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&cnt, c);
+  __syncthreads();
+  return 1.f / (float)max(cnt, 1);
+}
+
 // Phase 1: rows [blockIdx.x*rows_per_block, ...). Each wave owns one row at a time.
 // If `fused_finalize` (grid == 1) the same block reduces the row results.
 template <typename T>
@@ -38,12 +62,13 @@ __global__ void __launch_bounds__(1024) softmax_xent_kernel(
   const int nw = blockDim.x >> 6;
   const int r_begin = blockIdx.x * rows_per_block;
   const int r_end = min(B, r_begin + rows_per_block);
+  if (grad_scale <= 0.f) grad_scale = valid_grad_scale(labels, B, C, ignore_index);
   float my_loss = 0.f;
   int my_hit = 0, my_valid = 0;
   for (int r = r_begin + wid; r < r_end; r += nw) {
     const T* x = logits + (long long)r * C;
     const long long y = labels[r];
-    const bool valid = (y != ignore_index);
+    const bool valid = label_ok(y, C, ignore_index);
     // pass 1: max + argmax
     float m = -INFINITY;
     int am = 0x7fffffff;
@@ -120,12 +145,13 @@ __global__ void __launch_bounds__(1024) softmax_xent_narrow_kernel(
     int ignore_index) {
   constexpr int CMAX = 32;
   const float eps = label_smoothing, smooth = eps / (float)C;
+  if (grad_scale <= 0.f) grad_scale = valid_grad_scale(labels, B, C, ignore_index);
   float my_loss = 0.f;
   int my_hit = 0, my_valid = 0;
   for (int r = threadIdx.x; r < B; r += blockDim.x) {
     const T* x = logits + (long long)r * C;
     const long long y = labels[r];
-    const bool valid = (y != ignore_index);
+    const bool valid = label_ok(y, C, ignore_index);
     float v[CMAX];
 #pragma unroll
     for (int j = 0; j < CMAX; ++j) v[j] = j < C ? ld(x, j) : -INFINITY;
@@ -185,12 +211,12 @@ __global__ void __launch_bounds__(1024) softmax_xent_narrow_kernel(
 __global__ void __launch_bounds__(1024) xent_finalize_kernel(
     const float* __restrict__ row_loss, const int* __restrict__ row_hit,
     const int64_t* __restrict__ labels, float* __restrict__ loss_out, int* __restrict__ hits_out,
-    int B, int ignore_index) {
+    int B, int C, int ignore_index) {
   __shared__ float sl[16];
   __shared__ int sh[16], sv[16];
   float l = 0.f; int h = 0, v = 0;
   for (int r = threadIdx.x; r < B; r += blockDim.x) {
-    l += row_loss[r]; h += row_hit[r]; v += (labels[r] != ignore_index) ? 1 : 0;
+    l += row_loss[r]; h += row_hit[r]; v += label_ok(labels[r], C, ignore_index) ? 1 : 0;
   }
   l = wave_sum(l);
 #pragma unroll
@@ -230,7 +256,7 @@ void launch_xent_t(const T* logits, const int64_t* labels, T* dlogits, float* ro
                      dlogits, row_loss, row_hit, loss_out, hits_out, B, C, grad_scale, smoothing,
                      ignore_index, rows_per_block, 0);
   hipLaunchKernelGGL(xent_finalize_kernel, dim3(1), dim3(1024), 0, s, row_loss, row_hit, labels,
-                     loss_out, hits_out, B, ignore_index);
+                     loss_out, hits_out, B, C, ignore_index);
 }
 
 void launch_softmax_xent_bf16(const u16* logits, const int64_t* labels, u16* dlogits,

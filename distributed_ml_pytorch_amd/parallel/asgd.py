@@ -67,6 +67,7 @@ class Asynchronous(Optimizer):
                              "(the push/pull vector is the whole model, as in the reference)")
         dev = arena.device
         self.acc = torch.zeros(arena.numel, dtype=torch.float32, device=dev)
+        self._mom_steps = 0
         self.mom = torch.zeros_like(self.acc) if momentum else None
         self.idx = 0
         self.timer = _NO_TIMER      # a utils.metrics.StepTimer when the trainer wires one
@@ -93,17 +94,21 @@ class Asynchronous(Optimizer):
     def _local_update(self, lr: float):
         g = self.param_groups[0]
         a = self.arena
+        # torch.optim.SGD seeds the momentum buffer with the first gradient
+        # (no dampening); the buffer starts at zero, so dampening 0 on the
+        # first update gives exactly that
+        damp = g["dampening"] if self._mom_steps > 0 else 0.0
+        self._mom_steps += 1
         if self._nat is not None:
             self._nat.asgd_fused_step(a.g32, a.p32, self.acc, self.mom, a.w16, lr,
-                                      g["weight_decay"], g["momentum"], g["dampening"],
-                                      g["nesterov"])
+                                      g["weight_decay"], g["momentum"], damp, g["nesterov"])
             return
         with torch.no_grad():
             d = a.g32
             if g["weight_decay"]:
                 d = d + g["weight_decay"] * a.p32
             if self.mom is not None:
-                self.mom.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
+                self.mom.mul_(g["momentum"]).add_(d, alpha=1 - damp)
                 d = d + g["momentum"] * self.mom if g["nesterov"] else self.mom
             self.acc.add_(d, alpha=-lr)
             a.p32.add_(d, alpha=-lr)

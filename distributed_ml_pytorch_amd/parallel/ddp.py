@@ -109,6 +109,7 @@ class FusedSGD(Optimizer):
         self.arena = arena
         self.grad_scale = grad_scale
         self.mom = torch.zeros_like(arena.p32) if momentum else None
+        self._mom_steps = 0
         self._nat = None
         if arena.device.type == "cuda":
             from ..ops._ext import native
@@ -147,15 +148,18 @@ class FusedSGD(Optimizer):
             # momentum must see the averaged gradient: scale grads explicitly
             a.g32.mul_(self.grad_scale)
             lr_eff, wd_eff = lr, g["weight_decay"]
+        # first update: momentum buffer = gradient, as torch.optim.SGD (no dampening)
+        damp = g["dampening"] if self._mom_steps > 0 else 0.0
+        self._mom_steps += 1
         if self._nat is not None:
             self._nat.asgd_fused_step(a.g32, a.p32, None, self.mom, a.w16, lr_eff, wd_eff,
-                                      g["momentum"], g["dampening"], g["nesterov"])
+                                      g["momentum"], damp, g["nesterov"])
         else:
             d = a.g32
             if wd_eff:
                 d = d + wd_eff * a.p32
             if self.mom is not None:
-                self.mom.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
+                self.mom.mul_(g["momentum"]).add_(d, alpha=1 - damp)
                 d = d + g["momentum"] * self.mom if g["nesterov"] else self.mom
             a.p32.add_(d, alpha=-lr_eff)
             if a.w16 is not None:

@@ -100,6 +100,7 @@ def load_worker_optimizer(path: str, optimizer) -> None:
                 optimizer.acc.copy_(o["acc"])
             if o.get("mom") is not None and getattr(optimizer, "mom", None) is not None:
                 optimizer.mom.copy_(o["mom"])
+                optimizer._mom_steps = max(1, int(o.get("idx", 1)))   # buffer already seeded
     client = getattr(optimizer, "client", None)
     if client is not None and sd.get("client"):
         client.load_state_dict(sd["client"])

@@ -202,3 +202,30 @@ def test_cifar_binary_reader(tmp_path):
     assert src == "cifar10" and len(tr) == 20 and len(te) == 4
     x, y = tr[0]
     assert x.shape == (3, 32, 32) and -1.0 <= float(x.min()) and float(x.max()) <= 1.0
+
+
+def test_fused_sgd_dampening_matches_torch_sgd():
+    """Momentum with dampening: the first update seeds the buffer with the raw
+    gradient, as torch.optim.SGD does (the zero-initialised buffer
+    scaled step 1 by (1 - dampening))."""
+    import torch.nn as nn
+
+    from distributed_ml_pytorch_amd.parallel.arena import attach_arena
+    from distributed_ml_pytorch_amd.parallel.ddp import FusedSGD
+
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(6, 5), nn.Tanh(), nn.Linear(5, 3))
+    ref = nn.Sequential(nn.Linear(6, 5), nn.Tanh(), nn.Linear(5, 3))
+    ref.load_state_dict(m.state_dict())
+    arena = attach_arena(m, shadow_dtype=None)
+    opt = FusedSGD(list(m.parameters()), arena, lr=0.1, momentum=0.9, dampening=0.3)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9, dampening=0.3)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(4):
+        x = torch.randn(8, 6, generator=g)
+        for mod, o in ((m, opt), (ref, ropt)):
+            o.zero_grad()
+            mod(x).pow(2).sum().backward()
+            o.step()
+    for p, q in zip(m.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)

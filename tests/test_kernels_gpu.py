@@ -378,3 +378,24 @@ def test_fused_qkv_attention(B, N, H):
         a = qkv.grad.view(B, N, 3, D)[:, :, t]
         r = qr.grad.view(B, N, 3, D)[:, :, t]
         assert rel(a, r) < 2e-2, (t, rel(a, r))
+
+
+@pytest.mark.parametrize("C", [10, 1000])
+def test_xent_ignore_index_grad_is_mean_over_valid_rows(C):
+    """Rows labelled ignore_index (and out-of-range labels) contribute nothing and
+    the gradient is scaled by 1/#valid, matching F.cross_entropy's mean."""
+    from distributed_ml_pytorch_amd.ops.functional import softmax_cross_entropy
+
+    torch.manual_seed(0)
+    B = 300
+    x = torch.randn(B, C, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    y = torch.randint(0, C, (B,), device="cuda")
+    y[::3] = -100
+    loss, hits = softmax_cross_entropy(x, y)
+    loss.backward()
+    xr = x.detach().float().requires_grad_(True)
+    lr = torch.nn.functional.cross_entropy(xr, y, ignore_index=-100)
+    lr.backward()
+    torch.testing.assert_close(loss.float(), lr, rtol=1e-2, atol=1e-3)
+    assert float((x.grad.float() - xr.grad).norm() / xr.grad.norm()) < 1e-2
+    assert float(x.grad[::3].float().abs().max()) == 0.0
