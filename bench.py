@@ -43,6 +43,10 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+# per-shape kernel picks measured offline on MI355X (ops/tuner.py); set before the
+# package is imported
+os.environ.setdefault("DMP_CONV_TUNE_CACHE", os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "tuning", "mi355x_tune_cache.json"))
 
 METRIC = "samples/sec (whole node) ResNet-18 ASGD at 1/2/4/8 MI355X; time-to-target-loss"
 

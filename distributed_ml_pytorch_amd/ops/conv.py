@@ -36,6 +36,9 @@ from .tuner import TUNER
 _NATIVE_ENABLED = True
 _CONFIGS = None
 _SMALL_MAX_K = 32
+# few-input-channel stems: "small" = the VALU kernels of conv_small.hip (BN
+# statistics in the epilogue), "im2col" = patch matrix + MFMA GEMM
+_STEM = os.environ.get("DMP_STEM", "small")
 
 # Weight gradients on a side HIP stream.  A layer's wgrad depends only on its
 # dY and X, and nothing in the rest of the backward depends on it (it lands in
@@ -430,8 +433,8 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
             if part is not None:
                 y._dmp_bn_part = part
             return (y, xa) if alias else y
-        if master is not None and b is None and not relu and small_conv_supported(
-                x, master, stride, padding, dilation, groups):
+        if master is not None and b is None and not relu and _STEM != "im2col" and \
+                small_conv_supported(x, master, stride, padding, dilation, groups):
             w16 = getattr(master, "_dmp_w16", None)
             if w16 is None or not w16.is_contiguous(memory_format=torch.channels_last):
                 w16 = master.detach().to(torch.bfloat16).contiguous(

@@ -6,7 +6,10 @@ eligible configuration is timed with HIP events on the current stream and the
 fastest is cached for the process.  Tuning never runs while a stream is being
 captured into a graph (the heuristic default is used then) and can be
 disabled with ``DMP_CONV_TUNE=0``.  ``DMP_CONV_TUNE_CACHE=path.json`` persists
-choices across processes.
+choices across processes (``bench.py`` defaults it to the committed
+``tuning/mi355x_tune_cache.json``, measured with more rounds than a cold start
+can afford: deterministic picks and no tuning at startup; shapes missing from
+it are tuned and added).
 """
 from __future__ import annotations
 
@@ -68,9 +71,14 @@ class KernelTuner:
             return best
 
     def _save(self):
+        # atomic replace: several ranks of one node may tune and save concurrently
         try:
-            with open(self.path, "w") as f:
-                json.dump({json.dumps(list(k)): v for k, v in self.cache.items()}, f)
+            os.makedirs(os.path.dirname(os.path.abspath(self.path)), exist_ok=True)
+            tmp = f"{self.path}.{os.getpid()}.tmp"
+            with open(tmp, "w") as f:
+                json.dump({json.dumps(list(k)): v for k, v in sorted(
+                    self.cache.items(), key=lambda kv: json.dumps(list(kv[0])))}, f, indent=0)
+            os.replace(tmp, self.path)
         except OSError:
             pass
 
