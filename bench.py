@@ -15,6 +15,10 @@ Topologies (``--ps``):
   all-gather, both on a side HIP stream over RCCL/xGMI, landed with
   staleness <= 1 step.  Simultaneous pushes are SUMMED, as a central Downpour
   PS adds every worker's delta (``--delta-scale mean`` averages instead).
+  The collectives make it lock-step at pull time (bounded drift).
+* ``sharded_async``: the same 1/N shards, each served by its own PS thread
+  (point-to-point gloo push/pull, host-staged payloads): no collective after
+  start-up, so a late rank delays only its own shard's replies.
 * ``central``: the reference topology (/root/reference/Makefile:13-20,
   example/main.py:135-138): rank 0 is the parameter server (fp32 master on its
   GPU, payloads over one RCCL communicator per (PS, worker) pair, headers on a
@@ -63,7 +67,7 @@ def parse(argv=None):
                     help="also time K steps at the reference's default batch "
                          "(/root/reference/example/main.py:142); 0 skips")
     ap.add_argument("--mode", default="asgd", choices=["asgd", "sync", "single"])
-    ap.add_argument("--ps", default="auto", choices=["auto", "local", "sharded", "central"])
+    ap.add_argument("--ps", default="auto", choices=["auto", "local", "sharded", "sharded_async", "central"])
     ap.add_argument("--delta-scale", default="sum",
                     help="sharded PS: 'sum' of simultaneous pushes (Downpour PS), 'mean', or x")
     ap.add_argument("--n-push", type=int, default=10)
@@ -345,7 +349,7 @@ def run(a):
                        "seq_len": None, "image": "x".join(map(str, in_shape)),
                        "parallelism": par, "n_push": a.n_push, "n_pull": a.n_pull,
                        "staleness": a.staleness, "lr": a.lr,
-                       "push_combine": a.delta_scale if a.ps == "sharded" else "sum",
+                       "push_combine": a.delta_scale if a.ps.startswith("sharded") else "sum",
                        "hip_graph": bool(graphed), "master_dtype": "fp32"},
             "world_size": world,
             "backend": info.backend,

@@ -46,7 +46,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--n-train", type=int, default=50000)
     p.add_argument("--n-test", type=int, default=10000)
     p.add_argument("--mode", default="asgd", choices=["asgd", "sync", "single"])
-    p.add_argument("--ps", default="central", choices=["central", "sharded", "local"])
+    p.add_argument("--ps", default="central", choices=["central", "sharded", "sharded_async", "local"])
     p.add_argument("--payload", default="auto", choices=["auto", "gloo", "rccl"])
     p.add_argument("--backend", default="auto", choices=["auto", "gloo", "nccl"])
     p.add_argument("--staleness", type=int, default=1)

@@ -99,15 +99,21 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // 16-byte chunk swizzle (an involution) for a row-major [rows][BK] bf16 tile.
-//  BK=64 (128-B rows, 2 rows per 256-B bank row): chunk ^= (row>>1)&7
-//  BK=32 ( 64-B rows, 4 rows per bank row):       chunk ^= (-(row>>2))&3
-// Both make each ds_read_b128 lane group (rows l&15, chunk c + (l>>4)) hit 16
-// distinct 16-B slots.  Rows r and r+16 share the same XOR, so fragment rows
+//  BK=64 (128-B rows, 2 rows per 256-B bank row): chunk ^= ((row>>1)&3) << 1
+//  BK=32 ( 64-B rows, 4 rows per bank row):       chunk ^= ((row>>2)&1) << 1
+// A ds_read_b128 fragment read (lane l: row p + (l&15), chunk c + (l>>4)) is
+// serviced in lane groups {0-3,12-15,20-27} / {4-11,16-19,28-31} (+32): rows
+// p..p+3 and p+12..p+15 at one chunk, p+4..p+11 at the next.  These XORs give
+// 16 distinct 16-B slots per group for ANY start row p, not only p % 16 == 0:
+// the halo kernels read fragments at row offsets of +1, +2, W+2, ... (one per
+// tap), where the previous (row>>1)&7 / (-(row>>2))&3 forms conflicted (34 %
+// extra LDS cycles measured on the 64-channel halo forward,
+// profiles/halo_pmc_r1.txt).  Rows r and r+16 share the XOR, so fragment rows
 // 16 apart differ by a constant offset (folded into ds_read immediates).
 template <int BK>
 __device__ __forceinline__ int swz(int row, int c) {
-  if constexpr (BK == 64) return c ^ ((row >> 1) & 7);
-  else return c ^ ((-(row >> 2)) & 3);
+  if constexpr (BK == 64) return c ^ (((row >> 1) & 3) << 1);
+  else return c ^ (((row >> 2) & 1) << 1);
 }
 
 // MODE 0: forward conv.  MODE 1: data gradient, one parity class per blockIdx.z.
@@ -426,7 +432,7 @@ struct HaloGeom {
   int TH, TB, HROWS, A_INS;
 };
 
-constexpr int kHaloAPW = 6;   // max halo DMA instructions per wave per stage
+constexpr int kHaloAPW = 8;   // max halo DMA instructions per wave per stage
 
 template <int BM, int BN, int BK, int WM, int WN, int NS, bool FLIP, bool STATS>
 __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, HaloGeom hg) {
@@ -518,29 +524,49 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) offB[ks] = rb * BK + swz<BK>(rb, ks * 4 + (lane >> 4)) * 8;
   }
+  // (tap, k-step) steps with the fragments double-buffered in registers: the
+  // reads of step st+1 are issued ahead of step st's MFMAs, so each step's LDS
+  // latency hides behind the previous step's TM*TN MFMAs (reading each step's
+  // operands just before its MFMAs left ~3 exposed lgkmcnt waits per tap)
   auto compute = [&](int buf) {
     const u16* As = lds_h + buf * STAGE;
     const u16* Bs = As + A_EL;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
+    constexpr int KS = BK / 32, NSTEP = 9 * KS;
+    bf16x8 af[2][TM], bw[2][TN];
+    auto load = [&](int st, int slot) {
+      const int t = st / KS, ks = st % KS;
       const int rowoff = (t / 3) * HW2 + (t % 3);
       const int wt = FLIP ? 8 - t : t;
 #pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8 af[TM], bw[TN];
+      for (int i = 0; i < TM; ++i) {
+        const int row = hrow[i] + rowoff;
+        af[slot][i] = *reinterpret_cast<const bf16x8*>(
+            As + row * BK + swz<BK>(row, ks * 4 + (lane >> 4)) * 8);
+      }
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int row = hrow[i] + rowoff;
-          af[i] = *reinterpret_cast<const bf16x8*>(
-              As + row * BK + swz<BK>(row, ks * 4 + (lane >> 4)) * 8);
+      for (int j = 0; j < TN; ++j)
+        bw[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + wt * BN * BK + offB[ks] + j * 16 * BK);
+    };
+    load(0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);   // step 0's reads first
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
+      if (st + 1 < NSTEP) load(st + 1, (st + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bw[st & 1][j], af[st & 1][i], acc[i][j]);
+      // pin the schedule: step st+1's reads interleaved one per MFMA of step st
+      // (the scheduler otherwise sinks each read next to its first use)
+      if (st + 1 < NSTEP) {
+#pragma unroll
+        for (int k = 0; k < TM + TN && k < TM * TN; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          bw[j] = *reinterpret_cast<const bf16x8*>(Bs + wt * BN * BK + offB[ks] + j * 16 * BK);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bw[j], af[i], acc[i][j]);
+        if (TM * TN > TM + TN) __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
       }
     }
   };
@@ -778,9 +804,15 @@ static void dispatch(const ConvArgs& a, int cfg, int classes, hipStream_t s) {
   X(5, 128, 64, 32, 2, 2, 1)  \
   X(6, 256, 64, 32, 4, 2, 1)  \
   X(7, 64, 64, 32, 2, 2, 1)   \
-  X(8, 128, 64, 32, 4, 2, 1)
+  X(8, 128, 64, 32, 4, 2, 1)   \
+  X(9, 256, 64, 32, 4, 1, 1)   \
+  X(10, 256, 64, 32, 4, 1, 2)  \
+  X(11, 128, 64, 32, 2, 1, 1)  \
+  X(12, 128, 128, 32, 2, 2, 1) \
+  X(13, 256, 128, 32, 4, 2, 1) \
+  X(14, 512, 64, 32, 8, 1, 1)
 
-constexpr int kHaloBase = 100, kNumHaloConfigs = 9;
+constexpr int kHaloBase = 100, kNumHaloConfigs = 15;
 
 static bool halo_cfg(int cfg, int* bm, int* bn, int* bk, int* nw, int* ns) {
   switch (cfg - kHaloBase) {

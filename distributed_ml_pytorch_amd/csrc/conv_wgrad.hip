@@ -22,6 +22,8 @@
 //   BP   - reduction rows per stage (32 / 64)
 //   NS   - pipeline depth: NS-1 stages of DMA in flight, retired with a
 //          counted s_waitcnt vmcnt(N) before one raw s_barrier per stage.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dmp {
@@ -271,92 +273,135 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 // ------------------------------------------------- 3x3 stride-1 halo wgrad
 // dW[co][r][s][ci] += sum_p dY[p][co] * X[p shifted by (r-1, s-1)][ci] for 3x3 /
 // stride 1 / pad 1.  The gather kernel above fetches X once per tap column
-// tile; here a block owns one tap ROW r, a 64 x 64 (co, ci) tile and a run of
-// BM-pixel tiles (whole image rows / whole images, as the forward halo kernel),
-// and per tile stages dY [BM][64] plus the input rows the tap row reads,
+// tile; here a block owns a 64 x 64 (co, ci) tile and TR tap rows (TR = 1: one
+// row r, grid.y enumerates r; TR = 3: all nine taps) and walks a run of
+// BM-pixel tiles (whole image rows / whole images, as the forward halo kernel).
+// Per tile it stages dY [BM][64] plus the input rows those tap rows read,
 // X[h - 1 + r][-1 .. W] (W + 2 columns, zero outside the image), ONCE: the
-// three taps s = 0, 1, 2 are the same staged rows offset by s.  Both images are
-// [row][64] with the 32-B granule swizzle and read with ds_read_b64_tr_b16;
-// a lane supplies its own row address per tr read, so the shifted pixel->row
-// map needs no layout change.  4 waves, wave w: all 64 co x ci 16w..16w+15 x 3
-// taps (12 accumulator tiles).  Partial sums go to dW with fp32 atomics, or
-// plain read-add-write when one block owns the tile (splits == 1).
+// taps are the same staged rows offset by r * (W + 2) + s.  Both images are
+// [row][64] with the 32-B granule swizzle and read with ds_read_b64_tr_b16; a
+// lane supplies its own row address per tr read, so the shifted pixel -> row
+// map needs no layout change.  4 waves, wave w: all 64 co x ci 16w..16w+15 x
+// 3*TR taps (12 or 36 accumulator tiles).
+//
+// Tiles stream through an NS-deep ring of LDS-DMA stages (counted vmcnt + one
+// raw s_barrier per tile): every wave issues the same D_PW + XPW DMAs per stage
+// (padding rows past the staged image read zeros), so "stage t landed" is
+// vmcnt <= (NS - 2) * (D_PW + XPW).  With NS = 2 one tile of compute (~0.3 us
+// at BM 128, TR 1) had to cover a whole HBM round trip.
+// Blocks are mapped XCD-aware: the tiles of one pixel split share an XCD's L2.
+// Partial sums go to dW with fp32 atomics, or plain read-add-write when one
+// block owns the tile (splits == 1).
 struct WgradHaloGeom {
-  int TH, TB, XROWS, XINS, ntiles, tiles_per_split;
+  int TH, TB, THX, XROWS, XPW, ntiles, tiles_per_split;
 };
 
-constexpr int kWhXPW = 8;   // max X-row DMA instructions per wave per tile
+constexpr int kWhXPW = 12;   // max X-row DMA instructions per wave per stage
 
-template <int BM>
+// vmcnt wait with a launch-time (wave-uniform) count
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  switch (n) {
+#define DMP_WV(k) \
+  case k:         \
+    wait_vm<k>(); \
+    break;
+    DMP_WV(1) DMP_WV(2) DMP_WV(3) DMP_WV(4) DMP_WV(5) DMP_WV(6) DMP_WV(7) DMP_WV(8) DMP_WV(9)
+    DMP_WV(10) DMP_WV(11) DMP_WV(12) DMP_WV(13) DMP_WV(14) DMP_WV(15) DMP_WV(16) DMP_WV(17)
+    DMP_WV(18) DMP_WV(19) DMP_WV(20) DMP_WV(21) DMP_WV(22) DMP_WV(23) DMP_WV(24) DMP_WV(25)
+    DMP_WV(26) DMP_WV(27) DMP_WV(28) DMP_WV(29) DMP_WV(30) DMP_WV(31) DMP_WV(32) DMP_WV(33)
+    DMP_WV(34) DMP_WV(35) DMP_WV(36) DMP_WV(37) DMP_WV(38) DMP_WV(39) DMP_WV(40)
+#undef DMP_WV
+    default:
+      wait_vm<0>();
+  }
+}
+
+template <int BM, int NS, int TR>
 __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, WgradHaloGeom hg,
                                                               int atomic) {
   constexpr int NW = 4, CW = 64;                  // 64-channel rows (128 B)
-  constexpr int D_INS = BM * 8 / 64;              // dY DMA instructions per tile
-  constexpr int D_PW = D_INS / NW;
-  static_assert(D_INS % NW == 0, "dY split");
+  constexpr int D_PW = BM / 32;                   // dY DMA instructions per wave per tile
+  constexpr int NT = 3 * TR;                      // taps per block
   extern __shared__ __attribute__((aligned(16))) u16 lds_w[];
+  const int XPW = hg.XPW;
   const int D_EL = BM * CW;
-  const int STAGE = D_EL + hg.XINS * 8 * CW;
+  const int STAGE = D_EL + XPW * NW * 512;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ci0 = blockIdx.x * CW;
-  const int co0 = (blockIdx.y / 3) * CW, r = blockIdx.y % 3;
-  const int t_begin = blockIdx.z * hg.tiles_per_split;
+  // XCD-aware bijective remap: consecutive logical blocks (the (ci, co, r)
+  // tiles of one pixel split) land on one XCD under round-robin dispatch
+  const int nx = gridDim.x, ny = gridDim.y, G = nx * ny * gridDim.z;
+  const int bid = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int bx = lid % nx, by = (lid / nx) % ny, bz = lid / (nx * ny);
+  const int ci0 = bx * CW;
+  const int co0 = (TR == 3 ? by : by / 3) * CW, r0 = TR == 3 ? 0 : by % 3;
+  const int t_begin = bz * hg.tiles_per_split;
   const int t_end = min(hg.ntiles, t_begin + hg.tiles_per_split);
   if (t_begin >= t_end) return;
-  const int H = a.GH, W = a.GW, C = a.CI, CO = a.CO, TH = hg.TH, W2 = W + 2;
+  const int H = a.GH, W = a.GW, C = a.CI, CO = a.CO, TH = hg.TH, THX = hg.THX, W2 = W + 2;
   const int img = H * W;
-  const long long P = a.P;
+  const int P = (int)a.P;
 
   // dY DMA slots (fixed per lane): row of the tile, swizzled source column
-  int d_row[D_PW], d_col[D_PW];
+  int d_row[D_PW], d_off[D_PW];
 #pragma unroll
   for (int j = 0; j < D_PW; ++j) {
     const int row = (wid + j * NW) * 8 + lane / 8, pch = lane % 8;
     d_row[j] = row;
-    d_col[j] = co0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8;
+    d_off[j] = row * CO + co0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8;
   }
-  // X DMA slots: staged row -> (image in tile, row in tile, column incl. halo)
-  int x_tb[kWhXPW], x_th[kWhXPW], x_w[kWhXPW], x_col[kWhXPW];
+  // X DMA slots: staged row -> element offset relative to the tile's first
+  // pixel (x_off) + {valid, image in tile, source row - h0} (x_inf)
+  int x_off[kWhXPW];
+  unsigned x_inf[kWhXPW];
 #pragma unroll
   for (int j = 0; j < kWhXPW; ++j) {
-    const int row = (wid + j * NW) * 8 + lane / 8, pch = lane % 8;
-    const int tb = row / (TH * W2), rem = row - tb * TH * W2;
-    x_tb[j] = tb;
-    x_th[j] = rem / W2;
-    x_w[j] = rem - x_th[j] * W2 - 1;
-    x_col[j] = ci0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8;
+    x_off[j] = 0;
+    x_inf[j] = 0;
+    if (j < XPW) {
+      const int row = (wid + j * NW) * 8 + lane / 8, pch = lane % 8;
+      const int tb = row / (THX * W2), rem = row - tb * THX * W2;
+      const int th = rem / W2, w = rem - th * W2 - 1;
+      const int dh = th - 1 + r0;
+      const bool ok = row < hg.XROWS && tb < hg.TB && (unsigned)w < (unsigned)W;
+      x_off[j] = (tb * img + dh * W + w) * C + ci0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) +
+                 (pch & 1) * 8;
+      x_inf[j] = (ok ? 0x80000000u : 0u) | ((unsigned)tb << 16) | ((unsigned)(dh + 64) << 8);
+    }
   }
   const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.dy, 0, (int)(2 * P * CO), 0x00020000);
+      (void*)a.dy, 0, (int)(2LL * P * CO), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.x, 0, (int)(2LL * a.B * H * W * C), 0x00020000);
+      (void*)a.x, 0, (int)(2LL * a.B * img * C), 0x00020000);
 
+  // issue stage `t` into ring slot `buf`; a tile past the run loads zeros so
+  // every wave's DMA count per stage stays D_PW + XPW
   auto stage = [&](int buf, int t) {
     u16* Ds = lds_w + buf * STAGE;
     u16* Xs = Ds + D_EL;
-    const long long m0 = (long long)t * BM;
-    const int b0 = (int)(m0 / img), h0 = (int)(m0 - (long long)b0 * img) / W;
+    const bool live = t < t_end;
+    const int m0 = t * BM;
+    const int b0 = m0 / img, h0 = (m0 - b0 * img) / W;
 #pragma unroll
     for (int j = 0; j < D_PW; ++j) {
-      const long long p = m0 + d_row[j];
-      bdma16w(rsD, p < P ? 2u * (unsigned)(p * CO + d_col[j]) : kOOBw, Ds + (wid + j * NW) * 512);
+      const bool ok = live && m0 + d_row[j] < P;
+      bdma16w(rsD, ok ? 2u * (unsigned)(m0 * CO + d_off[j]) : kOOBw, Ds + (wid + j * NW) * 512);
     }
 #pragma unroll
     for (int j = 0; j < kWhXPW; ++j) {
-      const int ins = wid + j * NW;
-      if (ins < hg.XINS) {
-        const int b = b0 + x_tb[j], h = h0 - 1 + r + x_th[j], w = x_w[j];
-        const bool ok = x_tb[j] < hg.TB && b < a.B && (unsigned)h < (unsigned)H &&
-                        (unsigned)w < (unsigned)W;
-        bdma16w(rsX, ok ? 2u * (unsigned)(((b * H + h) * W + w) * C + x_col[j]) : kOOBw,
-                Xs + ins * 512);
+      if (j < XPW) {
+        const unsigned inf = x_inf[j];
+        const int tb = (int)((inf >> 16) & 0x7fff), dh = (int)((inf >> 8) & 255) - 64;
+        const bool ok = live && (inf >> 31) && b0 + tb < a.B && (unsigned)(h0 + dh) < (unsigned)H;
+        bdma16w(rsX, ok ? 2u * (unsigned)(m0 * C + x_off[j]) : kOOBw, Xs + (wid + j * NW) * 512);
       }
     }
   };
 
-  // staged X row of the lane's reduction rows (pixels pk*32 + 8g + q and +4)
+  // staged X row of the lane's reduction rows (pixels pk*32 + 8g + q and +4), tap (0, 0)
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pc = li & 3;
   int xr_lo[BM / 32], xr_hi[BM / 32];
 #pragma unroll
@@ -366,7 +411,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, Wgrad
       const int pl = pk * 32 + 8 * g + q + 4 * hsel;
       const int tb = pl / (TH * W), r2 = pl - tb * TH * W;
       const int th = r2 / W, tw = r2 - th * W;
-      const int xr = (tb * TH + th) * W2 + tw;
+      const int xr = (tb * THX + th) * W2 + tw;
       if (hsel) xr_hi[pk] = xr; else xr_lo[pk] = xr;
     }
   }
@@ -375,71 +420,109 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, Wgrad
         (__attribute__((address_space(3))) s16x4_t*)(img_ + wg_off<CW>(row, col)));
   };
 
-  f32x4 acc[3][4];
+  f32x4 acc[NT][4];
 #pragma unroll
-  for (int s = 0; s < 3; ++s)
+  for (int s = 0; s < NT; ++s)
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[s][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // pk steps with the fragments double-buffered in registers and the reads of
+  // step pk+1 pinned between step pk's MFMAs (sched_group_barrier): the
+  // scheduler otherwise sinks every read next to its first use and each step
+  // waits out its own LDS latency
   auto compute = [&](int buf) {
     const u16* Ds = lds_w + buf * STAGE;
     const u16* Xs = Ds + D_EL;
-#pragma unroll
-    for (int pk = 0; pk < BM / 32; ++pk) {
-      bf16x8 af[4], bx[3];
+    constexpr int NPK = BM / 32, NRD = 8 + 6 * TR, NMF = 12 * TR;
+    bf16x8 af[2][4], bx[2][3 * TR];
+    auto load = [&](int pk, int slot) {
       const int drow = pk * 32 + 8 * g + q;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const s16x4_t lo = tr(Ds, drow, i * 16 + 4 * pc), hi = tr(Ds, drow + 4, i * 16 + 4 * pc);
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        af[slot][i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        const s16x4_t lo = tr(Xs, xr_lo[pk] + s, wid * 16 + 4 * pc);
-        const s16x4_t hi = tr(Xs, xr_hi[pk] + s, wid * 16 + 4 * pc);
-        bx[s] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      for (int r = 0; r < TR; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const s16x4_t lo = tr(Xs, xr_lo[pk] + r * W2 + s, wid * 16 + 4 * pc);
+          const s16x4_t hi = tr(Xs, xr_hi[pk] + r * W2 + s, wid * 16 + 4 * pc);
+          bx[slot][r * 3 + s] =
+              __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+    };
+    load(0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
+#pragma unroll
+    for (int pk = 0; pk < NPK; ++pk) {
+      if (pk + 1 < NPK) load(pk + 1, (pk + 1) & 1);
+#pragma unroll
+      for (int t = 0; t < 3 * TR; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[t][i] = mfma16w(af[pk & 1][i], bx[pk & 1][t], acc[t][i]);
+      if (pk + 1 < NPK) {
+        // one read of step pk+1 after each MFMA of step pk, the rest at the end
+#pragma unroll
+        for (int m = 0; m < NMF; ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (m < NRD) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if constexpr (NRD > NMF) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NMF, 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
       }
-#pragma unroll
-      for (int s = 0; s < 3; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[s][i] = mfma16w(af[i], bx[s], acc[s][i]);
     }
   };
 
-  stage(0, t_begin);
-  for (int t = t_begin; t < t_end; ++t) {
-    wait_vm<0>();                       // tile t landed (this wave's DMAs) ...
-    __builtin_amdgcn_s_barrier();       // ... for every wave; tile t-1's buffer is free
+  const int nt = t_end - t_begin;
+  const int vm_wait = (NS - 2) * (D_PW + XPW);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) stage(s, t_begin + s);
+  for (int it = 0; it < nt; ++it) {
+    if (NS == 2) wait_vm<0>();
+    else wait_vm_rt(vm_wait);           // tile `it` landed (this wave's DMAs) ...
+    __builtin_amdgcn_s_barrier();       // ... for every wave; slot (it-1) % NS is free
     asm volatile("" ::: "memory");
-    if (t + 1 < t_end) stage((t + 1 - t_begin) & 1, t + 1);
-    compute((t - t_begin) & 1);
+    stage((it + NS - 1) % NS, t_begin + it + NS - 1);
+    compute(it % NS);
   }
+  wait_vm<0>();
   // D layout: lane holds rows co = 4*(lane>>4)+rr of column ci = lane & 15
   const long long K = 9LL * C;
   const int ci = ci0 + wid * 16 + (lane & 15);
 #pragma unroll
-  for (int s = 0; s < 3; ++s)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int co = co0 + i * 16 + 4 * (lane >> 4) + rr;
-        float* dst = a.dw + (long long)co * K + (r * 3 + s) * C + ci;
-        if (atomic) atomicAdd(dst, acc[s][i][rr]);
-        else *dst += acc[s][i][rr];
+        float* dst = a.dw + (long long)co * K + ((r0 + t / 3) * 3 + t % 3) * C + ci;
+        if (atomic == 1) atomicAdd(dst, acc[t][i][rr]);
+        else if (atomic == 0) *dst += acc[t][i][rr];
+        else *dst = acc[t][i][rr];   // timing diagnostic only (DMP_WGRAD_HALO_DIAG=store)
       }
 }
 
-// halo wgrad cfg ids: kWhBase + bm_sel * 4 + spl, BM = 64 << bm_sel, target
-// block count 128 << spl
+// halo wgrad cfg ids: kWhBase + variant * 12 + bm_sel * 4 + spl; BM = 64 << bm_sel,
+// target block count 128 << spl; variant -> (NS, TR) below (ids 1000..1011 are
+// the round-1 kernel's configs: NS 2, one tap row per block)
 constexpr int kWhBase = 1000;
+constexpr int kWhVariants = 5;
+constexpr int kWhNS[kWhVariants] = {2, 3, 4, 2, 3};
+constexpr int kWhTR[kWhVariants] = {1, 1, 1, 3, 3};
 
 static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R, int S, int stride,
-                            int pad, WgradHaloGeom* g, int* bm_out, size_t* lds, int* splits) {
+                            int pad, WgradHaloGeom* g, int* bm_out, int* ns_out, int* tr_out,
+                            size_t* lds, int* splits) {
   const int id = cfg - kWhBase;
-  if (id < 0 || id >= 12) return false;
-  const int bm = 64 << (id / 4), target = 128 << (id % 4);
+  if (id < 0 || id >= 12 * kWhVariants) return false;
+  const int var = id / 12, rest = id % 12;
+  const int bm = 64 << (rest / 4), target = 128 << (rest % 4);
+  const int ns = kWhNS[var], tr = kWhTR[var];
   if (R != 3 || S != 3 || stride != 1 || pad != 1 || CI % 64 || CO % 64) return false;
+  if (tr == 3 && bm > 128) return false;   // 36 accumulator tiles + hoisted addresses spill
   const int img = H * W;
   WgradHaloGeom h{};
   if (bm <= img) {
@@ -451,22 +534,27 @@ static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R,
     h.TH = H;
     h.TB = bm / img;
   }
-  h.XROWS = h.TB * h.TH * (W + 2);
-  h.XINS = (h.XROWS + 7) / 8;
-  if (h.XINS > kWhXPW * 4) return false;
+  h.THX = h.TH + tr - 1;
+  h.XROWS = h.TB * h.THX * (W + 2);
+  h.XPW = ((h.XROWS + 7) / 8 + 3) / 4;
+  if (h.XPW > kWhXPW || h.THX + 1 > 127 || h.TB > 0x7fff) return false;
+  if ((ns - 2) * (bm / 32 + h.XPW) > 40) return false;
   const long long M = (long long)B * img;
+  if (2LL * M * (CO > CI ? CO : CI) >= (1LL << 31)) return false;
   h.ntiles = (int)((M + bm - 1) / bm);
-  const int per = (CI / 64) * (CO / 64) * 3;
+  const int per = (CI / 64) * (CO / 64) * (3 / tr);
   int sp = target / per;
   if (sp < 1) sp = 1;
   if (sp > h.ntiles) sp = h.ntiles;
   h.tiles_per_split = (h.ntiles + sp - 1) / sp;
   sp = (h.ntiles + h.tiles_per_split - 1) / h.tiles_per_split;
-  const size_t stage = (size_t)bm * 64 + (size_t)h.XINS * 8 * 64;
-  *lds = 2 * stage * 2;
+  const size_t stage = (size_t)bm * 64 + (size_t)h.XPW * 4 * 512;
+  *lds = (size_t)ns * stage * 2;
   if (*lds > 160 * 1024) return false;
   *g = h;
   *bm_out = bm;
+  *ns_out = ns;
+  *tr_out = tr;
   *splits = sp;
   return true;
 }
@@ -474,25 +562,38 @@ static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R,
 bool conv_wgrad_halo_ok(int cfg, int B, int H, int W, int CI, int CO, int R, int S, int stride,
                         int pad) {
   WgradHaloGeom g;
-  int bm, sp;
+  int bm, ns, tr, sp;
   size_t lds;
-  return wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &lds, &sp);
+  return wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &lds, &sp);
 }
 int conv_wgrad_halo_base() { return kWhBase; }
-int conv_wgrad_num_halo_configs() { return 12; }
+int conv_wgrad_num_halo_configs() { return 12 * kWhVariants; }
 
-template <int BM>
+template <int BM, int NS, int TR>
 static void launch_wgrad_halo_t(const WgradArgs& a, const WgradHaloGeom& g, size_t lds, int splits,
                                 hipStream_t s) {
   static bool attr = false;
+  static int diag = -1;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<BM>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<BM, NS, TR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  const dim3 grid((unsigned)(a.CI / 64), (unsigned)(a.CO / 64 * 3), (unsigned)splits);
-  hipLaunchKernelGGL(conv_wgrad_halo_kernel<BM>, grid, dim3(256), lds, s, a, g,
-                     splits > 1 ? 1 : 0);
+  if (diag < 0) {
+    const char* e = getenv("DMP_WGRAD_HALO_DIAG");
+    diag = (e && e[0] == 's') ? 1 : 0;
+  }
+  const dim3 grid((unsigned)(a.CI / 64), (unsigned)(a.CO / 64 * (3 / TR)), (unsigned)splits);
+  hipLaunchKernelGGL((conv_wgrad_halo_kernel<BM, NS, TR>), grid, dim3(256), lds, s, a, g,
+                     diag ? 2 : (splits > 1 ? 1 : 0));
+}
+
+template <int NS, int TR>
+static void launch_wgrad_halo_bm(int bm, const WgradArgs& a, const WgradHaloGeom& g, size_t lds,
+                                 int sp, hipStream_t s) {
+  if (bm == 64) launch_wgrad_halo_t<64, NS, TR>(a, g, lds, sp, s);
+  else if (TR == 3 || bm == 128) launch_wgrad_halo_t<128, NS, TR>(a, g, lds, sp, s);
+  else launch_wgrad_halo_t<(TR == 3 ? 128 : 256), NS, TR>(a, g, lds, sp, s);   // TR 3: BM <= 128
 }
 
 // cfg bits: [1:0] BNW (0 auto, 1 -> 64, 2 -> 128, 3 -> 192), [2] BP (0 -> 64, 1 -> 32),
@@ -516,12 +617,17 @@ void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int
               dbias};
   if (cfg >= kWhBase && dbias == nullptr) {
     WgradHaloGeom g;
-    int bm, sp;
+    int bm, ns, tr, sp;
     size_t lds;
-    if (wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &lds, &sp)) {
-      if (bm == 64) launch_wgrad_halo_t<64>(a, g, lds, sp, s);
-      else if (bm == 128) launch_wgrad_halo_t<128>(a, g, lds, sp, s);
-      else launch_wgrad_halo_t<256>(a, g, lds, sp, s);
+    if (wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &lds, &sp)) {
+      if (tr == 3) {
+        if (ns == 2) launch_wgrad_halo_bm<2, 3>(bm, a, g, lds, sp, s);
+        else launch_wgrad_halo_bm<3, 3>(bm, a, g, lds, sp, s);
+      } else {
+        if (ns == 2) launch_wgrad_halo_bm<2, 1>(bm, a, g, lds, sp, s);
+        else if (ns == 3) launch_wgrad_halo_bm<3, 1>(bm, a, g, lds, sp, s);
+        else launch_wgrad_halo_bm<4, 1>(bm, a, g, lds, sp, s);
+      }
       return;
     }
     cfg = -1;   // not applicable: gather kernel, heuristic variant

@@ -6,7 +6,9 @@ the central topology, workers train with ``Asynchronous``; ``--no-distributed``
 
 * ``mode="asgd"``   Downpour SGD; ``ps`` = ``central`` (reference star,
   gloo or RCCL payloads), ``sharded`` (PS co-located on every GPU, collective
-  push/pull) or ``local`` (in-process PS, 1 device);
+  push/pull), ``sharded_async`` (one PS thread per shard, point-to-point
+  push/pull, no rank waits for another: parallel/async_sharded.py) or
+  ``local`` (in-process PS, 1 device);
 * ``mode="sync"``   bucketed all-reduce data parallel;
 * ``mode="single"`` plain SGD, no communication.
 
@@ -31,6 +33,7 @@ from ..models import build_model
 from ..ops.functional import softmax_cross_entropy
 from ..parallel.arena import attach_arena
 from ..parallel.asgd import Asynchronous
+from ..parallel.async_sharded import AsyncShardedPSClient
 from ..parallel.clients import (GlooPSClient, LocalPSClient, RcclPSClient, ShardedPSClient)
 from ..parallel.ddp import BucketedAllReduce, FusedSGD
 from ..parallel.server import ParameterServer, make_ps_groups
@@ -64,7 +67,7 @@ class TrainConfig:
     pull_mode: str = "overwrite"
     wire_dtype: str = "fp32"
     mode: str = "asgd"                # asgd | sync | single
-    ps: str = "central"               # central | sharded | local
+    ps: str = "central"               # central | sharded | sharded_async | local
     payload: str = "auto"             # central PS payload transport: gloo | rccl | auto
     dtype: str = "bf16"               # compute dtype on GPU (CPU always fp32)
     cuda: bool = True
@@ -147,6 +150,8 @@ class Worker:
             return LocalPSClient(**kw)
         if cfg.ps == "sharded":
             return ShardedPSClient(delta_scale=cfg.delta_scale, **kw)
+        if cfg.ps == "sharded_async":
+            return AsyncShardedPSClient(delta_scale=cfg.delta_scale, **kw)
         if cfg.ps == "central":
             ctrl, pairs = ps_groups if ps_groups is not None else (None, {})
             if pairs and self.device.type == "cuda" and _payload(cfg, info) == "rccl":

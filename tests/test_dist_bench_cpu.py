@@ -66,6 +66,18 @@ def test_bench_central_ps_three_ranks():
     assert 0 <= ps["staleness_mean"] <= 4
 
 
+def test_bench_sharded_async_three_ranks():
+    """``--ps sharded_async``: every rank trains; shard servers answer point-to-point."""
+    r, lines = _bench(["--gpus", "3", "--ps", "sharded_async", "--steps", "4", "--warmup", "2",
+                       "--model", "mlp", "--batch", "8", "--n-push", "2", "--n-pull", "2",
+                       "--ttl-target", "0", "--ref-batch", "0"])
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 3 and out["workers"] == 3
+    assert out["config"]["parallelism"] == "asgd-sharded_async-ps x3"
+
+
 def test_bench_central_ps_with_time_to_target():
     """Two PS sessions (throughput, then a fresh model for time-to-target)."""
     r, lines = _bench(["--gpus", "3", "--ps", "central", "--steps", "2", "--warmup", "1",
@@ -265,12 +277,12 @@ def _converge(rank, world, ps):
 
     cfg = _train_cfg(ps=ps, n_train=1024, n_test=256, test_batch_size=256, batch_size=32,
                      lr=0.02, n_push=4, n_pull=4, evaluate=True, epochs=1,
-                     delta_scale="mean" if ps == "sharded" else "sum")
+                     delta_scale="mean" if ps.startswith("sharded") else "sum")
     res = run_training(cfg, DistInfo(rank, world, rank, "gloo", torch.device("cpu")))
     return {k: v for k, v in res.items() if isinstance(v, (int, float, str, dict))}
 
 
-@pytest.mark.parametrize("ps", ["central", "sharded"])
+@pytest.mark.parametrize("ps", ["central", "sharded", "sharded_async"])
 def test_eight_rank_asgd_converges(ps):
     """1 PS + 7 workers (reference topology at BASELINE config #3's size) and an
     8-way sharded PS both learn the synthetic task."""
