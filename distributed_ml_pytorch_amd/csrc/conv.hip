@@ -695,6 +695,269 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   }
 }
 
+// ------------------------------------ persistent 3x3 halo tiles, 64 channels
+// The 64-channel layers (ResNet-18 CIFAR stage 1: 32x32 x 64 -> 64) run the
+// halo kernel above with only C/32 = 2 chunks per block, and every block
+// re-stages all nine 64x32 weight taps per chunk: 72 KB of weights DMA'd per
+// 256 output pixels beside 43 KB of halo input.  These kernels are bound by the
+// global->LDS fill rate (~10-15 B/clk/CU, profiles/conv_kernels_r2.txt), so
+// here the whole 9 x 64 x 64 weight tensor stays RESIDENT in LDS (72 KB,
+// fetched once per block) and a persistent block streams BM-pixel halo tiles
+// with all 64 input channels (128-B rows) through an NS-deep LDS-DMA ring:
+// the fill traffic per pixel drops ~2.7x.  4 waves, wave = 64 pixels x 64
+// output channels (TM = BM / 64 fragments of 16 pixels, TN = 4).
+// Per tile the epilogue of the PREVIOUS tile runs after the next stage's DMA
+// is issued, so its stores drain under this tile's MFMAs; the ring wait then
+// counts only DMA pieces (vmcnt <= (NS-2) * APW also covers those stores,
+// whatever order loads and stores retire in).  BN partial sums accumulate in
+// registers over all of a block's tiles (one slot reduction per block).
+// FLIP = stride-1 data gradient (dY, Wt, mirrored taps); no residual addend
+// (the host routes addend dgrads to conv_halo_kernel).
+struct HaloPGeom {
+  int TH, TB, HROWS, APW, AINS, ntiles;   // APW: pieces per wave (>= AINS / NW), AINS: exact
+};
+
+constexpr int kHpAPW = 12;   // max halo DMA pieces per wave per tile
+
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+#define DMP_WV(k) \
+  case k:         \
+    wait_vm<k>(); \
+    break;
+    DMP_WV(1) DMP_WV(2) DMP_WV(3) DMP_WV(4) DMP_WV(5) DMP_WV(6) DMP_WV(7) DMP_WV(8) DMP_WV(9)
+    DMP_WV(10) DMP_WV(11) DMP_WV(12) DMP_WV(13) DMP_WV(14) DMP_WV(15) DMP_WV(16) DMP_WV(17)
+    DMP_WV(18) DMP_WV(19) DMP_WV(20) DMP_WV(21) DMP_WV(22) DMP_WV(23) DMP_WV(24)
+#undef DMP_WV
+    default:
+      wait_vm<0>();
+  }
+}
+
+template <int BM, int NS, int NW, bool FLIP, bool STATS>
+__global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloPGeom hg) {
+  constexpr int BK = 64, BN = 64, RPI = 8;
+  constexpr int TM = BM / NW / 16, TN = BN / 16, KS = BK / 32, NSTEP = 9 * KS;
+  constexpr int W_EL = 9 * BN * BK;
+  extern __shared__ __attribute__((aligned(16))) u16 lds_p[];
+  const int APW = hg.APW;
+  // NS = 2 drains the ring every tile (vmcnt(0)), so waves may issue unequal
+  // piece counts and the stage holds exactly AINS pieces; deeper rings count
+  // pieces per wave and pad every wave to APW
+  const int STAGE = (NS == 2 ? hg.AINS : APW * NW) * RPI * BK;
+  u16* Ws = lds_p;
+  u16* Hs = lds_p + W_EL;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n0 = blockIdx.y * BN;
+  const int H = a.GH, W = a.GW, C = a.CI, TH = hg.TH, W2 = W + 2;
+  const int img = H * W;
+  const int P = a.B * img;
+  const int G = gridDim.x, ntiles = hg.ntiles;
+  const int nt = (ntiles - (int)blockIdx.x + G - 1) / G;
+  if (nt <= 0) return;
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, 0, (int)(2LL * P * C), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.w, 0, (int)(2LL * a.CO * 9 * C), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.y, 0, (int)(2LL * P * a.CO), 0x00020000);
+
+  // resident weights: row = tap * 64 + output channel, 72 pieces (18 per wave)
+#pragma unroll
+  for (int j = 0; j < 9 * BN / RPI / NW; ++j) {
+    const int ins = wid + j * NW;
+    const int row = ins * RPI + lane / 8;
+    const int t = row / BN, co = row - t * BN;
+    const bool ok = n0 + co < a.CO;
+    bdma16(rsB, ok ? 2u * (unsigned)(((n0 + co) * 9 + t) * C + swz<BK>(row, lane % 8) * 8) : kOOB,
+           Ws + ins * (RPI * BK));
+  }
+  // halo DMA slots: staged row -> element offset from the tile's first pixel +
+  // {valid, image in tile, source row - h0}
+  int x_off[kHpAPW];
+  unsigned x_inf[kHpAPW];
+  const int per_img = (TH + 2) * W2;
+#pragma unroll
+  for (int j = 0; j < kHpAPW; ++j) {
+    x_off[j] = 0;
+    x_inf[j] = 0;
+    if (j < APW) {
+      const int row = (wid + j * NW) * RPI + lane / 8;
+      const int tb = row / per_img, rem = row - tb * per_img;
+      const int hh = rem / W2, w = rem - hh * W2 - 1, dh = hh - 1;
+      const bool ok = row < hg.HROWS && tb < hg.TB && (unsigned)w < (unsigned)W;
+      x_off[j] = (tb * img + dh * W + w) * C + swz<BK>(row, lane % 8) * 8;
+      x_inf[j] = (ok ? 0x80000000u : 0u) | ((unsigned)tb << 16) | ((unsigned)(dh + 64) << 8);
+    }
+  }
+  auto tile_of = [&](int k) { return (int)blockIdx.x + k * G; };
+  auto stage = [&](int buf, int k) {
+    u16* As = Hs + buf * STAGE;
+    const int t = tile_of(k);
+    const bool live = k < nt;
+    const int m0 = t * BM;
+    const int b0 = m0 / img, h0 = (m0 - b0 * img) / W;
+#pragma unroll
+    for (int j = 0; j < kHpAPW; ++j) {
+      if (j < APW && (NS != 2 || wid + j * NW < hg.AINS)) {
+        const unsigned inf = x_inf[j];
+        const int tb = (int)((inf >> 16) & 0x7fff), dh = (int)((inf >> 8) & 255) - 64;
+        const bool ok = live && (inf >> 31) && b0 + tb < a.B && (unsigned)(h0 + dh) < (unsigned)H;
+        bdma16(rsA, ok ? 2u * (unsigned)(m0 * C + x_off[j]) : kOOB, As + (wid + j * NW) * 512);
+      }
+    }
+  };
+
+  int hrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = wid * (BM / NW) + i * 16 + (lane & 15);
+    const int tb = ml / (TH * W), r2 = ml - tb * TH * W;
+    const int th = r2 / W, tw = r2 - th * W;
+    hrow[i] = (tb * (TH + 2) + th) * W2 + tw;
+  }
+  const int rb = lane & 15;
+  f32x4 acc[TM][TN];
+  auto compute = [&](int buf) {
+    const u16* As = Hs + buf * STAGE;
+    // fragments prefetched PD steps ahead (PD = 2 when a step has <= 8 MFMAs:
+    // one step's MFMAs alone do not cover an LDS read round trip at 1 wave/SIMD)
+    constexpr int PD = (TM * TN <= 8 && NW == 4) ? 2 : 1, NB = PD + 1;
+    bf16x8 af[NB][TM], bw[NB][TN];
+    auto load = [&](int st, int slot) {
+      const int t = st / KS, ks = st % KS;
+      const int rowoff = (t / 3) * W2 + (t % 3);
+      const int wt = FLIP ? 8 - t : t;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = hrow[i] + rowoff;
+        af[slot][i] = *reinterpret_cast<const bf16x8*>(
+            As + row * BK + swz<BK>(row, ks * 4 + (lane >> 4)) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bw[slot][j] = *reinterpret_cast<const bf16x8*>(
+            Ws + (wt * BN + j * 16 + rb) * BK + swz<BK>(rb, ks * 4 + (lane >> 4)) * 8);
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) load(p, p);
+    __builtin_amdgcn_sched_group_barrier(0x100, PD * (TM + TN), 0);
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
+      if (st + PD < NSTEP) load(st + PD, (st + PD) % NB);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = mfma16(bw[st % NB][j], af[st % NB][i], acc[i][j]);
+      if (st + PD < NSTEP) {
+#pragma unroll
+        for (int k = 0; k < TM + TN && k < TM * TN; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if (TM * TN > TM + TN) __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
+      }
+    }
+  };
+
+  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+  float bj[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bj[j][r] = (!FLIP && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
+  }
+  float s_sum[TN][4], s_sq[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s_sum[j][r] = 0.f; s_sq[j][r] = 0.f; }
+  auto epilogue = [&](int k) {
+    const int m0 = tile_of(k) * BM;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wid * (BM / NW) + i * 16 + (lane & 15);
+      const bool mok = m < P;
+      const unsigned rowoff = 2u * (unsigned)(m * a.CO);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + j * 16 + 4 * (lane >> 4);
+        const bool ok = mok && n < a.CO;
+        u16 hv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = acc[i][j][r] + bj[j][r];
+          if (!FLIP && a.relu) t = fmaxf(t, 0.f);
+          hv[r] = f2bf(t);
+          if (STATS) {
+            const float v = ok ? bf2f(hv[r]) : 0.f;
+            s_sum[j][r] += v;
+            s_sq[j][r] += v * v;
+          }
+        }
+        const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
+        __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
+      }
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) stage(s, s);
+  const int vm_wait = (NS - 2) * APW;
+  for (int k = 0; k < nt; ++k) {
+    if (NS == 2) wait_vm<0>();
+    else wait_vm_n(vm_wait);            // tile k (and, at k = 0, the weights) landed ...
+    __builtin_amdgcn_s_barrier();       // ... for every wave; slot (k-1) % NS is free
+    asm volatile("" ::: "memory");
+    stage((k + NS - 1) % NS, k + NS - 1);
+    if (k > 0) epilogue(k - 1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    compute(k % NS);
+  }
+  epilogue(nt - 1);
+  if (STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s_sum[j][r] = row_sum16(s_sum[j][r]);
+        s_sq[j][r] = row_sum16(s_sq[j][r]);
+      }
+    wait_vm<0>();                        // the ring's trailing (zero) DMAs have landed
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(Hs);   // [NW][BN] sums, then [NW][BN] squares
+    if ((lane & 15) == 15) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = j * 16 + 4 * (lane >> 4) + r;
+          red[wid * BN + nl] = s_sum[j][r];
+          red[NW * BN + wid * BN + nl] = s_sq[j][r];
+        }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.CO) {
+      float ss = 0.f, qq = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) { ss += red[w * BN + tid]; qq += red[NW * BN + w * BN + tid]; }
+      const int slot = blockIdx.x % kBnSlots;
+      atomicAdd(a.part + (long long)slot * a.CO + n0 + tid, ss);
+      atomicAdd(a.part + (long long)(kBnSlots + slot) * a.CO + n0 + tid, qq);
+    }
+  }
+}
+
 // W[co][r][s][ci] -> Wt[ci][r][s][co]  (bf16)
 __global__ void __launch_bounds__(256) conv_weight_transpose_kernel(
     const u16* __restrict__ w, u16* __restrict__ wt, int CO, int RS, int CI) {
@@ -813,6 +1076,8 @@ static void dispatch(const ConvArgs& a, int cfg, int classes, hipStream_t s) {
   X(14, 512, 64, 32, 8, 1, 1)
 
 constexpr int kHaloBase = 100, kNumHaloConfigs = 15;
+// persistent 64-channel halo kernels (conv_halo64p_kernel): ids after the tile configs
+constexpr int kHaloPBase = kHaloBase + kNumHaloConfigs, kNumHaloPConfigs = 3;
 
 static bool halo_cfg(int cfg, int* bm, int* bn, int* bk, int* nw, int* ns) {
   switch (cfg - kHaloBase) {
@@ -853,13 +1118,57 @@ static bool halo_geom(int cfg, int H, int W, int C, int R, int S, int stride, in
   return true;
 }
 
+// persistent 64-channel halo ids kHaloPBase + i -> (BM, NS, waves)
+static const int kHaloP[3][3] = {{256, 2, 4}, {128, 3, 4}, {256, 2, 8}};
+
+static bool halop_geom(int cfg, int B, int H, int W, int C, int R, int S, int stride, int pad,
+                       HaloPGeom* g, int* bm_out, int* ns_out, int* nw_out, size_t* lds) {
+  const int id = cfg - kHaloPBase;
+  if (id < 0 || id >= kNumHaloPConfigs) return false;
+  const int bm = kHaloP[id][0], ns = kHaloP[id][1], nw = kHaloP[id][2];
+  if (R != 3 || S != 3 || stride != 1 || pad != 1 || C != 64) return false;
+  const int img = H * W;
+  HaloPGeom h{};
+  if (bm <= img) {
+    if (bm % W != 0 || img % bm != 0) return false;
+    h.TH = bm / W;
+    h.TB = 1;
+  } else {
+    if (bm % img != 0) return false;
+    h.TH = H;
+    h.TB = bm / img;
+  }
+  h.HROWS = h.TB * (h.TH + 2) * (W + 2);
+  h.AINS = (h.HROWS + 7) / 8;
+  h.APW = (h.AINS + nw - 1) / nw;
+  if (h.APW > kHpAPW || (ns - 2) * h.APW > 24) return false;
+  const long long P = (long long)B * img;
+  if (2LL * P * 64 >= (1LL << 31)) return false;
+  h.ntiles = (int)((P + bm - 1) / bm);
+  const size_t pieces = ns == 2 ? (size_t)h.AINS : (size_t)h.APW * nw;
+  const size_t bytes = 2 * ((size_t)9 * 64 * 64 + (size_t)ns * pieces * 8 * 64);
+  if (bytes > 160 * 1024) return false;
+  *g = h;
+  *bm_out = bm;
+  *ns_out = ns;
+  *nw_out = nw;
+  *lds = bytes;
+  return true;
+}
+
 bool conv_halo_ok(int cfg, int H, int W, int C, int R, int S, int stride, int pad) {
+  if (cfg >= kHaloPBase) {
+    HaloPGeom g;
+    int bm, ns, nw;
+    size_t lds;
+    return halop_geom(cfg, 1, H, W, C, R, S, stride, pad, &g, &bm, &ns, &nw, &lds);
+  }
   HaloGeom g;
   size_t lds;
   return halo_geom(cfg, H, W, C, R, S, stride, pad, &g, &lds);
 }
 
-int conv_num_halo_configs() { return kNumHaloConfigs; }
+int conv_num_halo_configs() { return kNumHaloConfigs + kNumHaloPConfigs; }
 int conv_halo_base() { return kHaloBase; }
 
 template <int BM, int BN, int BK, int WM, int WN, int NS, bool FLIP, bool STATS>
@@ -876,12 +1185,52 @@ static void launch_halo_t(const ConvArgs& a, const HaloGeom& g, size_t lds, hipS
   hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, a, g);
 }
 
+template <int BM, int NS, int NW, bool FLIP, bool STATS>
+static void launch_halop_t(const ConvArgs& a, const HaloPGeom& g, size_t lds, hipStream_t s) {
+  auto kern = conv_halo64p_kernel<BM, NS, NW, FLIP, STATS>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  // persistent: one block per CU (the resident weights + ring fill the LDS)
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int ny = (a.CO + 63) / 64;
+  int gx = (cus + ny - 1) / ny;
+  if (gx > g.ntiles) gx = g.ntiles;
+  hipLaunchKernelGGL(kern, dim3((unsigned)gx, (unsigned)ny), dim3(64 * NW), lds, s, a, g);
+}
+
 // true if launched (cfg is a halo config that applies to this geometry)
 template <bool FLIP, bool STATS>
 static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
   HaloGeom g;
   size_t lds;
   if (a.GH != a.OH || a.GW != a.OW) return false;
+  if (cfg >= kHaloPBase) {
+    HaloPGeom pg;
+    int bm, ns, nw;
+    size_t plds;
+    // a residual-gradient addend is not fused in the persistent kernel: take the
+    // 4-wave halo tile for those dgrads instead
+    if (FLIP && a.addend != nullptr)
+      return launch_halo<FLIP, STATS>(a, kHaloBase + 9, s) ||
+             launch_halo<FLIP, STATS>(a, kHaloBase + 5, s);
+    if (!halop_geom(cfg, a.B, a.GH, a.GW, a.CI, a.R, a.S, a.stride, a.pad, &pg, &bm, &ns, &nw,
+                    &plds))
+      return false;
+    if (nw == 8) launch_halop_t<256, 2, 8, FLIP, STATS>(a, pg, plds, s);
+    else if (bm == 256) launch_halop_t<256, 2, 4, FLIP, STATS>(a, pg, plds, s);
+    else launch_halop_t<128, 3, 4, FLIP, STATS>(a, pg, plds, s);
+    return true;
+  }
   if (!halo_geom(cfg, a.GH, a.GW, a.CI, a.R, a.S, a.stride, a.pad, &g, &lds)) return false;
   switch (cfg - kHaloBase) {
 #define X(i, BM, BN, BK, WM, WN, NS) \

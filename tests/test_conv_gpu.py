@@ -297,3 +297,44 @@ def test_resnet_block_alias_shortcut_grad(stride, cin, planes):
     yb = blk.bn2(blk.conv2(h), residual=sc)
     (yb.float() * g).sum().backward()
     assert _rel(x.grad, xb.grad) < 1e-2
+
+
+@pytest.mark.parametrize("stride,cin,planes", [(1, 256, 64), (2, 256, 128), (1, 64, 64)])
+def test_resnet_bottleneck_block_grad(stride, cin, planes):
+    """ResNet-50 Bottleneck (1x1 -> 3x3 -> 1x1, BN+ReLU fused, residual summed in
+    bn3 and the shortcut gradient in conv1's dgrad) on the native path vs an fp32
+    functional reference: identity shortcut, strided projection, widening
+    projection."""
+    from distributed_ml_pytorch_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(0)
+    blk = Bottleneck(cin, planes, stride).cuda()
+    x = torch.randn(4, cin, 14, 14, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=CL).requires_grad_(True)
+    y = blk(x)
+    g = torch.randn(y.shape, device="cuda")
+    (y.float() * g).sum().backward()
+
+    def w(conv):
+        return conv.weight.detach().to(torch.bfloat16).float()
+
+    def bn(t, m):
+        return F.batch_norm(t, None, None, m.weight.detach(), m.bias.detach(), True, 0.1, m.eps)
+
+    xr = x.detach().float().requires_grad_(True)
+    h = F.relu(bn(F.conv2d(xr, w(blk.conv1)), blk.bn1))
+    h = F.relu(bn(F.conv2d(h, w(blk.conv2), None, stride, 1), blk.bn2))
+    sc = xr if blk.shortcut is None else bn(F.conv2d(xr, w(blk.shortcut[0]), None, stride),
+                                            blk.shortcut[1])
+    yr = F.relu(bn(F.conv2d(h, w(blk.conv3)), blk.bn3) + sc)
+    (yr * g).sum().backward()
+    assert _rel(y, yr) < 3e-2
+    assert _rel(x.grad, xr.grad) < 8e-2      # three bf16 conv+BN levels deep
+    for conv in (blk.conv1, blk.conv2, blk.conv3):
+        assert torch.isfinite(conv.weight.grad).all()
+    # weight gradient of the last conv (one level deep) against the oracle
+    wr3 = w(blk.conv3).requires_grad_(True)
+    h2 = h.detach()
+    yr3 = F.relu(bn(F.conv2d(h2, wr3), blk.bn3) + sc.detach())
+    (yr3 * g).sum().backward()
+    assert _rel(blk.conv3.weight.grad, wr3.grad) < 6e-2
