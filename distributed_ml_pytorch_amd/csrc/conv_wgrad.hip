@@ -316,11 +316,18 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
   }
 }
 
-template <int BM, int NS, int TR>
-__global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, WgradHaloGeom hg,
-                                                              int atomic) {
-  constexpr int NW = 4, CW = 64;                  // 64-channel rows (128 B)
-  constexpr int D_PW = BM / 32;                   // dY DMA instructions per wave per tile
+// PG = 2: 8 waves in two pixel groups.  Group g (waves 4g..4g+3) owns the
+// same 64 x 16-column slices as the 4-wave block but only pk steps
+// [g * NPK / 2, (g+1) * NPK / 2) of every tile; at the end group 1 parks its
+// accumulators in LDS and group 0 adds them before the single atomic flush.
+// One such block per CU replaces two 4-wave blocks: the same two waves per
+// SIMD, half the fp32 partials through the memory-side atomic units (~1.3
+// TB/s chip-wide, ~25 % of the 4-wave kernel's time: profiles/conv_kernels_r2.txt).
+template <int BM, int NS, int TR, int PG = 1>
+__global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, WgradHaloGeom hg,
+                                                                   int atomic) {
+  constexpr int NW = 4 * PG, CW = 64;             // 64-channel rows (128 B)
+  constexpr int D_PW = BM / 8 / NW;               // dY DMA instructions per wave per tile
   constexpr int NT = 3 * TR;                      // taps per block
   extern __shared__ __attribute__((aligned(16))) u16 lds_w[];
   const int XPW = hg.XPW;
@@ -329,6 +336,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, Wgrad
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid & 3, grp = wid >> 2;         // column slice, pixel group
   // XCD-aware bijective remap: consecutive logical blocks (the (ci, co, r)
   // tiles of one pixel split) land on one XCD under round-robin dispatch
   const int nx = gridDim.x, ny = gridDim.y, G = nx * ny * gridDim.z;
@@ -403,12 +411,12 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, Wgrad
 
   // staged X row of the lane's reduction rows (pixels pk*32 + 8g + q and +4), tap (0, 0)
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pc = li & 3;
-  int xr_lo[BM / 32], xr_hi[BM / 32];
+  int xr_lo[BM / 32 / PG], xr_hi[BM / 32 / PG];
 #pragma unroll
-  for (int pk = 0; pk < BM / 32; ++pk) {
+  for (int pk = 0; pk < BM / 32 / PG; ++pk) {
 #pragma unroll
     for (int hsel = 0; hsel < 2; ++hsel) {
-      const int pl = pk * 32 + 8 * g + q + 4 * hsel;
+      const int pl = (grp * (BM / 32 / PG) + pk) * 32 + 8 * g + q + 4 * hsel;
       const int tb = pl / (TH * W), r2 = pl - tb * TH * W;
       const int th = r2 / W, tw = r2 - th * W;
       const int xr = (tb * THX + th) * W2 + tw;
@@ -433,9 +441,10 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, Wgrad
   auto compute = [&](int buf) {
     const u16* Ds = lds_w + buf * STAGE;
     const u16* Xs = Ds + D_EL;
-    constexpr int NPK = BM / 32, NRD = 8 + 6 * TR, NMF = 12 * TR;
+    constexpr int NPK = BM / 32 / PG, NRD = 8 + 6 * TR, NMF = 12 * TR;
     bf16x8 af[2][4], bx[2][3 * TR];
-    auto load = [&](int pk, int slot) {
+    auto load = [&](int pkl, int slot) {
+      const int pk = grp * NPK + pkl;   // this group's share of the tile
       const int drow = pk * 32 + 8 * g + q;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -446,8 +455,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, Wgrad
       for (int r = 0; r < TR; ++r)
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
-          const s16x4_t lo = tr(Xs, xr_lo[pk] + r * W2 + s, wid * 16 + 4 * pc);
-          const s16x4_t hi = tr(Xs, xr_hi[pk] + r * W2 + s, wid * 16 + 4 * pc);
+          const s16x4_t lo = tr(Xs, xr_lo[pkl] + r * W2 + s, wc * 16 + 4 * pc);
+          const s16x4_t hi = tr(Xs, xr_hi[pkl] + r * W2 + s, wc * 16 + 4 * pc);
           bx[slot][r * 3 + s] =
               __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
@@ -488,9 +497,29 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, Wgrad
     compute(it % NS);
   }
   wait_vm<0>();
+  if constexpr (PG == 2) {
+    // group 1 parks its partial sums in LDS (the staging ring is drained and
+    // every wave is past its last read after the barrier), group 0 adds them
+    __syncthreads();
+    float* park = reinterpret_cast<float*>(lds_w);   // [4 waves][NT*4][64 lanes] f32x4
+    if (grp == 1) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<f32x4*>(park + ((wc * NT * 4 + t * 4 + i) * 64 + lane) * 4) = acc[t][i];
+    }
+    __syncthreads();
+    if (grp == 1) return;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[t][i] += *reinterpret_cast<const f32x4*>(park + ((wc * NT * 4 + t * 4 + i) * 64 + lane) * 4);
+  }
   // D layout: lane holds rows co = 4*(lane>>4)+rr of column ci = lane & 15
   const long long K = 9LL * C;
-  const int ci = ci0 + wid * 16 + (lane & 15);
+  const int ci = ci0 + wc * 16 + (lane & 15);
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -509,18 +538,20 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(WgradArgs a, Wgrad
 // target block count 128 << spl; variant -> (NS, TR) below (ids 1000..1011 are
 // the round-1 kernel's configs: NS 2, one tap row per block)
 constexpr int kWhBase = 1000;
-constexpr int kWhVariants = 5;
-constexpr int kWhNS[kWhVariants] = {2, 3, 4, 2, 3};
-constexpr int kWhTR[kWhVariants] = {1, 1, 1, 3, 3};
+constexpr int kWhVariants = 6;
+constexpr int kWhNS[kWhVariants] = {2, 3, 4, 2, 3, 2};
+constexpr int kWhTR[kWhVariants] = {1, 1, 1, 3, 3, 1};
+constexpr int kWhPG[kWhVariants] = {1, 1, 1, 1, 1, 2};   // pixel groups (8 waves when 2)
 
 static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R, int S, int stride,
                             int pad, WgradHaloGeom* g, int* bm_out, int* ns_out, int* tr_out,
-                            size_t* lds, int* splits) {
+                            int* pg_out, size_t* lds, int* splits) {
   const int id = cfg - kWhBase;
   if (id < 0 || id >= 12 * kWhVariants) return false;
   const int var = id / 12, rest = id % 12;
   const int bm = 64 << (rest / 4), target = 128 << (rest % 4);
-  const int ns = kWhNS[var], tr = kWhTR[var];
+  const int ns = kWhNS[var], tr = kWhTR[var], pg = kWhPG[var];
+  if (pg == 2 && bm < 128) return false;
   if (R != 3 || S != 3 || stride != 1 || pad != 1 || CI % 64 || CO % 64) return false;
   if (tr == 3 && bm > 128) return false;   // 36 accumulator tiles + hoisted addresses spill
   const int img = H * W;
@@ -536,7 +567,7 @@ static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R,
   }
   h.THX = h.TH + tr - 1;
   h.XROWS = h.TB * h.THX * (W + 2);
-  h.XPW = ((h.XROWS + 7) / 8 + 3) / 4;
+  h.XPW = ((h.XROWS + 7) / 8 + 4 * pg - 1) / (4 * pg);
   if (h.XPW > kWhXPW || h.THX + 1 > 127 || h.TB > 0x7fff) return false;
   if ((ns - 2) * (bm / 32 + h.XPW) > 40) return false;
   const long long M = (long long)B * img;
@@ -548,13 +579,14 @@ static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R,
   if (sp > h.ntiles) sp = h.ntiles;
   h.tiles_per_split = (h.ntiles + sp - 1) / sp;
   sp = (h.ntiles + h.tiles_per_split - 1) / h.tiles_per_split;
-  const size_t stage = (size_t)bm * 64 + (size_t)h.XPW * 4 * 512;
+  const size_t stage = (size_t)bm * 64 + (size_t)h.XPW * 4 * pg * 512;
   *lds = (size_t)ns * stage * 2;
   if (*lds > 160 * 1024) return false;
   *g = h;
   *bm_out = bm;
   *ns_out = ns;
   *tr_out = tr;
+  *pg_out = pg;
   *splits = sp;
   return true;
 }
@@ -562,20 +594,21 @@ static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R,
 bool conv_wgrad_halo_ok(int cfg, int B, int H, int W, int CI, int CO, int R, int S, int stride,
                         int pad) {
   WgradHaloGeom g;
-  int bm, ns, tr, sp;
+  int bm, ns, tr, pg, sp;
   size_t lds;
-  return wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &lds, &sp);
+  return wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &pg, &lds,
+                         &sp);
 }
 int conv_wgrad_halo_base() { return kWhBase; }
 int conv_wgrad_num_halo_configs() { return 12 * kWhVariants; }
 
-template <int BM, int NS, int TR>
+template <int BM, int NS, int TR, int PG = 1>
 static void launch_wgrad_halo_t(const WgradArgs& a, const WgradHaloGeom& g, size_t lds, int splits,
                                 hipStream_t s) {
   static bool attr = false;
   static int diag = -1;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<BM, NS, TR>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<BM, NS, TR, PG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
@@ -584,7 +617,7 @@ static void launch_wgrad_halo_t(const WgradArgs& a, const WgradHaloGeom& g, size
     diag = (e && e[0] == 's') ? 1 : 0;
   }
   const dim3 grid((unsigned)(a.CI / 64), (unsigned)(a.CO / 64 * (3 / TR)), (unsigned)splits);
-  hipLaunchKernelGGL((conv_wgrad_halo_kernel<BM, NS, TR>), grid, dim3(256), lds, s, a, g,
+  hipLaunchKernelGGL((conv_wgrad_halo_kernel<BM, NS, TR, PG>), grid, dim3(256 * PG), lds, s, a, g,
                      diag ? 2 : (splits > 1 ? 1 : 0));
 }
 
@@ -617,10 +650,14 @@ void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int
               dbias};
   if (cfg >= kWhBase && dbias == nullptr) {
     WgradHaloGeom g;
-    int bm, ns, tr, sp;
+    int bm, ns, tr, pg, sp;
     size_t lds;
-    if (wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &lds, &sp)) {
-      if (tr == 3) {
+    if (wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &pg, &lds,
+                        &sp)) {
+      if (pg == 2) {
+        if (bm == 128) launch_wgrad_halo_t<128, 2, 1, 2>(a, g, lds, sp, s);
+        else launch_wgrad_halo_t<256, 2, 1, 2>(a, g, lds, sp, s);
+      } else if (tr == 3) {
         if (ns == 2) launch_wgrad_halo_bm<2, 3>(bm, a, g, lds, sp, s);
         else launch_wgrad_halo_bm<3, 3>(bm, a, g, lds, sp, s);
       } else {

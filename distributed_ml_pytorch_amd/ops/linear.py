@@ -113,9 +113,21 @@ def _small_splits(mode: int, K: int) -> int:
     return max(1, min(1023, K // 256)) if mode == 2 else 1
 
 
+def _small_split_options(mode: int, K: int):
+    """Split-K counts of the any-shape kernel worth timing in wgrad mode: the
+    default (~256 rows per split) and finer ones.  A classifier head's weight
+    gradient (10 x 512 over a batch of 512) is 8 output tiles; with 2 splits its
+    16 blocks walk 8 serial k-stages each and the launch is latency-bound
+    (52 us per ResNet-18 step); 16-64 splits finish in one or two stages."""
+    if mode != 2:
+        return [1]
+    return sorted({_small_splits(mode, K)} |
+                  {max(1, min(1023, K // r)) for r in (32, 64, 128)})
+
+
 def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bool):
     if not ok:
-        return [_enc(_SMALL, _small_splits(mode, K))]
+        return [_enc(_SMALL, s) for s in _small_split_options(mode, K)]
     cands = []
     for c in native().gemm_configs():
         cid, bm, bn = c[0], c[1], c[2]
@@ -126,7 +138,7 @@ def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bo
         else:
             cands.append(_enc(cid, 1))
     if M * N * K < (1 << 22):
-        cands.append(_enc(_SMALL, _small_splits(mode, K)))
+        cands += [_enc(_SMALL, s) for s in _small_split_options(mode, K)]
     if _GEMM_MODE == "auto" and plain and mode in (0, 1):
         cands.append(_BLAS)
     return cands

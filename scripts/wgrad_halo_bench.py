@@ -13,7 +13,7 @@ from distributed_ml_pytorch_amd.ops._ext import native
 from distributed_ml_pytorch_amd.ops.conv import _wgrad_candidates
 
 CL = torch.channels_last
-VARIANTS = {0: "NS2 TR1", 1: "NS3 TR1", 2: "NS4 TR1", 3: "NS2 TR3", 4: "NS3 TR3"}
+VARIANTS = {0: "NS2 TR1", 1: "NS3 TR1", 2: "NS4 TR1", 3: "NS2 TR3", 4: "NS3 TR3", 5: "NS2 TR1 PG2"}
 
 
 def t_us(fn, it=10, rounds=3):
