@@ -97,7 +97,9 @@ def test_native_rejects_bad_shapes(nat):
 @pytest.mark.parametrize("B,C,dtype,ls", [(64, 10, torch.bfloat16, 0.0), (256, 10, torch.float32, 0.0),
                                           (1000, 1000, torch.bfloat16, 0.0), (3, 130, torch.float32, 0.0),
                                           (2500, 10, torch.bfloat16, 0.0), (512, 32, torch.float32, 0.1),
-                                          (300, 33, torch.float32, 0.1), (77, 1, torch.float32, 0.0)])
+                                          (300, 33, torch.float32, 0.1), (77, 1, torch.float32, 0.0),
+                                          (128, 1000, torch.bfloat16, 0.1), (8, 1000, torch.float32, 0.0),
+                                          (40, 2000, torch.bfloat16, 0.0), (10, 1500, torch.float32, 0.0)])
 def test_softmax_xent(B, C, dtype, ls):
     from distributed_ml_pytorch_amd.ops.functional import softmax_cross_entropy
 
