@@ -694,7 +694,7 @@ int64_t mat_ld(const Tensor& t, at::ScalarType dt, int64_t rows, int64_t cols,
 // mode 1: a [M,K], b [K,N]; mode 2: a [K,M], b [K,N], c fp32 accumulated.
 void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
           optional<Tensor> c2, optional<Tensor> bias, optional<Tensor> aux,
-          optional<Tensor> dbias, int64_t splits, bool relu) {
+          optional<Tensor> dbias, int64_t splits, bool relu, optional<Tensor> part) {
   TORCH_CHECK(!relu || epi == 0, "gemm: relu only with the store epilogue");
   TORCH_CHECK(mode >= 0 && mode <= 2, "gemm: mode must be 0 (fwd), 1 (dgrad) or 2 (wgrad)");
   TORCH_CHECK(c.dim() == 2 && a.dim() == 2 && b.dim() == 2, "gemm: 2-D operands expected");
@@ -745,6 +745,12 @@ void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
                 "gemm: dbias must be a contiguous fp32 [M] GPU tensor");
     dbp = dbias->data_ptr<float>();
   }
+  float* partp = nullptr;
+  if (part.has_value() && part->defined()) {
+    TORCH_CHECK(epi == 0 && cfg >= 0, "gemm: BN partial sums need the MFMA store epilogue");
+    TORCH_CHECK(N % 8 == 0 && ldc % 8 == 0, "gemm: BN partial sums need N % 8 == 0");
+    partp = bn_slots(part, N, c.options()).data_ptr<float>();
+  }
   if (cfg >= 0) {
     // MFMA tiles: 16-B DMA pieces along k (row-major operand) or along the
     // row (k-strided operand), 8-B bf16x4 output stores
@@ -771,7 +777,7 @@ void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
   dmp::launch_gemm((int)mode, (int)epi, (int)cfg, reinterpret_cast<const uint16_t*>(a.data_ptr()),
                    (int)lda, reinterpret_cast<const uint16_t*>(b.data_ptr()), (int)ldb,
                    c.data_ptr(), (int)ldc, c2p, biasp, auxp, dbp, (int)M, (int)N, (int)K,
-                   (int)std::max<int64_t>(1, splits), cur_stream(), relu);
+                   (int)std::max<int64_t>(1, splits), cur_stream(), relu, partp);
 }
 
 std::vector<std::vector<int64_t>> gemm_configs() {
@@ -1101,7 +1107,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("gemm", &gemm, "bf16 MFMA GEMM (fwd / dgrad / wgrad modes, fused epilogues)",
         py::arg("mode"), py::arg("epi"), py::arg("cfg"), py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("c2") = py::none(), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
-        py::arg("dbias") = py::none(), py::arg("splits") = 1, py::arg("relu") = false);
+        py::arg("dbias") = py::none(), py::arg("splits") = 1, py::arg("relu") = false,
+        py::arg("part") = py::none());
   m.def("im2col", &im2col, "NHWC patch rows [B*OH*OW, Kp], k = (r, s, ci), zero-padded",
         py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));
   m.def("col2im", &col2im, "gather-form inverse of im2col -> channels_last dX", py::arg("dcols"),

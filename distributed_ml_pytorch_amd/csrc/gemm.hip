@@ -62,6 +62,8 @@ struct GemmArgs {
   int k_chunk;        // reduction rows per blockIdx.y (split-K), multiple of BK
   int tiles_n;
   int relu;           // EPI_STORE: max(0, .) after bias / addend (linear -> ReLU)
+  float* part;        // EPI_STORE: optional BatchNorm slot sums [2][kBnSlots][N] of the
+                      // stored bf16 outputs (a 1x1 conv feeding a BatchNorm)
 };
 
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -331,6 +333,11 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
       const int lrow = lane / CPR, ch = lane - lrow * CPR;
       const bool lane_on = lrow < RPI;
       const int n = n0 + rb + ch * 8;
+      // BN partial sums of the stored values, per column (EPI_STORE, 16-B path)
+      const bool stats = EPI == EPI_STORE && g.part != nullptr;
+      float s_sum[8], s_sq[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s_sum[e] = 0.f; s_sq[e] = 0.f; }
       // an output width / row stride that is not whole 16-B pieces (10-class
       // heads, LeNet's 84 / 6 / 16 columns) is stored element by element
       const bool narrow = ((g.N | g.ldc) & 7) != 0;
@@ -396,6 +403,14 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
             out.v[e] = f2bf(a * d);
           }
         }
+        if (stats && o[q] != kOOBg) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float yv = bf2f(out.v[e]);
+            s_sum[e] += yv;
+            s_sq[e] += yv * yv;
+          }
+        }
         if (!narrow) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, out), rsC, o[q], 0,
                                                  0);
@@ -409,6 +424,27 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
               __builtin_amdgcn_raw_buffer_store_b16(out.v[e], rsC, o[q] + 2u * e, 0, 0);
               if constexpr (EPI == EPI_GELU)
                 __builtin_amdgcn_raw_buffer_store_b16(out2.v[e], rsC2, o[q] + 2u * e, 0, 0);
+            }
+          }
+        }
+      }
+      if (stats) {
+        // the RPI row lanes of each 8-column segment, then one atomic per
+        // column per wave into slot (block % kBnSlots)
+#pragma unroll
+        for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s_sum[e] += __shfl_xor(s_sum[e], off, 64);
+            s_sq[e] += __shfl_xor(s_sq[e], off, 64);
+          }
+        if (lrow == 0) {
+          const int slot = (int)(blockIdx.x % kBnSlots);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            if (n + e < g.N) {
+              atomicAdd(g.part + (long long)slot * g.N + n + e, s_sum[e]);
+              atomicAdd(g.part + (long long)(kBnSlots + slot) * g.N + n + e, s_sq[e]);
             }
           }
         }
@@ -624,9 +660,10 @@ void gemm_config_info(int cfg, int* info) {
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
-                 hipStream_t s, bool relu) {
+                 hipStream_t s, bool relu, float* part) {
   GemmArgs g{};
   g.relu = relu ? 1 : 0;
+  g.part = part;
   g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.aux = aux; g.dbias = dbias;
   g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   if (splits < 1 || mode != 2) splits = 1;   // split-K only for the fp32-accumulating pass

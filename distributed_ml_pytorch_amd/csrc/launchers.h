@@ -152,7 +152,7 @@ void gemm_config_info(int cfg, int* info);   // {BM, BN, threads, stages, BK}
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
-                 hipStream_t s, bool relu = false);
+                 hipStream_t s, bool relu = false, float* part = nullptr);
 
 // im2col.hip: patch matrix [B*OH*OW][Kp] (k = (r, s, ci), zero-padded) and its
 // gather-form inverse; ReLU backward from the saved output

@@ -128,11 +128,75 @@ def _halo_candidates(H, W, C, R, S, stride, pad):
     return list(native().conv_halo_configs(H, W, C, R, S, stride, pad))
 
 
+# ---------------------------------------------- 1x1 / stride-1 convs as GEMMs
+# A 1x1 stride-1 unpadded conv over channels_last NHWC rows IS a GEMM:
+#   fwd   Y[m][co] = X[m][:] . W[co][:]     (csrc/gemm.hip mode 0, + BN partial
+#                                            sums of the stored outputs)
+#   dgrad dX = dY W                         (mode 1, + the shortcut-alias addend)
+#   wgrad dW += dY^T X                      (mode 2, fp32 into the arena view)
+# The MFMA GEMM reaches 800-1000 TF/s on these shapes where the implicit-GEMM
+# conv tiles (built around the tap gather) stay at 500-700
+# (profiles/gemm_vs_hipblaslt_r2.txt, linear_vs_conv1x1_r1.txt): the route is a
+# tuner candidate (_GEMM_ROUTE) next to the conv tiles for every such layer
+# (the ResNet-50 bottleneck's 1x1 convs).
+_GEMM_ROUTE = 30000
+_GEMM_1X1 = os.environ.get("DMP_CONV_GEMM1X1", "1") != "0"
+
+
+def _gemm1x1_ok(w_shape, stride, pad, ci, co) -> bool:
+    return (_GEMM_1X1 and tuple(w_shape[2:]) == (1, 1) and stride == 1 and pad == 0
+            and ci % 8 == 0 and co % 8 == 0)
+
+
+def _rows_nhwc(t):
+    """[B, C, H, W] channels_last -> its [B*H*W, C] row view (no copy)."""
+    t = t.contiguous(memory_format=torch.channels_last)
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def _gemm1x1_fwd(x, w16, part=None, relu=False):
+    from .linear import gemm
+
+    B, CI, H, W = x.shape
+    CO = w16.shape[0]
+    y2 = torch.empty(B * H * W, CO, dtype=x.dtype, device=x.device)
+    gemm(0, 0, _rows_nhwc(x), w16.reshape(CO, CI), y2, relu=relu, part=part)
+    return y2.view(B, H, W, CO).permute(0, 3, 1, 2)
+
+
+def _gemm1x1_dgrad(dy, w16, addend=None):
+    from .linear import gemm
+
+    B, CO, H, W = dy.shape
+    CI = w16.shape[1]
+    dx2 = torch.empty(B * H * W, CI, dtype=dy.dtype, device=dy.device)
+    aux = _rows_nhwc(addend) if addend is not None else None
+    gemm(1, 0, _rows_nhwc(dy), w16.reshape(CO, CI), dx2, aux=aux)
+    return dx2.view(B, H, W, CI).permute(0, 3, 1, 2)
+
+
+def _gemm1x1_wgrad(dy, x, g):
+    """g: fp32 [CO, CI, 1, 1] (channels_last) accumulated in place."""
+    from .linear import gemm
+
+    gemm(2, 3, _rows_nhwc(dy), _rows_nhwc(x), g.reshape(g.shape[0], g.shape[1]))
+
+
 def _fwd_cfg(x, w16, stride, pad):
     key = ("fwd", *x.shape, w16.shape[0], w16.shape[2], w16.shape[3], stride, pad)
     cands = _igemm_candidates(w16.shape[0]) + _halo_candidates(
         x.shape[2], x.shape[3], x.shape[1], w16.shape[2], w16.shape[3], stride, pad)
-    return TUNER.best(key, lambda c: native().conv_fwd(x, w16, stride, pad, True, c), cands)
+    if _gemm1x1_ok(w16.shape, stride, pad, x.shape[1], w16.shape[0]):
+        cands.append(_GEMM_ROUTE)
+
+    def run(c):
+        if c == _GEMM_ROUTE:
+            part = torch.zeros(2 * BN_SLOTS * w16.shape[0] + BN_TAIL, dtype=torch.float32,
+                               device=x.device)
+            _gemm1x1_fwd(x, w16, part)
+        else:
+            native().conv_fwd(x, w16, stride, pad, True, c)
+    return TUNER.best(key, run, cands)
 
 
 def _dgrad_cfg(dy, w16, H, W, stride, pad):
@@ -140,7 +204,15 @@ def _dgrad_cfg(dy, w16, H, W, stride, pad):
     cands = _igemm_candidates(w16.shape[1])
     if (H, W) == tuple(dy.shape[2:]):
         cands += _halo_candidates(H, W, dy.shape[1], w16.shape[2], w16.shape[3], stride, pad)
-    return TUNER.best(key, lambda c: native().conv_dgrad(dy, w16, H, W, stride, pad, c), cands)
+    if _gemm1x1_ok(w16.shape, stride, pad, w16.shape[1], w16.shape[0]):
+        cands.append(_GEMM_ROUTE)
+
+    def run(c):
+        if c == _GEMM_ROUTE:
+            _gemm1x1_dgrad(dy, w16)
+        else:
+            native().conv_dgrad(dy, w16, H, W, stride, pad, c)
+    return TUNER.best(key, run, cands)
 
 
 def _wgrad_cfg(dy, x, shape, stride, pad):
@@ -155,7 +227,15 @@ def _wgrad_cfg(dy, x, shape, stride, pad):
         cands += list(native().conv_wgrad_halo_configs(x.shape[0], x.shape[2], x.shape[3],
                                                        shape[1], shape[0], shape[2], shape[3],
                                                        stride, pad))
-    return TUNER.best(key, lambda c: native().conv_wgrad(dy, x, scratch, stride, pad, c), cands)
+    if _gemm1x1_ok(shape, stride, pad, shape[1], shape[0]):
+        cands.append(_GEMM_ROUTE)
+
+    def run(c):
+        if c == _GEMM_ROUTE:
+            _gemm1x1_wgrad(dy, x, scratch)
+        else:
+            native().conv_wgrad(dy, x, scratch, stride, pad, c)
+    return TUNER.best(key, run, cands)
 
 
 class _NativeConv(Function):
@@ -172,7 +252,17 @@ class _NativeConv(Function):
             if b32.dtype != torch.float32 or not b32.is_contiguous():
                 b32 = b32.float().contiguous()
         ctx.bias = bias
-        y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats, cfg, slots, b32, relu)
+        if cfg == _GEMM_ROUTE and b32 is not None:
+            cfg = -1                     # the GEMM store epilogue takes no fp32 conv bias
+        if cfg == _GEMM_ROUTE:
+            part = None
+            if want_stats:
+                part = slots if slots is not None else torch.zeros(
+                    2 * BN_SLOTS * w16.shape[0] + BN_TAIL, dtype=torch.float32, device=x.device)
+            y = _gemm1x1_fwd(x, w16, part, relu)
+        else:
+            y, part, _ = native().conv_fwd(x, w16, stride, pad, want_stats, cfg, slots, b32,
+                                           relu)
         # ReLU fused in the epilogue; its backward masks dY by the saved output
         ctx.save_for_backward(x, w16, y if relu else None)
         ctx.master = master
@@ -198,7 +288,9 @@ class _NativeConv(Function):
             dy = native().relu_bwd(dy, y)
         dx = None
         master = ctx.master
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and _dgrad_cfg(dy, w16, H, W, stride, pad) == _GEMM_ROUTE:
+            dx = _gemm1x1_dgrad(dy, w16, dxa)
+        elif ctx.needs_input_grad[0]:
             cfg = _dgrad_cfg(dy, w16, H, W, stride, pad)
             wt = None
             ref = getattr(master, "_dmp_arena_ref", None)
@@ -213,7 +305,20 @@ class _NativeConv(Function):
         if master is not None and master.requires_grad:
             wcfg = _wgrad_cfg(dy, x, tuple(master.shape), stride, pad)
             g = master.grad if getattr(master, "_dmp_arena", False) else None
-            if g is not None and g.is_contiguous(memory_format=torch.channels_last):
+            if wcfg == _GEMM_ROUTE:
+                gg = g if g is not None and g.is_contiguous(
+                    memory_format=torch.channels_last) else None
+                if gg is None:
+                    gw = torch.zeros(tuple(master.shape), dtype=torch.float32, device=x.device)
+                    gw = gw.contiguous(memory_format=torch.channels_last)
+                    _gemm1x1_wgrad(dy, x, gw)
+                    gw = gw.to(master.dtype)
+                else:
+                    _gemm1x1_wgrad(dy, x, gg)
+                    cb = getattr(master, "_dmp_grad_ready", None)
+                    if cb is not None:
+                        cb(master)
+            elif g is not None and g.is_contiguous(memory_format=torch.channels_last):
                 cb = getattr(master, "_dmp_grad_ready", None)
                 if cb is None and _WG_STREAM_ENABLED:
                     _side_wgrad(x.device, lambda: native().conv_wgrad(dy, x, g, stride, pad, wcfg),

@@ -163,23 +163,29 @@ def _blas(mode, a, b, c, bias):
         torch.mm(a, b, out=c)
 
 
-def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None, relu=False):
+def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None, relu=False,
+         part=None):
     """C = epilogue(A(m,k) B(n,k)) on the native kernels (see csrc/gemm.hip):
     mode 0 fwd (a [M,K], b [N,K]), 1 dgrad (a [M,K], b [K,N]), 2 wgrad (a [K,M],
     b [K,N], fp32 c accumulated); epi 0 store(+bias,+aux), 1 GELU, 2 x gelu'(aux),
-    3 fp32 accumulate (+dbias)."""
+    3 fp32 accumulate (+dbias).  ``part``: BatchNorm slot sums [2][64][N] of the
+    stored outputs (epi 0, MFMA tiles; a 1x1 conv feeding a BatchNorm)."""
     M, N = c.shape
     K = a.shape[0] if mode == 2 else a.shape[1]
     if M == 0 or N == 0:
         return
     # outputs / aux of any row stride: the epilogues fall back to element access
     ok = _mfma_ok(mode, M, N, K, a, b)
-    plain = epi == 0 and aux is None and not relu
+    plain = epi == 0 and aux is None and not relu and part is None
     key = ("gemm", mode, epi, M, N, K, bias is not None, aux is not None, dbias is not None,
-           bool(relu))
+           bool(relu)) + (("stats",) if part is not None else ())
     pick = TUNER.cache.get(key)
     if pick is None:
         cands = _candidates(mode, epi, M, N, K, plain, ok)
+        if part is not None:
+            if not ok:
+                raise ValueError("gemm: BN partial sums need MFMA-compatible operands")
+            cands = [e for e in cands if e != _BLAS and _dec(e)[0] >= 0]
         if len(cands) == 1:
             pick = cands[0]
         else:
@@ -194,7 +200,9 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
                     _blas(mode, a, b, cs, bias)
                 else:
                     cfg_e, split_e = _dec(e)
-                    native().gemm(mode, epi, cfg_e, a, b, cs, c2, bias, aux, ds, split_e, relu)
+                    ps = torch.zeros_like(part) if part is not None else None
+                    native().gemm(mode, epi, cfg_e, a, b, cs, c2, bias, aux, ds, split_e, relu,
+                                  ps)
             pick = TUNER.best(key, run, cands)
             if pick == -1:
                 pick = _default(mode, M, N, K, ok)
@@ -202,7 +210,7 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
         _blas(mode, a, b, c, bias)
         return
     cfg, splits = _dec(pick)
-    native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits, relu)
+    native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits, relu, part)
 
 
 def _rows(t, k):

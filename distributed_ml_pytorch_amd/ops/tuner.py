@@ -19,7 +19,7 @@ import threading
 
 import torch
 
-_lock = threading.Lock()
+_lock = threading.RLock()   # a candidate may tune an inner kernel (1x1 conv -> GEMM)
 
 
 class KernelTuner:

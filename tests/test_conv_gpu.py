@@ -338,3 +338,51 @@ def test_resnet_bottleneck_block_grad(stride, cin, planes):
     yr3 = F.relu(bn(F.conv2d(h2, wr3), blk.bn3) + sc.detach())
     (yr3 * g).sum().backward()
     assert _rel(blk.conv3.weight.grad, wr3.grad) < 6e-2
+
+
+def test_conv1x1_gemm_route(monkeypatch):
+    """1x1 / stride-1 convs routed to the MFMA GEMM (ops/conv.py _GEMM_ROUTE):
+    forward + BN partial sums from the GEMM store epilogue, data gradient (+ the
+    shortcut-alias addend), weight gradient accumulated in fp32 -- helpers and
+    the full layer with the route forced, vs fp32."""
+    from distributed_ml_pytorch_amd.ops import conv as C
+    from distributed_ml_pytorch_amd.ops import layers as L
+
+    torch.manual_seed(0)
+    B, CI, H, W, CO = 8, 256, 14, 14, 64
+    x = torch.randn(B, CI, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(CO, CI, 1, 1, device="cuda") / CI ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr.backward(dy.float())
+    part = torch.zeros(2 * C.BN_SLOTS * CO + C.BN_TAIL, device="cuda")
+    y = C._gemm1x1_fwd(x, w, part)
+    assert y.is_contiguous(memory_format=CL)
+    assert _rel(y, yr) < 1e-2
+    ps = part[:2 * C.BN_SLOTS * CO].view(2, C.BN_SLOTS, CO).sum(1)
+    yf = y.float()
+    torch.testing.assert_close(ps[0], yf.sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(ps[1], (yf * yf).sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+    dx = C._gemm1x1_dgrad(dy, w)
+    assert _rel(dx, xr.grad) < 1e-2
+    add = torch.randn_like(x)
+    assert _rel(C._gemm1x1_dgrad(dy, w, add), xr.grad + add.float()) < 1e-2
+    g = torch.zeros(CO, CI, 1, 1, device="cuda").contiguous(memory_format=CL)
+    C._gemm1x1_wgrad(dy, x, g)
+    assert _rel(g, wr.grad) < 1e-2
+    # the whole layer with every pass forced onto the GEMM route
+    monkeypatch.setattr(C, "_fwd_cfg", lambda *a: C._GEMM_ROUTE)
+    monkeypatch.setattr(C, "_dgrad_cfg", lambda *a: C._GEMM_ROUTE)
+    monkeypatch.setattr(C, "_wgrad_cfg", lambda *a: C._GEMM_ROUTE)
+    conv = L.Conv2d(CI, CO, 1, bias=False).cuda()
+    with torch.no_grad():
+        conv.weight.copy_(w.float())
+    xa = x.detach().clone().requires_grad_(True)
+    yl = conv(xa)
+    yl.backward(dy)
+    assert _rel(yl, yr) < 1e-2
+    assert _rel(xa.grad, xr.grad) < 1e-2
+    assert _rel(conv.weight.grad, wr.grad) < 1e-2
