@@ -541,6 +541,62 @@ SmallGeom small_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t p
   return g;
 }
 
+// ImageNet stem (csrc/stem.hip): x [B, 3, H, W] channels_last bf16, w [64, 3, 7, 7]
+// channels_last bf16 -> (y [B, 64, H/2, W/2] channels_last, BN slots, xs for the wgrad)
+std::vector<Tensor> stem_fwd(Tensor x, Tensor w, bool want_stats, optional<Tensor> slots) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem: x must be a channels_last bf16 [B, 3, H, W] tensor");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == 64 &&
+                  w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem: w must be a channels_last bf16 [64, 3, 7, 7] tensor");
+  const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(dmp::stem_supported((int)H, (int)W), "stem: unsupported input size ", H, "x", W);
+  TORCH_CHECK(2 * B * (H / 2) * (W / 2) * 64 < (1LL << 31), "stem: batch too large");
+  auto xs = at::empty({B, H / 2, W / 2, 16}, x.options());
+  auto wp = at::empty({64, 256}, w.options());
+  auto y = at::empty({B, 64, H / 2, W / 2}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor part;
+  if (want_stats) part = bn_slots(slots, 64, x.options());
+  auto st = cur_stream();
+  dmp::launch_stem_s2d(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                       reinterpret_cast<uint16_t*>(xs.data_ptr()), (int)B, (int)H, (int)W, st);
+  dmp::launch_stem_wpack(reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                         reinterpret_cast<uint16_t*>(wp.data_ptr()), st);
+  dmp::launch_stem_fwd(reinterpret_cast<const uint16_t*>(xs.data_ptr()),
+                       reinterpret_cast<const uint16_t*>(wp.data_ptr()),
+                       reinterpret_cast<uint16_t*>(y.data_ptr()),
+                       want_stats ? part.data_ptr<float>() : nullptr, (int)B, (int)H, (int)W, st);
+  return {y, part, xs};
+}
+
+// dw (fp32 [64, 3, 7, 7] channels_last) += stem weight gradient from dY and the s2d input
+void stem_wgrad(Tensor dy, Tensor xs, Tensor dw) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc_bf16(dy, "dy");
+  check_gpu(xs, "xs");
+  check_gpu(dw, "dw");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 4 && dw.size(0) == 64 &&
+                  dw.size(1) == 3 && dw.size(2) == 7 && dw.size(3) == 7 &&
+                  dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem: dw must be an fp32 channels_last [64, 3, 7, 7] tensor");
+  TORCH_CHECK(xs.scalar_type() == at::kBFloat16 && xs.dim() == 4 && xs.size(3) == 16 &&
+                  xs.is_contiguous(), "stem: bad s2d input");
+  const int64_t B = xs.size(0), H = 2 * xs.size(1), W = 2 * xs.size(2);
+  TORCH_CHECK(dy.size(0) == B && dy.size(1) == 64 && dy.size(2) == H / 2 && dy.size(3) == W / 2,
+              "stem: dy shape mismatch");
+  TORCH_CHECK(dmp::stem_supported((int)H, (int)W), "stem: unsupported input size");
+  auto dwp = at::empty({64, 256}, dw.options().memory_format(at::MemoryFormat::Contiguous));
+  auto st = cur_stream();
+  dmp::launch_stem_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(xs.data_ptr()), dwp.data_ptr<float>(),
+                         (int)B, (int)H, (int)W, st);
+  dmp::launch_stem_wfold(dwp.data_ptr<float>(), dw.data_ptr<float>(), st);
+}
+
 std::vector<Tensor> conv_small_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad,
                                    bool want_stats, optional<Tensor> slots) {
   check_gpu(w, "w");
@@ -1073,6 +1129,12 @@ PYBIND11_MODULE(_native, m) {
   m.def("conv_halo_configs", &conv_halo_configs,
         "3x3/stride-1 halo-tile cfg ids applicable to (H, W, C, R, S, stride, pad)");
   m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials");
+  m.def("stem_supported", [](int64_t H, int64_t W) { return dmp::stem_supported((int)H, (int)W); },
+        "ImageNet 7x7/2 stem kernel applies to an H x W input");
+  m.def("stem_fwd", &stem_fwd, "ImageNet stem conv forward (+BN partials) via space-to-depth",
+        py::arg("x"), py::arg("w"), py::arg("want_stats"), py::arg("slots") = py::none());
+  m.def("stem_wgrad", &stem_wgrad, "ImageNet stem conv weight gradient (fp32 +=)", py::arg("dy"),
+        py::arg("xs"), py::arg("dw"));
   m.def("conv_small_fwd", &conv_small_fwd, "few-input-channel conv forward (+BN partials)",
         py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
         py::arg("slots") = py::none());

@@ -167,4 +167,14 @@ void launch_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long l
 void launch_conv_weight_transpose_batched(const uint16_t* src, uint16_t* dst,
                                           const long long* table, int n, long long max_elems,
                                           hipStream_t s);
+// stem.hip: ImageNet 7x7/2/3 stem (3 -> 64) as a 4x4 conv over a space-to-depth image
+bool stem_supported(int H, int W);
+void launch_stem_s2d(const uint16_t* x, uint16_t* xs, int B, int H, int W, hipStream_t s);
+void launch_stem_wpack(const uint16_t* w, uint16_t* wp, hipStream_t s);
+void launch_stem_wfold(const float* dwp, float* dw, hipStream_t s);
+void launch_stem_fwd(const uint16_t* xs, const uint16_t* wp, uint16_t* y, float* part, int B,
+                     int H, int W, hipStream_t s);
+void launch_stem_wgrad(const uint16_t* dy, const uint16_t* xs, float* dwp, int B, int H, int W,
+                       hipStream_t s);
+
 }  // namespace dmp

@@ -464,6 +464,61 @@ class _SmallConv(Function):
         return None, None, gw, None, None, None, None
 
 
+class _StemConv(Function):
+    """ImageNet 7x7/2/3 stem (3 -> 64 channels, csrc/stem.hip): the input is
+    space-to-depth packed once (2x2 pixel blocks -> 16 channels, the 4th colour
+    channel zero) so the conv becomes a stride-1 4x4 conv with K = 256 on MFMA;
+    the forward folds the BN partial sums into its store epilogue, the weight
+    gradient runs in the packed space and is folded back into the 7x7 arena
+    gradient.  The packed input is kept for the weight gradient (the stem's
+    input is data: no input gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, w16, master, want_stats, slots=None):
+        ctx.set_materialize_grads(False)
+        y, part, xs = native().stem_fwd(x, w16, want_stats, slots)
+        ctx.save_for_backward(xs)
+        ctx.master = master
+        if want_stats:
+            ctx.mark_non_differentiable(part)
+            return y, part
+        return y, None
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        if dy is None:
+            return None, None, None, None, None
+        (xs,) = ctx.saved_tensors
+        master = ctx.master
+        gw = None
+        if master is not None and master.requires_grad:
+            g = master.grad if getattr(master, "_dmp_arena", False) else None
+            if g is not None and g.is_contiguous(memory_format=torch.channels_last):
+                native().stem_wgrad(dy, xs, g)
+                cb = getattr(master, "_dmp_grad_ready", None)
+                if cb is not None:
+                    cb(master)
+            else:
+                gw = torch.empty(tuple(master.shape), dtype=torch.float32, device=xs.device,
+                                 memory_format=torch.channels_last).zero_()
+                native().stem_wgrad(dy, xs, gw)
+                gw = gw.to(master.dtype)
+        return None, None, gw, None, None
+
+
+def stem_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
+    if not (_NATIVE_ENABLED and _STEM != "im2col" and x.is_cuda and x.dtype == torch.bfloat16
+            and x.dim() == 4):
+        return False
+    if x.requires_grad or groups != 1 or _pair(dilation) != (1, 1):
+        return False
+    if _pair(stride) != (2, 2) or _pair(padding) != (3, 3):
+        return False
+    if tuple(weight.shape) != (64, 3, 7, 7):
+        return False
+    return bool(native().stem_supported(x.shape[2], x.shape[3]))
+
+
 def small_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
     if not (_NATIVE_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
         return False
@@ -546,6 +601,17 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
                     memory_format=torch.channels_last)
             y, part = _SmallConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
                                        bool(want_stats), slots if want_stats else None)
+            if part is not None:
+                y._dmp_bn_part = part
+            return (y, x) if alias else y
+        if master is not None and b is None and not relu and \
+                stem_conv_supported(x, master, stride, padding, dilation, groups):
+            w16 = getattr(master, "_dmp_w16", None)
+            if w16 is None or not w16.is_contiguous(memory_format=torch.channels_last):
+                w16 = master.detach().to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last)
+            y, part = _StemConv.apply(x, w16, master, bool(want_stats),
+                                      slots if want_stats else None)
             if part is not None:
                 y._dmp_bn_part = part
             return (y, x) if alias else y

@@ -386,3 +386,59 @@ def test_conv1x1_gemm_route(monkeypatch):
     assert _rel(yl, yr) < 1e-2
     assert _rel(xa.grad, xr.grad) < 1e-2
     assert _rel(conv.weight.grad, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("B,H", [(2, 224), (3, 48), (1, 8)])
+def test_stem_conv_fwd_stats_wgrad(B, H):
+    """ImageNet 7x7/2/3 stem (space-to-depth MFMA kernels) vs fp32 PyTorch."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    W = 224
+    assert nat.stem_supported(H, W) and not nat.stem_supported(H + 2, W)
+    assert not nat.stem_supported(H, 232)
+    torch.manual_seed(2)
+    x = torch.randn(B, 3, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(64, 3, 7, 7, device="cuda") / 147 ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(x.float(), wr, None, 2, 3)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr.backward(dy.float())
+    y, part, xs = nat.stem_fwd(x, w, True)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
+    assert _rel(y, yr) < 1e-2
+    ps = part[:2 * 64 * 64].view(2, 64, 64).sum(1)
+    yf = y.float()
+    torch.testing.assert_close(ps[0], yf.sum(dim=(0, 2, 3)), rtol=2e-3, atol=5e-2)
+    torch.testing.assert_close(ps[1], (yf * yf).sum(dim=(0, 2, 3)), rtol=2e-3, atol=5e-2)
+    y2, none, _ = nat.stem_fwd(x, w, False)
+    assert none is None or none.numel() == 0
+    assert torch.equal(y2, y)
+    dw = torch.zeros(64, 3, 7, 7, device="cuda").contiguous(memory_format=CL)
+    nat.stem_wgrad(dy, xs, dw)
+    assert _rel(dw, wr.grad) < 1e-2
+    nat.stem_wgrad(dy, xs, dw)
+    assert _rel(dw, 2 * wr.grad) < 1e-2
+
+
+def test_stem_conv_layer_route():
+    """ops.conv2d routes the ResNet stem to the native stem kernels (arena-less
+    master: the weight gradient comes back through autograd)."""
+    from distributed_ml_pytorch_amd.ops import conv as C
+
+    torch.manual_seed(3)
+    x = torch.randn(2, 3, 64, 224, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    master = torch.nn.Parameter((torch.randn(64, 3, 7, 7, device="cuda") / 147 ** 0.5)
+                                .contiguous(memory_format=CL))
+    assert C.stem_conv_supported(x, master, 2, 3, 1, 1)
+    slots = torch.zeros(2 * 64 * 64 + 4, device="cuda")
+    y = C.conv2d(x, None, None, 2, 3, 1, 1, master=master, want_stats=True, slots=slots)
+    assert hasattr(y, "_dmp_bn_part")
+    dy = torch.randn_like(y.float())
+    y.float().backward(dy)
+    wr = master.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.conv2d(x.float(), wr, None, 2, 3)
+    yr.backward(dy.to(torch.bfloat16).float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(master.grad, wr.grad) < 1e-2
