@@ -186,7 +186,7 @@ void check_nhwc_bf16(const Tensor& x, const char* name) {
 std::vector<Tensor> bn_fwd(Tensor x, optional<Tensor> res, optional<Tensor> gamma,
                            optional<Tensor> beta, optional<Tensor> running_mean,
                            optional<Tensor> running_var, double momentum, double eps,
-                           bool training, bool relu, optional<Tensor> slots) {
+                           bool training, bool relu, optional<Tensor> slots, bool want_mask) {
   check_nhwc_bf16(x, "x");
   const int64_t C = channels_of(x);
   const int64_t M = x.numel() / C;
@@ -207,19 +207,23 @@ std::vector<Tensor> bn_fwd(Tensor x, optional<Tensor> res, optional<Tensor> gamm
   auto fopt = x.options().dtype(at::kFloat);
   auto stats = at::empty({4, C}, fopt);
   auto part = bn_slots(slots, C, fopt);
+  // 1-bit ReLU mask [M][C/8] for the backward (instead of re-reading y)
+  Tensor mask;
+  if (want_mask && relu) mask = at::empty({M, C / 8}, x.options().dtype(at::kByte));
   dmp::launch_bn_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                      res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr,
                      reinterpret_cast<uint16_t*>(y.data_ptr()), ptr_or_null<float>(gamma),
                      ptr_or_null<float>(beta), ptr_or_null<float>(running_mean),
                      ptr_or_null<float>(running_var), stats.data_ptr<float>(),
                      part.data_ptr<float>(), M, (int)C, (float)momentum, (float)eps, training,
-                     relu, cur_stream());
-  return {y, stats};
+                     relu, cur_stream(), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr);
+  return {y, stats, mask};
 }
 
 std::vector<Tensor> bn_bwd(Tensor x, Tensor dy, optional<Tensor> y, optional<Tensor> gamma,
                            Tensor stats, optional<Tensor> dgamma, optional<Tensor> dbeta,
-                           bool relu, bool want_dres, optional<Tensor> slots) {
+                           bool relu, bool want_dres, optional<Tensor> slots,
+                           optional<Tensor> mask) {
   check_nhwc_bf16(x, "x");
   const int64_t C = channels_of(x);
   const int64_t M = x.numel() / C;
@@ -248,6 +252,13 @@ std::vector<Tensor> bn_bwd(Tensor x, Tensor dy, optional<Tensor> y, optional<Ten
   auto fopt = x.options().dtype(at::kFloat);
   auto part = bn_slots(slots, C, fopt);
   auto coef = at::empty({3, C}, fopt);
+  const uint8_t* mptr = nullptr;
+  if (relu && mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() == M * C / 8,
+                "bn: ReLU bit mask must be a contiguous uint8 [M, C/8] GPU tensor");
+    mptr = mask->data_ptr<uint8_t>();
+  }
   dmp::launch_bn_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                      reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                      have_y ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr,
@@ -255,8 +266,40 @@ std::vector<Tensor> bn_bwd(Tensor x, Tensor dy, optional<Tensor> y, optional<Ten
                      ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta), coef.data_ptr<float>(),
                      part.data_ptr<float>(), reinterpret_cast<uint16_t*>(dx.data_ptr()),
                      want_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr, M,
-                     (int)C, relu, cur_stream());
+                     (int)C, relu, cur_stream(), mptr);
   return {dx, want_dres ? dres : Tensor()};
+}
+
+// dz: the already ReLU-masked output gradient; part: the slot sums the consuming
+// conv's dgrad epilogue accumulated (re-zeroed here)
+Tensor bn_bwd_from_partials(Tensor x, Tensor dz, optional<Tensor> gamma, Tensor stats,
+                            optional<Tensor> dgamma, optional<Tensor> dbeta, Tensor part) {
+  check_nhwc_bf16(x, "x");
+  check_nhwc_bf16(dz, "dz");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: bad C");
+  TORCH_CHECK(dz.sizes() == x.sizes(), "dz shape mismatch");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * C, "bad stats");
+  for (auto* t : {&gamma, &dgamma, &dbeta}) {
+    if (t->has_value()) {
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == C &&
+                      (*t)->is_contiguous(),
+                  "bn gamma/dgamma/dbeta must be contiguous fp32 [C]");
+    }
+  }
+  auto fopt = x.options().dtype(at::kFloat);
+  part = bn_slots(part, C, fopt);
+  auto dx = at::empty_like(x);
+  auto coef = at::empty({3, C}, fopt);
+  dmp::launch_bn_bwd_from_partials(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                   reinterpret_cast<const uint16_t*>(dz.data_ptr()),
+                                   ptr_or_null<float>(gamma), stats.data_ptr<float>(),
+                                   ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta),
+                                   coef.data_ptr<float>(), part.data_ptr<float>(),
+                                   reinterpret_cast<uint16_t*>(dx.data_ptr()), M, (int)C,
+                                   cur_stream());
+  return dx;
 }
 
 // ------------------------------------------------------------------ pooling
@@ -449,7 +492,9 @@ void conv_weight_transpose_batched(Tensor src, Tensor dst, Tensor table, int64_t
 }
 
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
-                  int64_t cfg, optional<Tensor> wt_pre, optional<Tensor> addend) {
+                  int64_t cfg, optional<Tensor> wt_pre, optional<Tensor> addend,
+                  optional<Tensor> bn_x, optional<Tensor> bn_mask, optional<Tensor> bn_stats,
+                  optional<Tensor> bn_part, int64_t bn_relu) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc_bf16(dy, "dy");
   check_gpu(w, "w");
@@ -485,11 +530,40 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
     TORCH_CHECK(add_t.sizes() == dx.sizes(), "dgrad: addend must have the input's shape");
     add_ptr = reinterpret_cast<const uint16_t*>(add_t.data_ptr());
   }
+  // fused backward of the BatchNorm(+ReLU) that produced the conv input (bn_relu >= 0)
+  dmp::BnBwdFuse bnf{};
+  const bool fuse = bn_relu >= 0;
+  if (fuse) {
+    TORCH_CHECK(bn_relu <= 3 && bn_x.has_value() && bn_stats.has_value() && bn_part.has_value(),
+                "dgrad: BN fusion needs bn_x, bn_stats and bn_part");
+    check_nhwc_bf16(*bn_x, "bn_x");
+    TORCH_CHECK(bn_x->sizes() == dx.sizes(), "dgrad: bn_x must have the input's shape");
+    TORCH_CHECK(bn_stats->is_cuda() && bn_stats->scalar_type() == at::kFloat &&
+                    bn_stats->is_contiguous() && bn_stats->numel() == 4LL * g.CI,
+                "dgrad: bn_stats must be contiguous fp32 [4, C]");
+    bn_slots(bn_part, g.CI, dy.options().dtype(at::kFloat));
+    if (bn_relu == 1) {
+      TORCH_CHECK(bn_mask.has_value(), "dgrad: bn_relu 1 needs bn_mask");
+      check_nhwc_bf16(*bn_mask, "bn_mask");
+      TORCH_CHECK(bn_mask->sizes() == dx.sizes(), "dgrad: bn_mask must have the input's shape");
+      bnf.mask = reinterpret_cast<const uint16_t*>(bn_mask->data_ptr());
+    } else if (bn_relu == 3) {
+      TORCH_CHECK(bn_mask.has_value() && bn_mask->is_cuda() &&
+                      bn_mask->scalar_type() == at::kByte && bn_mask->is_contiguous() &&
+                      bn_mask->numel() == dx.numel() / 8,
+                  "dgrad: bn_relu 3 needs the uint8 [pixels, C/8] ReLU bit mask");
+      bnf.mask = reinterpret_cast<const uint16_t*>(bn_mask->data_ptr());
+    }
+    bnf.x = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
+    bnf.stats = bn_stats->data_ptr<float>();
+    bnf.part = bn_part->data_ptr<float>();
+    bnf.relu = (int)bn_relu;
+  }
   dmp::launch_conv_dgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                          reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                          reinterpret_cast<uint16_t*>(dx.data_ptr()), B, g.H, g.W, g.CI, g.OH,
                          g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream(),
-                         add_ptr);
+                         add_ptr, fuse ? &bnf : nullptr);
   return dx;
 }
 
@@ -1084,7 +1158,7 @@ std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optio
                                          optional<Tensor> gamma, optional<Tensor> beta,
                                          optional<Tensor> running_mean,
                                          optional<Tensor> running_var, double momentum,
-                                         double eps, bool relu) {
+                                         double eps, bool relu, bool want_mask) {
   check_nhwc_bf16(x, "x");
   const int64_t C = channels_of(x);
   const int64_t M = x.numel() / C;
@@ -1098,14 +1172,17 @@ std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optio
   }
   auto y = at::empty_like(x);
   auto stats = at::empty({4, C}, x.options().dtype(at::kFloat));
+  Tensor mask;
+  if (want_mask && relu) mask = at::empty({M, C / 8}, x.options().dtype(at::kByte));
   dmp::launch_bn_fwd_partials(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                               res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr,
                               reinterpret_cast<uint16_t*>(y.data_ptr()), ptr_or_null<float>(gamma),
                               ptr_or_null<float>(beta), ptr_or_null<float>(running_mean),
                               ptr_or_null<float>(running_var), stats.data_ptr<float>(),
                               part.data_ptr<float>(), M, (int)C, (float)momentum,
-                              (float)eps, relu, cur_stream());
-  return {y, stats};
+                              (float)eps, relu, cur_stream(),
+                              mask.defined() ? mask.data_ptr<uint8_t>() : nullptr);
+  return {y, stats, mask};
 }
 
 }  // namespace
@@ -1117,7 +1194,14 @@ PYBIND11_MODULE(_native, m) {
         py::arg("relu") = false);
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM conv data gradient", py::arg("dy"),
         py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"),
-        py::arg("cfg") = -1, py::arg("wt") = py::none(), py::arg("addend") = py::none());
+        py::arg("cfg") = -1, py::arg("wt") = py::none(), py::arg("addend") = py::none(),
+        py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
+        py::arg("bn_stats") = py::none(), py::arg("bn_part") = py::none(),
+        py::arg("bn_relu") = -1);
+  m.def("bn_bwd_from_partials", &bn_bwd_from_partials,
+        "BN backward from conv-dgrad-epilogue partials (dz already ReLU-masked)", py::arg("x"),
+        py::arg("dz"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"),
+        py::arg("part"));
   m.def("conv_weight_transpose_batched", &conv_weight_transpose_batched,
         "transpose every conv weight of a flat bf16 shadow in one launch");
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient (fp32 accumulate)",
@@ -1128,7 +1212,10 @@ PYBIND11_MODULE(_native, m) {
         "3x3/stride-1 halo wgrad cfg ids applicable to (B, H, W, CI, CO, R, S, stride, pad)");
   m.def("conv_halo_configs", &conv_halo_configs,
         "3x3/stride-1 halo-tile cfg ids applicable to (H, W, C, R, S, stride, pad)");
-  m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials");
+  m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials",
+        py::arg("x"), py::arg("part"), py::arg("G"), py::arg("res"), py::arg("gamma"),
+        py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"),
+        py::arg("eps"), py::arg("relu"), py::arg("want_mask") = false);
   m.def("stem_supported", [](int64_t H, int64_t W) { return dmp::stem_supported((int)H, (int)W); },
         "ImageNet 7x7/2 stem kernel applies to an H x W input");
   m.def("stem_fwd", &stem_fwd, "ImageNet stem conv forward (+BN partials) via space-to-depth",
@@ -1151,10 +1238,11 @@ PYBIND11_MODULE(_native, m) {
   m.def("bn_fwd", &bn_fwd, "NHWC batchnorm(+residual)(+relu) forward", py::arg("x"),
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("training"),
-        py::arg("relu"), py::arg("slots") = py::none());
+        py::arg("relu"), py::arg("slots") = py::none(), py::arg("want_mask") = false);
   m.def("bn_bwd", &bn_bwd, "NHWC batchnorm(+residual)(+relu) backward", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
-        py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"), py::arg("slots") = py::none());
+        py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"), py::arg("slots") = py::none(),
+        py::arg("mask") = py::none());
   m.def("layernorm_fwd", &layernorm_fwd,
         "row LayerNorm forward -> (y, mean, rstd[, h = x + residual])", py::arg("x"),
         py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("residual") = py::none());

@@ -34,7 +34,14 @@ __device__ __forceinline__ float bn_pre(float x, float sc, float sh) { return __
 // ReLU mask source of the backward: 0 = no ReLU, 1 = from the saved output y
 // (BN + residual + ReLU: the mask depends on the residual), 2 = recomputed from
 // x and the folded scale/shift in stats (no residual): one tensor read fewer in
-// both backward passes.
+// both backward passes, 3 = a 1-bit-per-element mask the forward apply wrote
+// beside y (BN + residual + ReLU): 1/16 of y's bytes in both backward passes.
+// Mask layout: one byte per 8-channel vector (bit k = channel c0 + k), i.e.
+// [M][C/8] bytes, the thread<->vector mapping of every kernel here.
+__device__ __forceinline__ void relu_mask_bits(unsigned bits, float g[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) g[k] = (bits >> k) & 1u ? g[k] : 0.f;
+}
 __device__ __forceinline__ void relu_mask_from_x(const float xv[8], const float* __restrict__ stats,
                                                  int C, int c0, float g[8]) {
 #pragma unroll
@@ -50,7 +57,8 @@ __device__ __forceinline__ void relu_mask_from_x(const float xv[8], const float*
 template <int MODE, int RELU>
 __global__ void __launch_bounds__(256) bn_partial_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
-    const float* __restrict__ stats, float* __restrict__ part, long long M, int C) {
+    const uint8_t* __restrict__ mask, const float* __restrict__ stats, float* __restrict__ part,
+    long long M, int C) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tpr = C >> 3;
   const int rpi = 256 / tpr;
@@ -84,12 +92,14 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(
     long long row = start + r0;
     for (; row + (U - 1) * rpi < end; row += U * rpi) {
       bf16x8 xr[U], dr[U], yr[U];
+      unsigned mb[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long long off = (row + u * rpi) * C + cg * 8;
         xr[u] = *reinterpret_cast<const bf16x8*>(x + off);
         if (MODE == 1) dr[u] = *reinterpret_cast<const bf16x8*>(dy + off);
         if (MODE == 1 && RELU == 1) yr[u] = *reinterpret_cast<const bf16x8*>(y + off);
+        if (MODE == 1 && RELU == 3) mb[u] = mask[off >> 3];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -100,6 +110,7 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(
           g[k] = MODE == 1 ? bf2f(dr[u].v[k]) : 0.f;
           if (MODE == 1 && RELU == 1) g[k] = bf2f(yr[u].v[k]) > 0.f ? g[k] : 0.f;
         }
+        if (MODE == 1 && RELU == 3) relu_mask_bits(mb[u], g);
         accum(xv, g);
       }
     }
@@ -115,6 +126,7 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(
 #pragma unroll
           for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
         }
+        if (RELU == 3) relu_mask_bits(mask[off >> 3], g);
       }
       accum(xv, g);
     }
@@ -207,10 +219,10 @@ __global__ void __launch_bounds__(1024) bn_fwd_finalize_kernel(
 }
 
 // -------- forward apply --------------------------------------------------
-template <bool RELU, bool RES>
+template <bool RELU, bool RES, bool MASK = false>
 __global__ void __launch_bounds__(256) bn_apply_kernel(
     const u16* __restrict__ x, const u16* __restrict__ res, const float* __restrict__ stats,
-    u16* __restrict__ y, long long nvec, int C) {
+    u16* __restrict__ y, long long nvec, int C, uint8_t* __restrict__ mask = nullptr) {
   const int tpr = C >> 3;
   const float* scale = stats + 2 * C;
   const float* shift = stats + 3 * C;
@@ -232,7 +244,19 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = fmaxf(o[k], 0.f);
     }
-    store8(y + v * 8, o);
+    if (MASK) {
+      bf16x8 r;
+      unsigned bits = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        r.v[k] = f2bf(o[k]);
+        bits |= (r.v[k] != 0 ? 1u : 0u) << k;   // the stored y > 0 (y >= 0 after the ReLU)
+      }
+      *reinterpret_cast<bf16x8*>(y + v * 8) = r;
+      mask[v] = (uint8_t)bits;
+    } else {
+      store8(y + v * 8, o);
+    }
   }
 }
 
@@ -263,8 +287,9 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(
 template <int RELU, bool WRITE_DRES>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
-    const float* __restrict__ coef, const float* __restrict__ stats, u16* __restrict__ dx,
-    u16* __restrict__ dres, long long nvec, int C) {
+    const uint8_t* __restrict__ mask, const float* __restrict__ coef,
+    const float* __restrict__ stats, u16* __restrict__ dx, u16* __restrict__ dres,
+    long long nvec, int C) {
   const int tpr = C >> 3;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
@@ -279,6 +304,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
       for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
     } else if (RELU == 2) {
       relu_mask_from_x(xv, stats, C, c0, g);
+    } else if (RELU == 3) {
+      relu_mask_bits(mask[v], g);
     }
     if (WRITE_DRES) store8(dres + v * 8, g);
     float o[8];
@@ -298,62 +325,75 @@ int bn_num_partials(long long M, int C) {
   return (int)g;
 }
 
+// forward apply; mask != nullptr (relu only) also writes the 1-bit ReLU mask
+static void bn_apply(const u16* x, const u16* res, const float* stats, u16* y, uint8_t* mask,
+                     long long M, int C, bool relu, hipStream_t s) {
+  const long long nvec = M * C / 8;
+  const dim3 grid(stream_grid(nvec, 256));
+  if (relu && mask) {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<true, true, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C, mask);
+    else hipLaunchKernelGGL((bn_apply_kernel<true, false, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C, mask);
+  } else if (relu) {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<true, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C, nullptr);
+    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C, nullptr);
+  } else {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<false, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C, nullptr);
+    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C, nullptr);
+  }
+}
+
 void launch_bn_fwd(const u16* x, const u16* res, u16* y, const float* gamma, const float* beta,
                    float* running_mean, float* running_var, float* stats, float* part,
                    long long M, int C, float momentum, float eps, bool training, bool relu,
-                   hipStream_t s) {
+                   hipStream_t s, uint8_t* mask) {
   const int G = bn_num_partials(M, C);
   const int rpi = 256 / (C / 8);
   const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
   if (training) {
     hipLaunchKernelGGL((bn_partial_kernel<0, 0>), dim3(G), dim3(256), lds, s, x, nullptr,
-                       nullptr, nullptr, part, M, C);
+                       nullptr, nullptr, nullptr, part, M, C);
   }
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part,
                      kBnSlots, M, C, gamma, beta, running_mean, running_var, momentum, eps,
                      stats, training ? 0 : 1);
-  const long long nvec = M * C / 8;
-  const dim3 grid(stream_grid(nvec, 256));
-  if (relu) {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<true, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
-  } else {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<false, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
-  }
+  bn_apply(x, res, stats, y, mask, M, C, relu, s);
 }
 
-// y == nullptr with relu: the ReLU mask is recomputed from x (no residual in
-// the forward); otherwise it is read from y.
+// ReLU mask of the backward: the 1-bit mask when given, else y, else (no
+// residual in the forward) recomputed from x.
 void launch_bn_bwd(const u16* x, const u16* dy, const u16* y, const float* gamma,
                    const float* stats, float* dgamma, float* dbeta, float* coef, float* part,
-                   u16* dx, u16* dres, long long M, int C, bool relu, hipStream_t s) {
+                   u16* dx, u16* dres, long long M, int C, bool relu, hipStream_t s,
+                   const uint8_t* mask) {
   const int G = bn_num_partials(M, C);
   const int rpi = 256 / (C / 8);
   const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
-  const int mode = !relu ? 0 : (y ? 1 : 2);
+  const int mode = !relu ? 0 : (mask ? 3 : (y ? 1 : 2));
 #define DMP_BN_PART(R)                                                                          \
-  hipLaunchKernelGGL((bn_partial_kernel<1, R>), dim3(G), dim3(256), lds, s, x, dy, y, stats, part, \
-                     M, C)
+  hipLaunchKernelGGL((bn_partial_kernel<1, R>), dim3(G), dim3(256), lds, s, x, dy, y, mask, stats, \
+                     part, M, C)
   if (mode == 0) DMP_BN_PART(0);
   else if (mode == 1) DMP_BN_PART(1);
-  else DMP_BN_PART(2);
+  else if (mode == 2) DMP_BN_PART(2);
+  else DMP_BN_PART(3);
 #undef DMP_BN_PART
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part,
                      kBnSlots, M, C, gamma, stats, dgamma, dbeta, coef);
   const long long nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, 256));
 #define DMP_BN_BAPPLY(R, D)                                                                   \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<R, D>), grid, dim3(256), 0, s, x, dy, y, coef, stats, \
-                     dx, dres, nvec, C)
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<R, D>), grid, dim3(256), 0, s, x, dy, y, mask, coef, \
+                     stats, dx, dres, nvec, C)
   if (dres) {
     if (mode == 0) DMP_BN_BAPPLY(0, true);
     else if (mode == 1) DMP_BN_BAPPLY(1, true);
-    else DMP_BN_BAPPLY(2, true);
+    else if (mode == 2) DMP_BN_BAPPLY(2, true);
+    else DMP_BN_BAPPLY(3, true);
   } else {
     if (mode == 0) DMP_BN_BAPPLY(0, false);
     else if (mode == 1) DMP_BN_BAPPLY(1, false);
-    else DMP_BN_BAPPLY(2, false);
+    else if (mode == 2) DMP_BN_BAPPLY(2, false);
+    else DMP_BN_BAPPLY(3, false);
   }
 #undef DMP_BN_BAPPLY
 }
@@ -361,23 +401,28 @@ void launch_bn_bwd(const u16* x, const u16* dy, const u16* y, const float* gamma
 }  // namespace dmp
 
 namespace dmp {
+// BN backward whose reductions were already made per block by the consuming
+// conv's data-gradient epilogue (conv.hip bnb_*, which also applied the ReLU
+// mask: dz arrives masked): finalize + a mask-free apply, no reduce pass.
+void launch_bn_bwd_from_partials(const u16* x, const u16* dz, const float* gamma,
+                                 const float* stats, float* dgamma, float* dbeta, float* coef,
+                                 float* part, u16* dx, long long M, int C, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part,
+                     kBnSlots, M, C, gamma, stats, dgamma, dbeta, coef);
+  const long long nvec = M * C / 8;
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<0, false>), dim3(stream_grid(nvec, 256)), dim3(256), 0,
+                     s, x, dz, nullptr, nullptr, coef, stats, dx, nullptr, nvec, C);
+}
+
 // BN forward whose statistics were already reduced per block by the producing
 // conv's epilogue (conv.hip STATS): finalize + apply only, no stats pass over x.
 void launch_bn_fwd_partials(const u16* x, const u16* res, u16* y, const float* gamma,
                             const float* beta, float* running_mean, float* running_var,
                             float* stats, float* part, long long M, int C,
-                            float momentum, float eps, bool relu, hipStream_t s) {
+                            float momentum, float eps, bool relu, hipStream_t s, uint8_t* mask) {
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part,
                      kBnSlots, M, C, gamma, beta, running_mean, running_var, momentum, eps,
                      stats, 0);
-  const long long nvec = M * C / 8;
-  const dim3 grid(stream_grid(nvec, 256));
-  if (relu) {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<true, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
-  } else {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<false, true>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), grid, dim3(256), 0, s, x, res, stats, y, nvec, C);
-  }
+  bn_apply(x, res, stats, y, mask, M, C, relu, s);
 }
 }  // namespace dmp

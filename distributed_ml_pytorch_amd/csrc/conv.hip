@@ -30,6 +30,7 @@
 // BatchNorm partial sums (no extra pass over Y).  Several tile configurations are
 // compiled; the host side times them per shape on first use (ops/tuner.py).
 #include "common.h"
+#include "launchers.h"
 
 namespace dmp {
 
@@ -48,7 +49,35 @@ struct ConvArgs {
   const float* bias;   // optional fp32 [CO] added in the fwd epilogue
   const u16* addend;   // dgrad: optional [B][H][W][CI] bf16 added to dX in the epilogue
   int relu;            // fwd: max(0, .) in the epilogue (conv -> ReLU, AlexNet)
+  // dgrad with STATS: backward of the BatchNorm(+ReLU) that produced this conv's
+  // input, fused into the epilogue (see bnb_* below)
+  const u16* bnx;       // the BN's input x [B][H][W][CI]
+  const u16* bnmask;    // bnrelu 1: the stored ReLU output (this conv's own input);
+                        // bnrelu 3: bn.hip's 1-bit ReLU mask [pixels][CI/8] bytes
+  const float* bnstat;  // the BN's [4][CI] mean | invstd | scale | shift
+  int bnrelu;           // 0 no ReLU, 1 / 3 mask from bnmask, 2 mask recomputed from bnx
 };
+
+// Data-gradient epilogue fused with the backward of the BatchNorm(+ReLU) whose
+// output the conv consumed (dgrad kernels instantiated with STATS): the kernel
+// stores dz = dX * relu'(.) instead of dX, and the two BN-backward reductions
+// sum(dz) and sum(dz * (x - mean)) leave through the same per-block slot sums
+// as the forward statistics (the second scaled by invstd at the block
+// reduction: sum(dz * xhat)).  That removes bn.hip's reduce pass (dY, x and y
+// re-read) and the ReLU-mask input of its apply pass.  The mask is the stored
+// ReLU output > 0 (bnrelu 1: BN + residual + ReLU, whose output is this conv's
+// own input) or is recomputed from x and the folded scale/shift exactly as
+// bn.hip relu_mask_from_x (bnrelu 2).
+__device__ __forceinline__ float bnb_lo(unsigned v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bnb_hi(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
+
+// relu'(.) of the BN output: stored output mk (bnrelu 1) or recomputed from the
+// BN input xb and the folded scale/shift (bnrelu 2, rounded as the stored y)
+__device__ __forceinline__ bool bnb_on(int bnrelu, float xb, float mk, float sc, float sh) {
+  if (bnrelu == 1 || bnrelu == 3) return mk > 0.f;
+  if (bnrelu == 2) return bf2f(f2bf(fmaxf(__fmaf_rn(xb, sc, sh), 0.f))) > 0.f;
+  return true;
+}
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
@@ -308,15 +337,30 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   const bool add_in = MODE == 1 && a.addend != nullptr;
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
+  constexpr bool BNB = MODE == 1 && STATS;   // fused BN(+ReLU) backward
+  const __amdgpu_buffer_rsrc_t rsBx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNB ? a.bnx : a.y), 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsBm = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNB && (a.bnrelu == 1 || a.bnrelu == 3) ? a.bnmask : a.y), 0,
+      (int)((a.bnrelu == 3 ? 1LL : 16LL) * a.B * a.OH * a.OW * a.CO / 8), 0x00020000);
   float bj[TN][4];
   bool nok[TN];
+  // BNB: per-channel mean | scale | shift of the BN (channels n..n+3 of tile j)
+  float bmu[BNB ? TN : 1][4], bsc[BNB ? TN : 1][4], bsh[BNB ? TN : 1][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
     nok[j] = n < a.CO;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 4; ++r) {
       bj[j][r] = (MODE == 0 && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
+      if constexpr (BNB) {
+        const int ch = nok[j] ? n + r : 0;
+        bmu[j][r] = a.bnstat[ch];
+        bsc[j][r] = a.bnrelu == 2 ? a.bnstat[2 * a.CO + ch] : 0.f;
+        bsh[j][r] = a.bnrelu == 2 ? a.bnstat[3 * a.CO + ch] : 0.f;
+      }
+    }
   }
   float s_sum[TN][4], s_sq[TN][4];
   if (STATS) {
@@ -353,13 +397,34 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
         ad[2] = __uint_as_float(av.y << 16);
         ad[3] = __uint_as_float(av.y & 0xffff0000u);
       }
+      float xb[4] = {0.f, 0.f, 0.f, 0.f}, mk[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BNB) {
+        const u32x2_t xv = __builtin_amdgcn_raw_buffer_load_b64(rsBx, ok ? rowoff + 2u * n : kOOB, 0, 0);
+        xb[0] = bnb_lo(xv.x); xb[1] = bnb_hi(xv.x); xb[2] = bnb_lo(xv.y); xb[3] = bnb_hi(xv.y);
+        if (a.bnrelu == 1) {
+          const u32x2_t mv =
+              __builtin_amdgcn_raw_buffer_load_b64(rsBm, ok ? rowoff + 2u * n : kOOB, 0, 0);
+          mk[0] = bnb_lo(mv.x); mk[1] = bnb_hi(mv.x); mk[2] = bnb_lo(mv.y); mk[3] = bnb_hi(mv.y);
+        } else if (a.bnrelu == 3) {
+          // byte (pixel, n / 8) of the bit mask; bits (n & 4) .. +3 are channels n .. n+3
+          const unsigned bits = __builtin_amdgcn_raw_buffer_load_b8(
+              rsBm, ok ? (rowoff >> 4) + (unsigned)(n >> 3) : kOOB, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mk[r] = (bits >> ((n & 4) + r)) & 1u ? 1.f : 0.f;
+        }
+      }
       u16 h[4];
-      float v[4];
+      float v[4], t[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float t = acc[i][j][r] + bj[j][r] + ad[r];
-        if (MODE == 0 && a.relu) t = fmaxf(t, 0.f);
-        h[r] = f2bf(t);
+        t[r] = acc[i][j][r] + bj[j][r] + ad[r];
+        if (MODE == 0 && a.relu) t[r] = fmaxf(t[r], 0.f);
+        if constexpr (BNB)
+          t[r] = bnb_on(a.bnrelu, xb[r], mk[r], bsc[j][r], bsh[j][r]) ? t[r] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        h[r] = f2bf(t[r]);
         v[r] = bf2f(h[r]);   // statistics of the stored (rounded) values
       }
       const u32x2_t packed = {(u32)h[0] | ((u32)h[1] << 16), (u32)h[2] | ((u32)h[3] << 16)};
@@ -370,7 +435,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
         for (int r = 0; r < 4; ++r) {
           const float x = v[r] * keep;
           s_sum[j][r] += x;
-          s_sq[j][r] += x * x;
+          if constexpr (BNB) s_sq[j][r] += x * (xb[r] - bmu[j][r]);
+          else s_sq[j][r] += x * x;
         }
       }
     }
@@ -403,7 +469,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
         float ss = 0.f, qq = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { ss += red[w * BN + nl]; qq += red[WM * BN + w * BN + nl]; }
-        const int slot = blockIdx.x % kBnSlots;
+        if (BNB) qq *= a.bnstat[a.CO + n];   // sum dz * (x - mean) -> sum dz * xhat
+        const int slot = (blockIdx.x + blockIdx.z * gridDim.x) % kBnSlots;
         atomicAdd(a.part + (long long)slot * a.CO + n, ss);
         atomicAdd(a.part + (long long)(kBnSlots + slot) * a.CO + n, qq);
       }
@@ -604,15 +671,30 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   const bool add_in = FLIP && a.addend != nullptr;
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  constexpr bool BNB = FLIP && STATS;   // fused BN(+ReLU) backward
+  const __amdgpu_buffer_rsrc_t rsBx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNB ? a.bnx : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsBm = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNB && (a.bnrelu == 1 || a.bnrelu == 3) ? a.bnmask : a.y), 0,
+      (int)((a.bnrelu == 3 ? 1LL : 16LL) * Mtot * a.CO / 8), 0x00020000);
   float bj[TN][4];
   bool nok[TN];
+  // BNB: per-channel mean | scale | shift of the BN (channels n..n+3 of tile j)
+  float bmu[BNB ? TN : 1][4], bsc[BNB ? TN : 1][4], bsh[BNB ? TN : 1][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
     nok[j] = n < a.CO;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 4; ++r) {
       bj[j][r] = (!FLIP && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
+      if constexpr (BNB) {
+        const int ch = nok[j] ? n + r : 0;
+        bmu[j][r] = a.bnstat[ch];
+        bsc[j][r] = a.bnrelu == 2 ? a.bnstat[2 * a.CO + ch] : 0.f;
+        bsh[j][r] = a.bnrelu == 2 ? a.bnstat[3 * a.CO + ch] : 0.f;
+      }
+    }
   }
   float s_sum[TN][4], s_sq[TN][4];
   if (STATS) {
@@ -639,13 +721,34 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
         ad[2] = __uint_as_float(av.y << 16);
         ad[3] = __uint_as_float(av.y & 0xffff0000u);
       }
+      float xb[4] = {0.f, 0.f, 0.f, 0.f}, mk[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BNB) {
+        const u32x2_t xv = __builtin_amdgcn_raw_buffer_load_b64(rsBx, ok ? rowoff + 2u * n : kOOB, 0, 0);
+        xb[0] = bnb_lo(xv.x); xb[1] = bnb_hi(xv.x); xb[2] = bnb_lo(xv.y); xb[3] = bnb_hi(xv.y);
+        if (a.bnrelu == 1) {
+          const u32x2_t mv =
+              __builtin_amdgcn_raw_buffer_load_b64(rsBm, ok ? rowoff + 2u * n : kOOB, 0, 0);
+          mk[0] = bnb_lo(mv.x); mk[1] = bnb_hi(mv.x); mk[2] = bnb_lo(mv.y); mk[3] = bnb_hi(mv.y);
+        } else if (a.bnrelu == 3) {
+          // byte (pixel, n / 8) of the bit mask; bits (n & 4) .. +3 are channels n .. n+3
+          const unsigned bits = __builtin_amdgcn_raw_buffer_load_b8(
+              rsBm, ok ? (rowoff >> 4) + (unsigned)(n >> 3) : kOOB, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mk[r] = (bits >> ((n & 4) + r)) & 1u ? 1.f : 0.f;
+        }
+      }
       u16 hv[4];
-      float v[4];
+      float v[4], t[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float t = acc[i][j][r] + bj[j][r] + ad[r];
-        if (!FLIP && a.relu) t = fmaxf(t, 0.f);
-        hv[r] = f2bf(t);
+        t[r] = acc[i][j][r] + bj[j][r] + ad[r];
+        if (!FLIP && a.relu) t[r] = fmaxf(t[r], 0.f);
+        if constexpr (BNB)
+          t[r] = bnb_on(a.bnrelu, xb[r], mk[r], bsc[j][r], bsh[j][r]) ? t[r] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hv[r] = f2bf(t[r]);
         v[r] = bf2f(hv[r]);
       }
       const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
@@ -656,7 +759,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
         for (int r = 0; r < 4; ++r) {
           const float x = v[r] * keep;
           s_sum[j][r] += x;
-          s_sq[j][r] += x * x;
+          if constexpr (BNB) s_sq[j][r] += x * (xb[r] - bmu[j][r]);
+          else s_sq[j][r] += x * x;
         }
       }
     }
@@ -687,7 +791,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
         float ss = 0.f, qq = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { ss += red[w * BN + nl]; qq += red[WM * BN + w * BN + nl]; }
-        const int slot = blockIdx.x % kBnSlots;
+        if (BNB) qq *= a.bnstat[a.CO + n];   // sum dz * (x - mean) -> sum dz * xhat
+        const int slot = (blockIdx.x + blockIdx.z * gridDim.x) % kBnSlots;
         atomicAdd(a.part + (long long)slot * a.CO + n, ss);
         atomicAdd(a.part + (long long)(kBnSlots + slot) * a.CO + n, qq);
       }
@@ -1218,17 +1323,20 @@ static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
     HaloPGeom pg;
     int bm, ns, nw;
     size_t plds;
-    // a residual-gradient addend is not fused in the persistent kernel: take the
-    // 4-wave halo tile for those dgrads instead
-    if (FLIP && a.addend != nullptr)
+    // a residual-gradient addend and the BN-backward epilogue are not fused in
+    // the persistent kernel (its deferred epilogue runs with the next tile's DMA
+    // in flight): take the 4-wave halo tile for those dgrads instead
+    if (FLIP && (a.addend != nullptr || STATS))
       return launch_halo<FLIP, STATS>(a, kHaloBase + 9, s) ||
              launch_halo<FLIP, STATS>(a, kHaloBase + 5, s);
     if (!halop_geom(cfg, a.B, a.GH, a.GW, a.CI, a.R, a.S, a.stride, a.pad, &pg, &bm, &ns, &nw,
                     &plds))
       return false;
-    if (nw == 8) launch_halop_t<256, 2, 8, FLIP, STATS>(a, pg, plds, s);
-    else if (bm == 256) launch_halop_t<256, 2, 4, FLIP, STATS>(a, pg, plds, s);
-    else launch_halop_t<128, 3, 4, FLIP, STATS>(a, pg, plds, s);
+    if constexpr (!(FLIP && STATS)) {
+      if (nw == 8) launch_halop_t<256, 2, 8, FLIP, STATS>(a, pg, plds, s);
+      else if (bm == 256) launch_halop_t<256, 2, 4, FLIP, STATS>(a, pg, plds, s);
+      else launch_halop_t<128, 3, 4, FLIP, STATS>(a, pg, plds, s);
+    }
     return true;
   }
   if (!halo_geom(cfg, a.GH, a.GW, a.CI, a.R, a.S, a.stride, a.pad, &g, &lds)) return false;
@@ -1268,17 +1376,25 @@ void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int
 // dX (B,H,W,CI) from dY (B,OH,OW,CO) and Wt [CI][R][S][CO]; stride*stride parity classes.
 void launch_conv_dgrad(const u16* dy, const u16* wt, u16* dx, int B, int H, int W, int CI,
                        int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                       hipStream_t s, const u16* addend) {
+                       hipStream_t s, const u16* addend, const BnBwdFuse* bnf) {
   const long long rows = (long long)B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
   ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad, rows, nullptr,
              addend};
+  if (bnf) {
+    a.part = bnf->part;
+    a.bnx = bnf->x;
+    a.bnmask = bnf->mask;
+    a.bnstat = bnf->stats;
+    a.bnrelu = bnf->relu;
+  }
   if (cfg >= kHaloBase) {
     // stride 1, 3x3, pad 1: dX = the same conv over dY with Wt and mirrored taps
-    if (launch_halo<true, false>(a, cfg, s)) return;
+    if (bnf ? launch_halo<true, true>(a, cfg, s) : launch_halo<true, false>(a, cfg, s)) return;
     cfg = -1;
   }
   if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(rows * stride * stride, CI);
-  dispatch<1, false>(a, cfg, stride * stride, s);
+  if (bnf) dispatch<1, true>(a, cfg, stride * stride, s);
+  else dispatch<1, false>(a, cfg, stride * stride, s);
 }
 
 void launch_conv_weight_transpose(const u16* w, u16* wt, int CO, int RS, int CI, hipStream_t s) {

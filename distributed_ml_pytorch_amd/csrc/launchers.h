@@ -38,10 +38,14 @@ int bn_num_partials(long long M, int C);
 void launch_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma,
                    const float* beta, float* running_mean, float* running_var, float* stats,
                    float* part, long long M, int C, float momentum, float eps, bool training,
-                   bool relu, hipStream_t s);
+                   bool relu, hipStream_t s, uint8_t* mask = nullptr);
+void launch_bn_bwd_from_partials(const uint16_t* x, const uint16_t* dz, const float* gamma,
+                                 const float* stats, float* dgamma, float* dbeta, float* coef,
+                                 float* part, uint16_t* dx, long long M, int C, hipStream_t s);
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const float* gamma,
                    const float* stats, float* dgamma, float* dbeta, float* coef, float* part,
-                   uint16_t* dx, uint16_t* dres, long long M, int C, bool relu, hipStream_t s);
+                   uint16_t* dx, uint16_t* dres, long long M, int C, bool relu, hipStream_t s,
+                   const uint8_t* mask = nullptr);
 
 // pool.hip
 void launch_gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s);
@@ -99,9 +103,22 @@ bool conv_wgrad_halo_ok(int cfg, int B, int H, int W, int CI, int CO, int R, int
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int B, int H,
                      int W, int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
                      int cfg, hipStream_t s, const float* bias = nullptr, bool relu = false);
+// Backward of the BatchNorm(+ReLU) that produced a conv's input, fused into the
+// conv's data-gradient epilogue (conv.hip bnb_*): the dgrad stores dz and adds
+// sum(dz), sum(dz * xhat) per channel into the BN's backward slot buffer.
+struct BnBwdFuse {
+  const uint16_t* x;     // BN input [B][H][W][C]
+  const uint16_t* mask;  // relu 1: stored BN(+residual)+ReLU output (the conv input);
+                         // relu 3: the BN's 1-bit ReLU mask (bytes)
+  const float* stats;    // [4][C] mean | invstd | scale | shift
+  float* part;           // [2][kBnSlots][C] (+tail) slot sums, zeroed
+  int relu;              // 0 none, 1 / 3 mask from `mask`, 2 mask from x and scale/shift
+};
+
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int B, int H, int W,
                        int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                       hipStream_t s, const uint16_t* addend = nullptr);
+                       hipStream_t s, const uint16_t* addend = nullptr,
+                       const BnBwdFuse* bnf = nullptr);
 void launch_conv_weight_transpose(const uint16_t* w, uint16_t* wt, int CO, int RS, int CI,
                                   hipStream_t s);
 // dbias: optional fp32 [CO] += column sums of dY (gather kernel only; halo cfgs fall back)
@@ -139,7 +156,8 @@ void launch_colsum_acc(const uint16_t* dy, float* out, float* slots, long long M
 void launch_bn_fwd_partials(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma,
                             const float* beta, float* running_mean, float* running_var,
                             float* stats, float* part, long long M, int C,
-                            float momentum, float eps, bool relu, hipStream_t s);
+                            float momentum, float eps, bool relu, hipStream_t s,
+                            uint8_t* mask = nullptr);
 
 // gemm.hip: bf16 MFMA GEMM for linear layers.  mode 0 fwd C = A B^T (A [M][K],
 // B [N][K]); mode 1 dgrad (A [M][K], B [K][N]); mode 2 wgrad, fp32 C += (A [K][M],

@@ -265,6 +265,10 @@ class _NativeConv(Function):
                                            relu)
         # ReLU fused in the epilogue; its backward masks dY by the saved output
         ctx.save_for_backward(x, w16, y if relu else None)
+        # input produced by a training BatchNorm(+ReLU): its backward reduce can
+        # run in this conv's dgrad epilogue (ops/functional.py BNLink)
+        link = getattr(x, "_dmp_bnlink", None)
+        ctx.bnlink = link if link is not None and link.consumer_ok(x) else None
         ctx.master = master
         ctx.geom = (x.shape[2], x.shape[3], stride, pad)
         # alias: x handed back as a third output (a view whose gradient arrives
@@ -298,7 +302,15 @@ class _NativeConv(Function):
             shadow = getattr(master, "_dmp_w16", None)
             if arena is not None and shadow is not None and shadow.data_ptr() == w16.data_ptr():
                 wt = arena.transposed_conv_shadow(master)
-            dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt, dxa)
+            bn = ctx.bnlink
+            if bn is not None:
+                dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt, dxa, bn_x=bn.x,
+                                         bn_mask=(x if bn.relu == 1 else
+                                                  bn.mask if bn.relu == 3 else None),
+                                         bn_stats=bn.stats, bn_part=bn.part, bn_relu=bn.relu)
+                bn.fused = (dx, dx._version)
+            else:
+                dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt, dxa)
         elif dxa is not None:
             dx = dxa
         gw = None

@@ -13,6 +13,8 @@ all-reduce overlap in sync-DP mode).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch.autograd import Function
@@ -108,6 +110,46 @@ def softmax_cross_entropy(logits, labels, label_smoothing: float = 0.0, ignore_i
 
 
 # ------------------------------------------------------------------ batchnorm
+# which BatchNorms hand their backward reduce to the consuming conv's dgrad
+# epilogue: "0" (default), "residual" (BN + residual + ReLU only) or "all".
+# Measured a loss or a wash (profiles/bn_bwd_fusion_r2.txt): the conv kernels
+# are bound by their per-CU global->LDS fill, and the epilogue's extra reads of
+# x (and the mask) go through that same path, costing more inside the conv
+# (+30-50 % on the 64-channel dgrads) than the standalone streaming reduce
+# they replace -- once the residual BNs keep a 1-bit ReLU mask instead of
+# re-reading y, the separate pass is the cheaper place for those bytes.
+_BN_BWD_FUSE = os.environ.get("DMP_BN_BWD_FUSE", "0")
+BN_BWD_FUSE_STATS = {"fused": 0, "fallback": 0}
+_BN_BITMASK = os.environ.get("DMP_BN_BITMASK", "1") != "0"   # backward passes by path (diagnostics)
+
+
+class BNLink:
+    """Hand-off between a training BatchNorm(+ReLU) and the native conv that
+    consumes its output (attached to the output as ``_dmp_bnlink``).
+
+    The conv's data-gradient epilogue can run the BN backward's reduce pass
+    itself (csrc/conv.hip ``bnb_*``): it stores dz = dX * relu'(.) and adds
+    sum(dz), sum(dz * xhat) into the BN's backward slot buffer ``part``, then
+    records ``fused = (dX, version)``.  The BN backward uses those partials only
+    if the gradient it receives IS that tensor, unmodified (same storage and
+    version: no other consumer's gradient was accumulated into it); otherwise it
+    re-zeroes the slots and runs the full reduce (the ReLU mask is idempotent,
+    so a pre-masked contribution stays correct)."""
+
+    __slots__ = ("x", "stats", "relu", "part", "y_ptr", "fused", "mask")
+
+    def __init__(self, x, stats, relu: int, part, y, mask=None):
+        self.x, self.stats, self.part = x, stats, part
+        # ReLU-mask source for the epilogue: 3 = the forward's bit mask
+        self.relu = 3 if (relu == 1 and mask is not None) else relu
+        self.mask = mask
+        self.y_ptr = y.data_ptr()
+        self.fused = None
+
+    def consumer_ok(self, inp) -> bool:
+        return inp.data_ptr() == self.y_ptr and inp.shape == self.x.shape
+
+
 class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
@@ -116,28 +158,40 @@ class _BNAct(Function):
             x = x.contiguous(memory_format=CL)
             if residual is not None:
                 residual = residual.contiguous(memory_format=CL)
+        # BN + residual + ReLU: the backward's ReLU mask depends on the residual;
+        # keep it as 1 bit per element (written by the apply) instead of y
+        want_mask = bool(relu and residual is not None and _BN_BITMASK)
         if part is not None and training:
             # statistics already reduced per block by the producing conv's epilogue
             C = x.shape[1]
-            y, stats = native().bn_fwd_from_partials(
+            y, stats, mask = native().bn_fwd_from_partials(
                 x, part, (part.numel() - 4) // (2 * C), residual, gamma, beta, running_mean,
-                running_var, float(momentum), float(eps), bool(relu))
+                running_var, float(momentum), float(eps), bool(relu), want_mask)
         else:
-            y, stats = native().bn_fwd(x, residual, gamma, beta, running_mean, running_var,
-                                       float(momentum), float(eps), bool(training), bool(relu),
-                                       slots[0] if slots is not None else None)
+            y, stats, mask = native().bn_fwd(x, residual, gamma, beta, running_mean, running_var,
+                                             float(momentum), float(eps), bool(training),
+                                             bool(relu), slots[0] if slots is not None else None,
+                                             want_mask)
         ctx.bslots = slots[1] if slots is not None else None
+        ctx.link = None
+        if (_BN_BWD_FUSE not in ("0", False) and training and x.dim() == 4 and x.is_cuda
+                and ctx.bslots is not None
+                and (residual is not None and relu or _BN_BWD_FUSE in ("all", True))):
+            mode = 0 if not relu else (1 if residual is not None else 2)
+            ctx.link = BNLink(x, stats, mode, ctx.bslots, y, mask)
+            y._dmp_bnlink = ctx.link
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.gamma, ctx.beta = gamma, beta
         # the backward re-derives the ReLU mask from x and the folded scale/shift
-        # unless a residual entered the forward (then the mask needs y)
-        ctx.save_for_backward(x, y if (relu and residual is not None) else None, stats)
+        # unless a residual entered the forward (then the bit mask, or y)
+        ctx.save_for_backward(x, y if (relu and residual is not None and mask is None) else None,
+                              stats, mask)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, stats = ctx.saved_tensors
+        x, y, stats, mask = ctx.saved_tensors
         gamma, beta = ctx.gamma, ctx.beta
         dg_arena, db_arena = _arena_grad(gamma), _arena_grad(beta)
         need_g = gamma is not None and ctx.needs_input_grad[1]
@@ -146,12 +200,27 @@ class _BNAct(Function):
             torch.zeros_like(gamma) if need_g else None)
         db = db_arena if db_arena is not None else (
             torch.zeros_like(beta) if need_b else None)
-        if x.dim() == 4:
-            dy = dy.contiguous(memory_format=CL)
+        link = ctx.link
+        fused = False
+        if link is not None and link.fused is not None:
+            fdx, fver = link.fused
+            link.fused = None
+            fused = (dy.data_ptr() == fdx.data_ptr() and dy._version == fver
+                     and dy.shape == fdx.shape and dy.stride() == fdx.stride())
+            BN_BWD_FUSE_STATS["fused" if fused else "fallback"] += 1
+            if not fused:
+                link.part.zero_()        # partial sums of an incomplete gradient
+        if fused:
+            # the consuming conv's dgrad already masked dz and reduced it
+            dx = native().bn_bwd_from_partials(x, dy, gamma, stats, dg, db, link.part)
+            dres = dy if ctx.has_res else None
         else:
-            dy = dy.contiguous()
-        dx, dres = native().bn_bwd(x, dy, y, gamma, stats, dg, db, ctx.relu, ctx.has_res,
-                                   ctx.bslots)
+            if x.dim() == 4:
+                dy = dy.contiguous(memory_format=CL)
+            else:
+                dy = dy.contiguous()
+            dx, dres = native().bn_bwd(x, dy, y, gamma, stats, dg, db, ctx.relu, ctx.has_res,
+                                       ctx.bslots, mask)
         if dg_arena is not None or db_arena is not None:
             _notify(gamma, beta)
         ret_g = None if (dg_arena is not None or not need_g) else dg

@@ -442,3 +442,91 @@ def test_stem_conv_layer_route():
     yr.backward(dy.to(torch.bfloat16).float())
     assert _rel(y, yr) < 1e-2
     assert _rel(master.grad, wr.grad) < 1e-2
+
+
+def _grads_with_bn_fusion(monkeypatch, fuse, model, x, g, bitmask=True):
+    from distributed_ml_pytorch_amd.ops import functional as Fn
+
+    monkeypatch.setattr(Fn, "_BN_BWD_FUSE", fuse if fuse else "0")
+    monkeypatch.setattr(Fn, "_BN_BITMASK", bitmask)
+    for p in model.parameters():
+        p.grad = None
+    xx = x.detach().clone().requires_grad_(True)
+    y = model(xx)
+    (y.float() * g).sum().backward()
+    torch.cuda.synchronize()
+    return y.detach(), [xx.grad] + [p.grad.detach().clone() for p in model.parameters()]
+
+
+@pytest.mark.parametrize("kind", ["basic_s1", "basic_s2", "bottleneck"])
+def test_bn_backward_fused_into_dgrad(kind, monkeypatch):
+    """BN(+ReLU) backward reductions run in the consuming conv's dgrad epilogue
+    (csrc/conv.hip bnb_*; ops/functional.py BNLink): gradients match the
+    separate reduce pass.  Two chained blocks exercise both ReLU-mask sources:
+    bn1 -> conv2 (mask recomputed from x) and block 1's bn2 + residual ->
+    block 2's conv1 with the shortcut gradient as the dgrad addend (mask from
+    the stored output)."""
+    from distributed_ml_pytorch_amd.models.resnet import BasicBlock, Bottleneck
+    from distributed_ml_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(0)
+    if kind == "bottleneck":
+        model = torch.nn.Sequential(Bottleneck(256, 64, 1), Bottleneck(256, 128, 2)).cuda()
+        x = torch.randn(4, 256, 14, 14, device="cuda")
+    else:
+        s = 1 if kind == "basic_s1" else 2
+        model = torch.nn.Sequential(BasicBlock(64, 64, 1), BasicBlock(64, 64 * s, s)).cuda()
+        x = torch.randn(4, 64, 16, 16, device="cuda")
+    x = x.to(torch.bfloat16).contiguous(memory_format=CL)
+    g = torch.randn(model(x).shape, device="cuda")
+    # reference: standalone reduce, ReLU mask of the residual BNs read from y
+    y0, ref = _grads_with_bn_fusion(monkeypatch, False, model, x, g, bitmask=False)
+    # standalone reduce with the forward's 1-bit mask
+    _, bits = _grads_with_bn_fusion(monkeypatch, False, model, x, g)
+    for a, b in zip(ref, bits):
+        assert _rel(b, a) < 5e-3
+    before = dict(Fn.BN_BWD_FUSE_STATS)
+    y1, got = _grads_with_bn_fusion(monkeypatch, "all", model, x, g)
+    assert Fn.BN_BWD_FUSE_STATS["fused"] > before["fused"]
+    assert _rel(y1, y0) < 1e-3        # forward untouched (atomic-order noise only)
+    for a, b in zip(ref, got):
+        assert _rel(b, a) < 5e-3
+    # the default policy (residual BNs only)
+    _, res = _grads_with_bn_fusion(monkeypatch, "residual", model, x, g)
+    for a, b in zip(ref, res):
+        assert _rel(b, a) < 5e-3
+    # a second identical step: persistent slot buffers were left zeroed
+    _, again = _grads_with_bn_fusion(monkeypatch, "all", model, x, g)
+    for a, b in zip(got, again):
+        assert _rel(b, a) < 5e-3
+
+
+def test_bn_backward_fusion_falls_back_on_shared_output(monkeypatch):
+    """A BN output read by two convs: each conv's dgrad records a fused
+    reduction, autograd sums the two input gradients, and the BN backward must
+    notice (different tensor) and redo the reduce over the summed gradient."""
+    from distributed_ml_pytorch_amd.ops import functional as Fn
+    from distributed_ml_pytorch_amd.ops.layers import BatchNorm2d, Conv2d
+
+    class Fork(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv0 = Conv2d(64, 64, 3, 1, 1, bias=False)
+            self.bn = BatchNorm2d(64, relu=True)
+            self.a = Conv2d(64, 64, 3, 1, 1, bias=False)
+            self.b = Conv2d(64, 64, 1, 1, 0, bias=False)
+
+        def forward(self, x):
+            h = self.bn(self.conv0(x))
+            return self.a(h) + self.b(h)
+
+    torch.manual_seed(0)
+    model = Fork().cuda()
+    x = torch.randn(4, 64, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    g = torch.randn(4, 64, 16, 16, device="cuda")
+    _, ref = _grads_with_bn_fusion(monkeypatch, False, model, x, g)
+    before = dict(Fn.BN_BWD_FUSE_STATS)
+    _, got = _grads_with_bn_fusion(monkeypatch, "all", model, x, g)
+    assert Fn.BN_BWD_FUSE_STATS["fallback"] > before["fallback"]
+    for a, b in zip(ref, got):
+        assert _rel(b, a) < 5e-3
