@@ -586,10 +586,16 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int
                 "wgrad: dbias must be a contiguous fp32 [CO] GPU tensor");
     db = dbias->data_ptr<float>();
   }
+  Tensor ws;   // slab-mode halo cfg: per-split partials, reduced into dw after the kernel
+  if (db == nullptr) {
+    const long long se = dmp::conv_wgrad_halo_slab_elems((int)cfg, g.B, g.H, g.W, g.CI, g.CO, g.R,
+                                                         g.S, (int)stride, (int)pad);
+    if (se > 0) ws = at::empty({(int64_t)se}, dw.options().memory_format(at::MemoryFormat::Contiguous));
+  }
   dmp::launch_conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                          reinterpret_cast<const uint16_t*>(x.data_ptr()), dw.data_ptr<float>(),
                          g.B, g.H, g.W, g.CI, g.OH, g.OW, g.CO, g.R, g.S, (int)stride, (int)pad,
-                         (int)cfg, cur_stream(), db);
+                         (int)cfg, cur_stream(), db, ws.defined() ? ws.data_ptr<float>() : nullptr);
 }
 
 // few-input-channel (stem) convolutions: x any dense bf16 4-D layout,
@@ -824,7 +830,7 @@ int64_t mat_ld(const Tensor& t, at::ScalarType dt, int64_t rows, int64_t cols,
 // mode 1: a [M,K], b [K,N]; mode 2: a [K,M], b [K,N], c fp32 accumulated.
 void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
           optional<Tensor> c2, optional<Tensor> bias, optional<Tensor> aux,
-          optional<Tensor> dbias, int64_t splits, bool relu, optional<Tensor> part) {
+          optional<Tensor> dbias, int64_t splits, bool relu, optional<Tensor> part, bool slab) {
   TORCH_CHECK(!relu || epi == 0, "gemm: relu only with the store epilogue");
   TORCH_CHECK(mode >= 0 && mode <= 2, "gemm: mode must be 0 (fwd), 1 (dgrad) or 2 (wgrad)");
   TORCH_CHECK(c.dim() == 2 && a.dim() == 2 && b.dim() == 2, "gemm: 2-D operands expected");
@@ -904,10 +910,17 @@ void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
     // bf16 outputs: 16-B row segments, or element stores when N / ldc are not
     // multiples of 8 (any width)
   }
+  // wgrad split-K through a plain-store slab + reduce pass instead of atomics
+  Tensor ws;
+  if (slab && mode == 2 && cfg >= 0) {
+    const int sp = dmp::gemm_effective_splits((int)K, (int)std::max<int64_t>(1, splits));
+    if (sp > 1) ws = at::empty({(int64_t)sp * M * N}, c.options().dtype(at::kFloat));
+  }
   dmp::launch_gemm((int)mode, (int)epi, (int)cfg, reinterpret_cast<const uint16_t*>(a.data_ptr()),
                    (int)lda, reinterpret_cast<const uint16_t*>(b.data_ptr()), (int)ldb,
                    c.data_ptr(), (int)ldc, c2p, biasp, auxp, dbp, (int)M, (int)N, (int)K,
-                   (int)std::max<int64_t>(1, splits), cur_stream(), relu, partp);
+                   (int)std::max<int64_t>(1, splits), cur_stream(), relu, partp,
+                   ws.defined() ? ws.data_ptr<float>() : nullptr);
 }
 
 std::vector<std::vector<int64_t>> gemm_configs() {
@@ -1145,11 +1158,13 @@ std::vector<int64_t> conv_wgrad_halo_configs(int64_t B, int64_t H, int64_t W, in
                                              int64_t CO, int64_t R, int64_t S, int64_t stride,
                                              int64_t pad) {
   std::vector<int64_t> out;
-  for (int i = 0; i < dmp::conv_wgrad_num_halo_configs(); ++i) {
-    const int c = dmp::conv_wgrad_halo_base() + i;
-    if (dmp::conv_wgrad_halo_ok(c, (int)B, (int)H, (int)W, (int)CI, (int)CO, (int)R, (int)S,
-                                (int)stride, (int)pad))
-      out.push_back(c);
+  for (int base : {dmp::conv_wgrad_halo_base(), dmp::conv_wgrad_halo_slab_base()}) {
+    for (int i = 0; i < dmp::conv_wgrad_num_halo_configs(); ++i) {
+      const int c = base + i;
+      if (dmp::conv_wgrad_halo_ok(c, (int)B, (int)H, (int)W, (int)CI, (int)CO, (int)R, (int)S,
+                                  (int)stride, (int)pad))
+        out.push_back(c);
+    }
   }
   return out;
 }
@@ -1258,7 +1273,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("mode"), py::arg("epi"), py::arg("cfg"), py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("c2") = py::none(), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("dbias") = py::none(), py::arg("splits") = 1, py::arg("relu") = false,
-        py::arg("part") = py::none());
+        py::arg("part") = py::none(), py::arg("slab") = false);
   m.def("im2col", &im2col, "NHWC patch rows [B*OH*OW, Kp], k = (r, s, ci), zero-padded",
         py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));
   m.def("col2im", &col2im, "gather-form inverse of im2col -> channels_last dX", py::arg("dcols"),

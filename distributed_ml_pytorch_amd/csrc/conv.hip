@@ -1178,11 +1178,26 @@ static void dispatch(const ConvArgs& a, int cfg, int classes, hipStream_t s) {
   X(11, 128, 64, 32, 2, 1, 1)  \
   X(12, 128, 128, 32, 2, 2, 1) \
   X(13, 256, 128, 32, 4, 2, 1) \
-  X(14, 512, 64, 32, 8, 1, 1)
+  X(14, 512, 64, 32, 8, 1, 1)  \
+  X(18, 224, 64, 32, 2, 2, 1)  \
+  X(19, 224, 64, 32, 2, 1, 1)  \
+  X(20, 112, 64, 32, 1, 2, 1)  \
+  X(21, 112, 128, 32, 1, 4, 1) \
+  X(22, 112, 128, 32, 1, 2, 1) \
+  X(23, 448, 64, 32, 4, 2, 1)  \
+  X(24, 224, 64, 32, 2, 2, 2)  \
+  X(25, 112, 128, 32, 1, 4, 2)
+// 18-25: whole-row tiles of 7 x 16 pixels for the ImageNet ResNet widths (56-
+// and 28-pixel rows: 4 / 2 / 8 rows of 56, 4 rows of 28), where none of the
+// power-of-two tiles above is a whole number of rows.  Ids 15-17 are the
+// persistent kernels below (kept: ids are cached by the tuner).
 
-constexpr int kHaloBase = 100, kNumHaloConfigs = 15;
-// persistent 64-channel halo kernels (conv_halo64p_kernel): ids after the tile configs
-constexpr int kHaloPBase = kHaloBase + kNumHaloConfigs, kNumHaloPConfigs = 3;
+constexpr int kHaloBase = 100, kNumHaloConfigs = 26;   // ids kHaloBase + [0, 26)
+// persistent 64-channel halo kernels (conv_halo64p_kernel): ids 115-117
+constexpr int kHaloPBase = kHaloBase + 15, kNumHaloPConfigs = 3;
+__host__ __device__ constexpr bool is_halop(int cfg) {
+  return cfg >= kHaloPBase && cfg < kHaloPBase + kNumHaloPConfigs;
+}
 
 static bool halo_cfg(int cfg, int* bm, int* bn, int* bk, int* nw, int* ns) {
   switch (cfg - kHaloBase) {
@@ -1262,7 +1277,7 @@ static bool halop_geom(int cfg, int B, int H, int W, int C, int R, int S, int st
 }
 
 bool conv_halo_ok(int cfg, int H, int W, int C, int R, int S, int stride, int pad) {
-  if (cfg >= kHaloPBase) {
+  if (is_halop(cfg)) {
     HaloPGeom g;
     int bm, ns, nw;
     size_t lds;
@@ -1273,7 +1288,7 @@ bool conv_halo_ok(int cfg, int H, int W, int C, int R, int S, int stride, int pa
   return halo_geom(cfg, H, W, C, R, S, stride, pad, &g, &lds);
 }
 
-int conv_num_halo_configs() { return kNumHaloConfigs + kNumHaloPConfigs; }
+int conv_num_halo_configs() { return kNumHaloConfigs; }
 int conv_halo_base() { return kHaloBase; }
 
 template <int BM, int BN, int BK, int WM, int WN, int NS, bool FLIP, bool STATS>
@@ -1319,7 +1334,7 @@ static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
   HaloGeom g;
   size_t lds;
   if (a.GH != a.OH || a.GW != a.OW) return false;
-  if (cfg >= kHaloPBase) {
+  if (is_halop(cfg)) {
     HaloPGeom pg;
     int bm, ns, nw;
     size_t plds;

@@ -40,6 +40,7 @@ struct WgradArgs {
   long long P;
   int p_chunk;      // rows of P per block (multiple of BP)
   float* dbias;     // optional fp32 [CO] += sum_p dY[p][co] (linear / conv bias grad)
+  float* slab;      // halo wgrad, slab mode: per-split partials [splits][CO][R][S][CI]
 };
 
 __device__ __forceinline__ f32x4 mfma16w(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -530,6 +531,7 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
         float* dst = a.dw + (long long)co * K + ((r0 + t / 3) * 3 + t % 3) * C + ci;
         if (atomic == 1) atomicAdd(dst, acc[t][i][rr]);
         else if (atomic == 0) *dst += acc[t][i][rr];
+        else if (atomic == 3) a.slab[(long long)bz * CO * K + (dst - a.dw)] = acc[t][i][rr];
         else *dst = acc[t][i][rr];   // timing diagnostic only (DMP_WGRAD_HALO_DIAG=store)
       }
 }
@@ -538,18 +540,31 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
 // target block count 128 << spl; variant -> (NS, TR) below (ids 1000..1011 are
 // the round-1 kernel's configs: NS 2, one tap row per block)
 constexpr int kWhBase = 1000;
-constexpr int kWhVariants = 6;
-constexpr int kWhNS[kWhVariants] = {2, 3, 4, 2, 3, 2};
-constexpr int kWhTR[kWhVariants] = {1, 1, 1, 3, 3, 1};
-constexpr int kWhPG[kWhVariants] = {1, 1, 1, 1, 1, 2};   // pixel groups (8 waves when 2)
+// variants 6-7: BM fixed at 224 = 4 rows of 56 (ImageNet ResNet stage 1, where no
+// power-of-two tile is a whole number of rows); only bm_sel 0 is valid there
+constexpr int kWhVariants = 8;
+constexpr int kWhNS[kWhVariants] = {2, 3, 4, 2, 3, 2, 2, 3};
+constexpr int kWhTR[kWhVariants] = {1, 1, 1, 3, 3, 1, 1, 1};
+constexpr int kWhPG[kWhVariants] = {1, 1, 1, 1, 1, 2, 1, 1};   // pixel groups (8 waves when 2)
+constexpr int kWhBM[kWhVariants] = {0, 0, 0, 0, 0, 0, 224, 224};   // 0: 64 << bm_sel
+
+// slab mode (ids kWhSlabBase + i = halo config kWhBase + i): the split-K partials
+// go to a [splits][dW] fp32 slab with plain stores (~6 TB/s chip-wide) and one
+// streaming pass adds them into dW, instead of fp32 atomics (~1.3 TB/s of added
+// bytes, ~25 % of the 64-channel wgrad: profiles/conv_kernels_r2.txt); offered
+// for the NS-2 one-tap-row variants when the geometry splits K
+constexpr int kWhSlabBase = 3000;
+constexpr bool wh_slab_variant(int var) { return var == 0 || var == 5 || var == 6; }
 
 static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R, int S, int stride,
                             int pad, WgradHaloGeom* g, int* bm_out, int* ns_out, int* tr_out,
                             int* pg_out, size_t* lds, int* splits) {
+  if (cfg >= kWhSlabBase) cfg -= kWhSlabBase - kWhBase;
   const int id = cfg - kWhBase;
   if (id < 0 || id >= 12 * kWhVariants) return false;
   const int var = id / 12, rest = id % 12;
-  const int bm = 64 << (rest / 4), target = 128 << (rest % 4);
+  if (kWhBM[var] != 0 && rest / 4 != 0) return false;
+  const int bm = kWhBM[var] != 0 ? kWhBM[var] : 64 << (rest / 4), target = 128 << (rest % 4);
   const int ns = kWhNS[var], tr = kWhTR[var], pg = kWhPG[var];
   if (pg == 2 && bm < 128) return false;
   if (R != 3 || S != 3 || stride != 1 || pad != 1 || CI % 64 || CO % 64) return false;
@@ -596,11 +611,57 @@ bool conv_wgrad_halo_ok(int cfg, int B, int H, int W, int CI, int CO, int R, int
   WgradHaloGeom g;
   int bm, ns, tr, pg, sp;
   size_t lds;
-  return wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &pg, &lds,
-                         &sp);
+  if (!wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &pg, &lds, &sp))
+    return false;
+  if (cfg >= kWhSlabBase) return sp > 1 && wh_slab_variant((cfg - kWhSlabBase) / 12);
+  return true;
+}
+// fp32 elements of the slab a slab-mode cfg needs (0: not a slab cfg / no split)
+long long conv_wgrad_halo_slab_elems(int cfg, int B, int H, int W, int CI, int CO, int R, int S,
+                                     int stride, int pad) {
+  if (cfg < kWhSlabBase || !conv_wgrad_halo_ok(cfg, B, H, W, CI, CO, R, S, stride, pad)) return 0;
+  WgradHaloGeom g;
+  int bm, ns, tr, pg, sp;
+  size_t lds;
+  wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &pg, &lds, &sp);
+  return (long long)sp * CO * R * S * CI;
 }
 int conv_wgrad_halo_base() { return kWhBase; }
+int conv_wgrad_halo_slab_base() { return kWhSlabBase; }
 int conv_wgrad_num_halo_configs() { return 12 * kWhVariants; }
+
+// dW[e] += sum_s slab[s][e]: a block = 16 float4 columns x 16 split lanes (the
+// split count runs to the hundreds on the 64-channel layers: a thread per
+// column walking every split was latency-bound), LDS reduce over the lanes
+__global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const float* __restrict__ slab,
+                                                                float* __restrict__ dw,
+                                                                long long n4, int splits) {
+  __shared__ float4 red[16][16];
+  const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+  const long long v = (long long)blockIdx.x * 16 + lx;
+  const float4* s4 = reinterpret_cast<const float4*>(slab);
+  float4 t = {0.f, 0.f, 0.f, 0.f};
+  if (v < n4) {
+    int sp = ly;
+#pragma unroll 4
+    for (; sp < splits; sp += 16) {
+      const float4 u = s4[sp * n4 + v];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+  }
+  red[ly][lx] = t;
+  __syncthreads();
+  if (ly == 0 && v < n4) {
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      const float4 u = red[k][lx];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    float4 d = reinterpret_cast<float4*>(dw)[v];
+    d.x += t.x; d.y += t.y; d.z += t.z; d.w += t.w;
+    reinterpret_cast<float4*>(dw)[v] = d;
+  }
+}
 
 template <int BM, int NS, int TR, int PG = 1>
 static void launch_wgrad_halo_t(const WgradArgs& a, const WgradHaloGeom& g, size_t lds, int splits,
@@ -617,13 +678,25 @@ static void launch_wgrad_halo_t(const WgradArgs& a, const WgradHaloGeom& g, size
     diag = (e && e[0] == 's') ? 1 : 0;
   }
   const dim3 grid((unsigned)(a.CI / 64), (unsigned)(a.CO / 64 * (3 / TR)), (unsigned)splits);
+  const int mode = diag ? 2 : (splits > 1 ? (a.slab != nullptr ? 3 : 1) : 0);
   hipLaunchKernelGGL((conv_wgrad_halo_kernel<BM, NS, TR, PG>), grid, dim3(256 * PG), lds, s, a, g,
-                     diag ? 2 : (splits > 1 ? 1 : 0));
+                     mode);
+  if (mode == 3) {
+    const long long n4 = (long long)a.CO * 9 * a.CI / 4;
+    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0,
+                       s, a.slab, a.dw, n4, splits);
+  }
 }
 
 template <int NS, int TR>
 static void launch_wgrad_halo_bm(int bm, const WgradArgs& a, const WgradHaloGeom& g, size_t lds,
                                  int sp, hipStream_t s) {
+  if constexpr (TR == 1) {
+    if (bm == 224) {
+      launch_wgrad_halo_t<224, NS, 1>(a, g, lds, sp, s);
+      return;
+    }
+  }
   if (bm == 64) launch_wgrad_halo_t<64, NS, TR>(a, g, lds, sp, s);
   else if (TR == 3 || bm == 128) launch_wgrad_halo_t<128, NS, TR>(a, g, lds, sp, s);
   else launch_wgrad_halo_t<(TR == 3 ? 128 : 256), NS, TR>(a, g, lds, sp, s);   // TR 3: BM <= 128
@@ -645,9 +718,13 @@ static void launch_wgrad_variant(const WgradArgs& a, dim3 grid, int bp, int ns, 
 
 void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int W, int CI,
                        int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                       hipStream_t s, float* dbias) {
+                       hipStream_t s, float* dbias, float* slab) {
   WgradArgs a{dy, x, dw, B, H, W, CI, OH, OW, CO, R, S, stride, pad, (long long)B * OH * OW, 0,
-              dbias};
+              dbias, nullptr};
+  if (cfg >= kWhSlabBase) {
+    if (slab != nullptr) a.slab = slab;
+    else cfg -= kWhSlabBase - kWhBase;   // no slab given: the atomic variant
+  }
   if (cfg >= kWhBase && dbias == nullptr) {
     WgradHaloGeom g;
     int bm, ns, tr, pg, sp;

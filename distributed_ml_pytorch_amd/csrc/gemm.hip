@@ -64,6 +64,8 @@ struct GemmArgs {
   int relu;           // EPI_STORE: max(0, .) after bias / addend (linear -> ReLU)
   float* part;        // EPI_STORE: optional BatchNorm slot sums [2][kBnSlots][N] of the
                       // stored bf16 outputs (a 1x1 conv feeding a BatchNorm)
+  float* slab;        // EPI_ACC32 split-K: per-split fp32 partials [splits][M][N] written
+                      // with plain stores, summed into C by gemm_slab_reduce_kernel
 };
 
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -282,6 +284,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
       // D layout: lane holds rows m = 4*(lane>>4) + r of column n = lane & 15
       float* C = reinterpret_cast<float*>(g.c);
       const bool atomic = gridDim.y > 1;
+      // split-K into a slab: plain stores (~6 TB/s chip-wide) instead of fp32
+      // atomics (~1.3 TB/s of added bytes), reduced by a streaming pass after
+      float* S = g.slab != nullptr ? g.slab + (long long)blockIdx.y * g.M * g.N : nullptr;
       if (do_bias && (lane & 15) == 0) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -300,9 +305,13 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
           for (int r = 0; r < 4; ++r) {
             const int m = m0 + ra + i * 16 + 4 * (lane >> 4) + r;
             if (m < g.M && n < g.N) {
-              float* p = C + (long long)m * g.ldc + n;
-              if (atomic) atomicAdd(p, acc[i][j][r]);
-              else *p += acc[i][j][r];
+              if (S != nullptr) {
+                S[(long long)m * g.N + n] = acc[i][j][r];
+              } else {
+                float* p = C + (long long)m * g.ldc + n;
+                if (atomic) atomicAdd(p, acc[i][j][r]);
+                else *p += acc[i][j][r];
+              }
             }
           }
         }
@@ -576,6 +585,37 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
   }
 }
 
+// C[m][n] (ldc) += sum over the splits of slab[s][m][n]; 4 columns per thread
+// when rows are whole float4s
+__global__ void __launch_bounds__(256) gemm_slab_reduce_kernel(const float* __restrict__ slab,
+                                                               float* __restrict__ c, int M, int N,
+                                                               int ldc, int splits) {
+  const long long MN = (long long)M * N;
+  const long long gs = (long long)gridDim.x * blockDim.x;
+  if ((N & 3) == 0 && (ldc & 3) == 0) {
+    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < MN / 4; v += gs) {
+      const long long e = v * 4;
+      const long long m = e / N, n = e - m * N;
+      float4 t = *reinterpret_cast<const float4*>(slab + e);
+      for (int sp = 1; sp < splits; ++sp) {
+        const float4 u = *reinterpret_cast<const float4*>(slab + sp * MN + e);
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      }
+      float4* o = reinterpret_cast<float4*>(c + m * ldc + n);
+      float4 cv = *o;
+      cv.x += t.x; cv.y += t.y; cv.z += t.z; cv.w += t.w;
+      *o = cv;
+    }
+  } else {
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < MN; e += gs) {
+      const long long m = e / N, n = e - m * N;
+      float t = slab[e];
+      for (int sp = 1; sp < splits; ++sp) t += slab[sp * MN + e];
+      c[m * ldc + n] += t;
+    }
+  }
+}
+
 template <bool AT, bool BT, int EPI>
 void launch_small(const GemmArgs& g, int splits, hipStream_t s) {
   hipLaunchKernelGGL((gemm_small_kernel<AT, BT, EPI>),
@@ -660,7 +700,7 @@ void gemm_config_info(int cfg, int* info) {
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
-                 hipStream_t s, bool relu, float* part) {
+                 hipStream_t s, bool relu, float* part, float* slab) {
   GemmArgs g{};
   g.relu = relu ? 1 : 0;
   g.part = part;
@@ -676,8 +716,23 @@ void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const u
     if (epi == EPI_DGELU) launch_mode<false, true, EPI_DGELU>(cfg, g, 1, s);
     else launch_mode<false, true, EPI_STORE>(cfg, g, 1, s);
   } else {
+    // slab split-K only for the MFMA tiles with more than one split
+    if (slab != nullptr && splits > 1 && cfg >= 0) g.slab = slab;
     launch_mode<true, true, EPI_ACC32>(cfg, g, splits, s);
+    if (g.slab != nullptr) {
+      const long long work = ((N & 3) == 0 && (ldc & 3) == 0) ? (long long)M * N / 4
+                                                               : (long long)M * N;
+      hipLaunchKernelGGL(gemm_slab_reduce_kernel, dim3(stream_grid(work, 256)), dim3(256), 0, s,
+                         slab, reinterpret_cast<float*>(c), M, N, ldc, splits);
+    }
   }
+}
+
+// effective split count launch_gemm uses for (K, requested splits) in mode 2
+int gemm_effective_splits(int K, int splits) {
+  if (splits < 1) splits = 1;
+  const int k_chunk = ((K + splits - 1) / splits + 63) / 64 * 64;
+  return (K + k_chunk - 1) / k_chunk;
 }
 
 }  // namespace dmp

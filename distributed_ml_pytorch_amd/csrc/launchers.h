@@ -100,6 +100,11 @@ int conv_wgrad_halo_base();
 int conv_wgrad_num_halo_configs();
 bool conv_wgrad_halo_ok(int cfg, int B, int H, int W, int CI, int CO, int R, int S, int stride,
                         int pad);
+// slab-mode halo wgrad ids: conv_wgrad_halo_slab_base() + the same [0, n) (plain-store
+// split-K partials + a reduce pass); fp32 slab elements a cfg needs (0: none)
+int conv_wgrad_halo_slab_base();
+long long conv_wgrad_halo_slab_elems(int cfg, int B, int H, int W, int CI, int CO, int R, int S,
+                                     int stride, int pad);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int B, int H,
                      int W, int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
                      int cfg, hipStream_t s, const float* bias = nullptr, bool relu = false);
@@ -124,7 +129,7 @@ void launch_conv_weight_transpose(const uint16_t* w, uint16_t* wt, int CO, int R
 // dbias: optional fp32 [CO] += column sums of dY (gather kernel only; halo cfgs fall back)
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int B, int H, int W,
                        int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                       hipStream_t s, float* dbias = nullptr);
+                       hipStream_t s, float* dbias = nullptr, float* slab = nullptr);
 
 // conv_small.hip: few-input-channel (stem) convolutions, VALU
 int conv_small_max_k();
@@ -170,7 +175,10 @@ void gemm_config_info(int cfg, int* info);   // {BM, BN, threads, stages, BK}
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
-                 hipStream_t s, bool relu = false, float* part = nullptr);
+                 hipStream_t s, bool relu = false, float* part = nullptr,
+                 float* slab = nullptr);
+// effective split-K count of launch_gemm (mode 2) for K and a requested count
+int gemm_effective_splits(int K, int splits);
 
 // im2col.hip: patch matrix [B*OH*OW][Kp] (k = (r, s, ci), zero-padded) and its
 // gather-form inverse; ReLU backward from the saved output

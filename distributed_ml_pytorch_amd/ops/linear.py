@@ -77,14 +77,22 @@ def _mfma_ok(mode: int, M: int, N: int, K: int, *mats) -> bool:
             and (N % 8 == 0 or b.stride(0) >= c8(N)))
 
 
-# candidate encoding: (cfg + 1) * 1024 + splits (cfg -1 = any-shape kernel);
-# _BLAS < 0; the tuner's "no pick" is -1
-def _enc(cfg: int, splits: int) -> int:
-    return (cfg + 1) * 1024 + splits
+# candidate encoding: (cfg + 1) * 1024 + splits (cfg -1 = any-shape kernel),
+# + _SLAB for a wgrad split-K reduced through a plain-store slab instead of fp32
+# atomics; _BLAS < 0; the tuner's "no pick" is -1
+_SLAB = 1 << 20
+
+
+def _enc(cfg: int, splits: int, slab: bool = False) -> int:
+    return (cfg + 1) * 1024 + splits + (_SLAB if slab else 0)
 
 
 def _dec(e: int):
-    return e // 1024 - 1, e % 1024
+    return (e % _SLAB) // 1024 - 1, e % 1024
+
+
+def _dec_slab(e: int) -> bool:
+    return e >= _SLAB
 
 
 def _wgrad_splits(M: int, N: int, K: int, bm: int, bn: int):
@@ -135,6 +143,7 @@ def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bo
             continue
         if mode == 2:
             cands += [_enc(cid, s) for s in _wgrad_splits(M, N, K, bm, bn)]
+            cands += [_enc(cid, s, True) for s in _wgrad_splits(M, N, K, bm, bn) if s > 1]
         else:
             cands.append(_enc(cid, 1))
     if M * N * K < (1 << 22):
@@ -202,7 +211,7 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
                     cfg_e, split_e = _dec(e)
                     ps = torch.zeros_like(part) if part is not None else None
                     native().gemm(mode, epi, cfg_e, a, b, cs, c2, bias, aux, ds, split_e, relu,
-                                  ps)
+                                  ps, _dec_slab(e))
             pick = TUNER.best(key, run, cands)
             if pick == -1:
                 pick = _default(mode, M, N, K, ok)
@@ -210,7 +219,8 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
         _blas(mode, a, b, c, bias)
         return
     cfg, splits = _dec(pick)
-    native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits, relu, part)
+    native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits, relu, part,
+                  _dec_slab(pick))
 
 
 def _rows(t, k):

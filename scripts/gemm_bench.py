@@ -62,16 +62,26 @@ def main():
                   + f"  {fl / tb / 1e6:.0f}/{fl / best / 1e6:.0f}", flush=True)
         # wgrad: fp32 accumulate, split-K sweep
         tb = timeit(lambda: torch.ops.aten.addmm.dtype_out(g, dy.t(), x, torch.float32, out=g))
-        res = {}
-        for c in [c for c in cfgs if ok(2, c)]:
-            for s in (1, 2, 4, 8):
-                res[(c, s)] = timeit(lambda: native().gemm(2, 3, c, dy, x, g, splits=s))
-        bestk = min(res, key=res.get)
-        print(f"{K:>5}->{N:<6} {'wgrad':>6} {tb:8.1f} "
-              + " ".join(f"{min(res[(c, s)] for s in (1, 2, 4, 8)):8.1f}" if ok(2, c) else "     nan"
-                         for c in cfgs)
-              + f"  {fl / tb / 1e6:.0f}/{fl / res[bestk] / 1e6:.0f}  best (cfg, splits)={bestk}",
-              flush=True)
+        for slab in (False, True):
+            res = {}
+            for c in [c for c in cfgs if ok(2, c)]:
+                for s in (1, 2, 4, 8, 16):
+                    res[(c, s)] = timeit(lambda: native().gemm(2, 3, c, dy, x, g, splits=s,
+                                                               slab=slab))
+            bestk = min(res, key=res.get)
+            tag = "wgradS" if slab else "wgrad"
+            print(f"{K:>5}->{N:<6} {tag:>6} {tb:8.1f} "
+                  + " ".join(f"{min(res[(c, s)] for s in (1, 2, 4, 8, 16)):8.1f}" if ok(2, c)
+                             else "     nan" for c in cfgs)
+                  + f"  {fl / tb / 1e6:.0f}/{fl / res[bestk] / 1e6:.0f}  best (cfg, splits)={bestk}",
+                  flush=True)
+        # slab split-K numerics vs the atomic path
+        g1 = torch.zeros_like(g)
+        g2 = torch.zeros_like(g)
+        native().gemm(2, 3, bestk[0], dy, x, g1, splits=4)
+        native().gemm(2, 3, bestk[0], dy, x, g2, splits=4, slab=True)
+        err = float((g1 - g2).norm() / g1.norm())
+        assert err < 1e-5, err
 
 
 if __name__ == "__main__":

@@ -30,9 +30,14 @@ def t_us(fn, it=10, rounds=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--shapes", default="r18", choices=["r18", "r50"],
+                    help="r18: CIFAR ResNet-18 layers; r50: ImageNet ResNet-50 stage 1-2 3x3 convs")
+    ap.add_argument("--igemm", type=int, default=0, help="also time the implicit-GEMM tiles")
     a = ap.parse_args()
     nat = native()
-    for C, HW in ((64, 32), (128, 16), (256, 8), (512, 4)):
+    shapes = ((64, 32), (128, 16), (256, 8), (512, 4)) if a.shapes == "r18" else \
+        ((64, 56), (128, 28), (256, 14))
+    for C, HW in shapes:
         B = a.batch
         x = torch.randn(B, C, HW, HW, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
         w = (torch.randn(C, C, 3, 3, device="cuda") * 0.02).to(torch.bfloat16).contiguous(memory_format=CL)
@@ -40,7 +45,11 @@ def main():
         tf = 2.0 * B * HW * HW * C * C * 9 / 1e12
         for name, run in (("fwd", lambda c: nat.conv_fwd(x, w, 1, 1, True, c)),
                           ("dgrad", lambda c: nat.conv_dgrad(dy, w, HW, HW, 1, 1, c))):
-            res = {c: t_us(lambda c=c: run(c)) for c in nat.conv_halo_configs(HW, HW, C, 3, 3, 1, 1)}
+            cands = list(nat.conv_halo_configs(HW, HW, C, 3, 3, 1, 1))
+            if a.igemm:
+                cands += list(range(nat.conv_num_configs() if hasattr(nat, "conv_num_configs")
+                                    else len(nat.conv_configs())))
+            res = {c: t_us(lambda c=c: run(c)) for c in cands}
             best = min(res, key=res.get)
             print(f"C={C:3d} {HW:2d}x{HW:<2d} {name:5s} best {best} {res[best]:6.1f} us "
                   f"{tf / res[best] * 1e6:5.0f} TF/s | " +

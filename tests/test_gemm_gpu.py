@@ -79,9 +79,10 @@ def test_gemm_dgrad(M, K, N, dgelu):
 
 
 @pytest.mark.parametrize("M,K,N", SHAPES)
-@pytest.mark.parametrize("splits", [1, 3])
-def test_gemm_wgrad(M, K, N, splits):
-    """gW[N, K] += dY^T X, gb[N] += colsum(dY), fp32 accumulate (split-K with atomics)."""
+@pytest.mark.parametrize("splits,slab", [(1, False), (3, False), (3, True)])
+def test_gemm_wgrad(M, K, N, splits, slab):
+    """gW[N, K] += dY^T X, gb[N] += colsum(dY), fp32 accumulate (split-K with atomics,
+    or through a plain-store partial slab + reduce pass)."""
     from distributed_ml_pytorch_amd.ops._ext import native
 
     torch.manual_seed(3)
@@ -94,7 +95,7 @@ def test_gemm_wgrad(M, K, N, splits):
     for cfg in _cfgs(2):
         g = torch.full((N, K), 0.25, device=dev)
         gb = torch.full((N,), -0.5, device=dev)
-        native().gemm(2, 3, cfg, dy, x, g, dbias=gb, splits=splits)
+        native().gemm(2, 3, cfg, dy, x, g, dbias=gb, splits=splits, slab=slab)
         assert _rel(g - 0.25, ref_w) < 2e-3, cfg
         assert _rel(gb + 0.5, ref_b) < 2e-3, cfg
 
