@@ -324,11 +324,11 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
       // move whole row segments.
       constexpr int WROWS = BM / WM, WCOLS = BN / WN, CPR = WCOLS / 8, RPI = 64 / CPR;
       // 16-B row padding when it fits, else (256x256 ring) an XOR swizzle of the
-      // 16-B chunks by row & 7 (needs 8 chunks per row)
+      // 16-B chunks by row & 7 (needs a multiple of 8 chunks per row)
       constexpr bool SWZ = NW * WROWS * (WCOLS + 8) > NS * STAGE;
       constexpr int PITCH = SWZ ? WCOLS : WCOLS + 8;
       static_assert(NW * WROWS * PITCH <= NS * STAGE, "epilogue tile fits in the ring's LDS");
-      static_assert(!SWZ || CPR == 8, "swizzled epilogue tile needs 8 chunks per row");
+      static_assert(!SWZ || CPR % 8 == 0, "swizzled epilogue tile needs 8k chunks per row");
       auto pchunk = [](int row, int c) { return SWZ ? (c ^ (row & 7)) : c; };
       constexpr int NR = (WROWS + RPI - 1) / RPI;   // row segments per lane
       const int cbytes = (int)(2LL * g.M * g.ldc);
@@ -640,6 +640,8 @@ constexpr Cfg kCfgs[] = {
     {128, 128, 32, 2, 2, 4},   // 7:  64 KiB, 4 waves, 2 blocks/CU, 3 k-tiles in flight
     {256, 128, 64, 2, 2, 3},   // 8: 144 KiB, 4 waves of 128x64 (1 wave / SIMD)
 };
+// (4 waves of 128x128 per 256x256 / 192x256 tile, accumulators in AGPRs: 20-40 %
+// slower than the 8-wave tiles on every ViT shape -- profiles/gemm_vs_hipblaslt_r2.txt)
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 constexpr bool cfg_ok(const Cfg& c, bool at, bool bt) {
