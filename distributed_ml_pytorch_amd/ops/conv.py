@@ -52,7 +52,9 @@ _STEM = os.environ.get("DMP_STEM", "small")
 # stream).  Opt-in (DMP_WGRAD_STREAM=1): measured on ResNet-18/CIFAR bs256 the
 # concurrent wgrad grids delay the single-block BN finalize kernels on the
 # critical path (bwd finalize 96 -> 244 us/step) and the step got 3.6% slower
-# (profiles/bench_steady_state_wgrad_stream_r1.txt).
+# (profiles/bench_steady_state_wgrad_stream_r1.txt); round 2 at bs512 (GEMM-route
+# 1x1 wgrads included): ResNet-18 -4 %, ResNet-50 +0.7 % (noise), and replaying
+# the graph on a high-priority stream -30 % (profiles/wgrad_stream_ab_r2.txt).
 _WG_STREAM_ENABLED = os.environ.get("DMP_WGRAD_STREAM", "0") == "1"
 _WG_STREAMS: dict = {}
 _WG_KEEP: list = []          # operands kept alive until the join
@@ -326,10 +328,13 @@ class _NativeConv(Function):
                     _gemm1x1_wgrad(dy, x, gw)
                     gw = gw.to(master.dtype)
                 else:
-                    _gemm1x1_wgrad(dy, x, gg)
                     cb = getattr(master, "_dmp_grad_ready", None)
-                    if cb is not None:
-                        cb(master)
+                    if cb is None and _WG_STREAM_ENABLED:
+                        _side_wgrad(x.device, lambda: _gemm1x1_wgrad(dy, x, gg), dy, x)
+                    else:
+                        _gemm1x1_wgrad(dy, x, gg)
+                        if cb is not None:
+                            cb(master)
             elif g is not None and g.is_contiguous(memory_format=torch.channels_last):
                 cb = getattr(master, "_dmp_grad_ready", None)
                 if cb is None and _WG_STREAM_ENABLED:
