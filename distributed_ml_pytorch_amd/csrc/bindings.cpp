@@ -1,4 +1,5 @@
 #include <cmath>
+#include <cstdlib>
 // Python bindings for the gfx950 kernels. Every op checks device, dtype,
 // contiguity and alignment on the host before launching (a mis-shaped launch
 // of a hand-written kernel must fail loudly here, never fault on the GPU), and
@@ -677,6 +678,16 @@ void stem_wgrad(Tensor dy, Tensor xs, Tensor dw) {
   dmp::launch_stem_wfold(dwp.data_ptr<float>(), dw.data_ptr<float>(), st);
 }
 
+// 3x3/s1/p1, CI <= 3, CO = 64 stems on MFMA (conv_small.hip stem3_*); DMP_STEM3=0
+// keeps the VALU kernels (A/B)
+bool stem3_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DMP_STEM3");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 std::vector<Tensor> conv_small_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad,
                                    bool want_stats, optional<Tensor> slots) {
   check_gpu(w, "w");
@@ -691,6 +702,15 @@ std::vector<Tensor> conv_small_fwd(Tensor x, Tensor w, int64_t stride, int64_t p
   if (want_stats) {
     G = dmp::kBnSlots;
     part = bn_slots(slots, g.CO, x.options());
+  }
+  if (stem3_enabled() && dmp::stem3_supported(g.CI, g.R, g.S, g.CO, (int)stride, (int)pad, g.W)) {
+    dmp::launch_stem3_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), (int)(2 * x.numel()),
+                          (int)x.stride(0), (int)x.stride(2), (int)x.stride(3), (int)x.stride(1),
+                          reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                          reinterpret_cast<uint16_t*>(y.data_ptr()),
+                          want_stats ? part.data_ptr<float>() : nullptr, g.B, g.H, g.W, g.CI,
+                          cur_stream());
+    return {y, part, at::scalar_tensor(G, at::kLong)};
   }
   dmp::launch_conv_small_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                              (int)(2 * x.numel()), (int)x.stride(0),
@@ -713,6 +733,14 @@ void conv_small_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pa
   TORCH_CHECK(dy.size(0) == g.B && dy.size(1) == g.CO && dy.size(2) == g.OH && dy.size(3) == g.OW,
               "small wgrad: dy shape mismatch");
   const long long P = (long long)g.B * g.OH * g.OW;
+  if (stem3_enabled() && dmp::stem3_supported(g.CI, g.R, g.S, g.CO, (int)stride, (int)pad, g.W)) {
+    dmp::launch_stem3_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                            reinterpret_cast<const uint16_t*>(x.data_ptr()), (int)(2 * x.numel()),
+                            (int)x.stride(0), (int)x.stride(2), (int)x.stride(3),
+                            (int)x.stride(1), dw.data_ptr<float>(), g.B, g.H, g.W, g.CI,
+                            cur_stream());
+    return;
+  }
   const int G = dmp::conv_small_wgrad_blocks(P, g.CO, g.R, g.S, g.CI);
   auto ws = at::empty({(int64_t)G * g.CO * g.R * g.S * g.CI}, dw.options());
   dmp::launch_conv_small_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
@@ -1200,6 +1228,107 @@ std::vector<Tensor> bn_fwd_from_partials(Tensor x, Tensor part, int64_t G, optio
   return {y, stats, mask};
 }
 
+
+// BatchNorm with the finalize folded into the apply passes (bn.hip fold kernels).
+// part: the forward slot sums (already filled by the producing conv when
+// have_partials, else reduced here first); zero_buf: the layer's backward slots,
+// zeroed by the apply for the next backward.
+std::vector<Tensor> bn_fwd_fold(Tensor x, Tensor part, bool have_partials, optional<Tensor> res,
+                                optional<Tensor> gamma, optional<Tensor> beta,
+                                optional<Tensor> running_mean, optional<Tensor> running_var,
+                                double momentum, double eps, bool relu, bool want_mask,
+                                optional<Tensor> zero_buf) {
+  check_nhwc_bf16(x, "x");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: C must be a multiple of 8 and <= 2048, got ", C);
+  auto fopt = x.options().dtype(at::kFloat);
+  part = bn_slots(part, C, fopt);
+  float* zb = nullptr;
+  if (zero_buf.has_value() && zero_buf->defined()) {
+    zb = bn_slots(zero_buf, C, fopt).data_ptr<float>();
+    TORCH_CHECK(zb != part.data_ptr<float>(), "bn fold: zero_buf must not alias part");
+  }
+  if (res) {
+    check_nhwc_bf16(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "res shape mismatch");
+  }
+  for (auto* t : {&gamma, &beta, &running_mean, &running_var}) {
+    if (t->has_value()) {
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == C &&
+                      (*t)->is_contiguous(),
+                  "bn affine/running tensors must be contiguous fp32 [C] on the GPU");
+    }
+  }
+  auto y = at::empty_like(x);
+  auto stats = at::empty({4, C}, fopt);
+  Tensor mask;
+  if (want_mask && relu) mask = at::empty({M, C / 8}, x.options().dtype(at::kByte));
+  dmp::launch_bn_fwd_fold(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                          res ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr,
+                          reinterpret_cast<uint16_t*>(y.data_ptr()), ptr_or_null<float>(gamma),
+                          ptr_or_null<float>(beta), ptr_or_null<float>(running_mean),
+                          ptr_or_null<float>(running_var), stats.data_ptr<float>(),
+                          part.data_ptr<float>(), zb, M, (int)C, (float)momentum, (float)eps,
+                          relu, have_partials, cur_stream(),
+                          mask.defined() ? mask.data_ptr<uint8_t>() : nullptr);
+  return {y, stats, mask};
+}
+
+// backward: reduce into `slots` (the layer's backward slots, zero on entry), then
+// the folded apply; zero_buf: the forward slot sums this layer's forward read
+std::vector<Tensor> bn_bwd_fold(Tensor x, Tensor dy, optional<Tensor> y, optional<Tensor> gamma,
+                                Tensor stats, optional<Tensor> dgamma, optional<Tensor> dbeta,
+                                bool relu, bool want_dres, Tensor slots, optional<Tensor> mask,
+                                optional<Tensor> zero_buf) {
+  check_nhwc_bf16(x, "x");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: bad C");
+  if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.dim() == 4)
+    dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc_bf16(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "dy shape mismatch");
+  const bool have_y = relu && y.has_value() && y->defined();
+  if (have_y) {
+    check_nhwc_bf16(*y, "y");
+    TORCH_CHECK(y->sizes() == x.sizes(), "y shape mismatch");
+  }
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * C, "bad stats");
+  for (auto* t : {&gamma, &dgamma, &dbeta}) {
+    if (t->has_value()) {
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == C &&
+                      (*t)->is_contiguous(),
+                  "bn gamma/dgamma/dbeta must be contiguous fp32 [C]");
+    }
+  }
+  auto fopt = x.options().dtype(at::kFloat);
+  auto part = bn_slots(slots, C, fopt);
+  float* zb = nullptr;
+  if (zero_buf.has_value() && zero_buf->defined()) {
+    zb = bn_slots(zero_buf, C, fopt).data_ptr<float>();
+    TORCH_CHECK(zb != part.data_ptr<float>(), "bn fold: zero_buf must not alias slots");
+  }
+  auto dx = at::empty_like(x);
+  Tensor dres;
+  if (want_dres) dres = at::empty_like(x);
+  const uint8_t* mptr = nullptr;
+  if (relu && mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() == M * C / 8,
+                "bn: ReLU bit mask must be a contiguous uint8 [M, C/8] GPU tensor");
+    mptr = mask->data_ptr<uint8_t>();
+  }
+  dmp::launch_bn_bwd_fold(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                          reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                          have_y ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr,
+                          ptr_or_null<float>(gamma), stats.data_ptr<float>(),
+                          ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta),
+                          part.data_ptr<float>(), zb, reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                          want_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr, M,
+                          (int)C, relu, cur_stream(), mptr);
+  return {dx, want_dres ? dres : Tensor()};
+}
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -1250,6 +1379,16 @@ PYBIND11_MODULE(_native, m) {
   m.def("cast_f32_bf16", &cast_f32_bf16, "flat fp32 -> bf16");
   m.def("sumsq", &sumsq, "sum of squares of a flat fp32 buffer");
   m.def("softmax_xent", &softmax_xent, "fused softmax cross entropy fwd+bwd");
+  m.def("bn_fwd_fold", &bn_fwd_fold, "BN forward, finalize folded into the apply",
+        py::arg("x"), py::arg("part"), py::arg("have_partials"), py::arg("res") = py::none(),
+        py::arg("gamma") = py::none(), py::arg("beta") = py::none(),
+        py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
+        py::arg("momentum") = 0.1, py::arg("eps") = 1e-5, py::arg("relu") = false,
+        py::arg("want_mask") = false, py::arg("zero_buf") = py::none());
+  m.def("bn_bwd_fold", &bn_bwd_fold, "BN backward, finalize folded into the apply",
+        py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("gamma"), py::arg("stats"),
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"),
+        py::arg("slots"), py::arg("mask") = py::none(), py::arg("zero_buf") = py::none());
   m.def("bn_fwd", &bn_fwd, "NHWC batchnorm(+residual)(+relu) forward", py::arg("x"),
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("training"),

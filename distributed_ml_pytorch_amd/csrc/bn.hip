@@ -12,6 +12,9 @@
 //            dx coefficients) -> apply  dx = A*dz + Cc*x + Bc  [and dres = dz]
 #include "common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace dmp {
 
 __device__ __forceinline__ void load8(const u16* p, float v[8]) {
@@ -396,6 +399,334 @@ void launch_bn_bwd(const u16* x, const u16* dy, const u16* y, const float* gamma
     else DMP_BN_BAPPLY(3, false);
   }
 #undef DMP_BN_BAPPLY
+}
+
+
+// -------- finalize folded into the apply passes --------------------------------
+// The separate 1-block finalize launches (one forward + one backward per BN:
+// 40 per ResNet-18 step, 106 per ResNet-50 step, each a dependent ~5 us dispatch
+// on the critical path) disappear: every apply block reduces the kBnSlots slot
+// sums of ITS channel slice itself (grid.y = C / CS slices of CS channels, so a
+// block reads CS x 128 floats from L2, never all C) and derives the folded
+// coefficients in LDS; all blocks of a slice run the same reduction in the same
+// order, so they agree bit for bit.  Row-block 0 of each slice publishes
+// stats / running stats (forward) or accumulates dgamma / dbeta (backward).
+// The slots can no longer be re-zeroed by their reader (other blocks may still
+// be reading), so each apply zeroes the OTHER direction's slots of the same
+// layer, whose reader finished earlier: the forward apply zeroes the backward
+// slots (read by the previous backward apply), the backward apply zeroes the
+// forward slots (read by this step's forward apply).  The host tracks the
+// leftovers of an unpaired pass (forward without backward) and zeroes them
+// eagerly (ops/functional.py).
+template <int CS>
+__device__ __forceinline__ void slice_slot_sums(const float* __restrict__ part, int C, int cs0,
+                                                float* __restrict__ lS, float* __restrict__ lQ) {
+  constexpr int NG = 256 / CS;          // thread groups splitting the slots
+  constexpr int PER = kBnSlots / NG;    // slots per thread (all loads independent)
+  static_assert(kBnSlots % NG == 0, "slot split");
+  __shared__ float rs[256], rq[256];
+  const int t = threadIdx.x, ch = t % CS, grp = t / CS;
+  const float* ps = part + cs0 + ch;
+  const float* pq = part + (long long)kBnSlots * C + cs0 + ch;
+  float a[PER], b[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    a[i] = ps[(long long)(grp + i * NG) * C];
+    b[i] = pq[(long long)(grp + i * NG) * C];
+  }
+  float sa = 0.f, sb = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { sa += a[i]; sb += b[i]; }
+  rs[t] = sa;
+  rq[t] = sb;
+  __syncthreads();
+  if (t < CS) {
+    float ta = 0.f, tb = 0.f;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) { ta += rs[k * CS + t]; tb += rq[k * CS + t]; }
+    lS[t] = ta;
+    lQ[t] = tb;
+  }
+}
+
+// zero the [2][kBnSlots] rows of this block's channel slice in `zb` (rows spread
+// over the slice's row blocks)
+template <int CS>
+__device__ __forceinline__ void slice_zero(float* __restrict__ zb, int C, int cs0) {
+  if (zb == nullptr || threadIdx.x >= CS) return;
+  for (int r = blockIdx.x; r < 2 * kBnSlots; r += gridDim.x)
+    zb[(long long)r * C + cs0 + threadIdx.x] = 0.f;
+}
+
+template <int CS, bool RELU, bool RES, bool MASK>
+__global__ void __launch_bounds__(256) bn_apply_fold_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ res, const float* __restrict__ part,
+    float* __restrict__ zero_buf, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
+    float* __restrict__ stats, u16* __restrict__ y, uint8_t* __restrict__ mask, long long M,
+    int C) {
+  __shared__ float lS[CS], lQ[CS];
+  const int t = threadIdx.x;
+  const int cs0 = blockIdx.y * CS;
+  slice_slot_sums<CS>(part, C, cs0, lS, lQ);
+  if (t < CS) {   // same thread wrote lS[t] / lQ[t]: no barrier needed before the reuse
+    const int c = cs0 + t;
+    const float mean = lS[t] / (float)M;
+    const float var = fmaxf(lQ[t] / (float)M - mean * mean, 0.f);
+    const float inv = rsqrtf(var + eps);
+    const float sc = (gamma ? gamma[c] : 1.f) * inv;
+    const float sh = (beta ? beta[c] : 0.f) - mean * sc;
+    if (blockIdx.x == 0) {
+      stats[c] = mean;
+      stats[C + c] = inv;
+      stats[2 * C + c] = sc;
+      stats[3 * C + c] = sh;
+      if (running_mean) {
+        const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+      }
+    }
+    lS[t] = sc;
+    lQ[t] = sh;
+  }
+  slice_zero<CS>(zero_buf, C, cs0);
+  __syncthreads();
+  constexpr int TPR = CS / 8, RPI = 256 / TPR;
+  const int cg = t % TPR, r0 = t / TPR;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sc[k] = lS[cg * 8 + k]; sh[k] = lQ[cg * 8 + k]; }
+  const long long rows_per_blk = (M + gridDim.x - 1) / gridDim.x;
+  const long long start = (long long)blockIdx.x * rows_per_blk;
+  const long long end = min(M, start + rows_per_blk);
+  auto one = [&](const bf16x8& xr, const bf16x8& rr, long long off) {
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o[k] = bn_pre(bf2f(xr.v[k]), sc[k], sh[k]);
+      if (RES) o[k] += bf2f(rr.v[k]);
+      if (RELU) o[k] = fmaxf(o[k], 0.f);
+    }
+    if (MASK) {
+      bf16x8 r;
+      unsigned bits = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        r.v[k] = f2bf(o[k]);
+        bits |= (r.v[k] != 0 ? 1u : 0u) << k;
+      }
+      *reinterpret_cast<bf16x8*>(y + off) = r;
+      mask[off >> 3] = (uint8_t)bits;
+    } else {
+      store8(y + off, o);
+    }
+  };
+  constexpr int U = 4;
+  long long row = start + r0;
+  const int cofs = cs0 + cg * 8;
+  for (; row + (U - 1) * RPI < end; row += U * RPI) {
+    bf16x8 xr[U], rr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long off = (row + u * RPI) * C + cofs;
+      xr[u] = *reinterpret_cast<const bf16x8*>(x + off);
+      if (RES) rr[u] = *reinterpret_cast<const bf16x8*>(res + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(xr[u], rr[u], (row + u * RPI) * C + cofs);
+  }
+  for (; row < end; row += RPI) {
+    const long long off = row * C + cofs;
+    bf16x8 xr = *reinterpret_cast<const bf16x8*>(x + off), rr;
+    if (RES) rr = *reinterpret_cast<const bf16x8*>(res + off);
+    one(xr, rr, off);
+  }
+}
+
+template <int CS, int RELU, bool WRITE_DRES>
+__global__ void __launch_bounds__(256) bn_bwd_apply_fold_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
+    const uint8_t* __restrict__ mask, const float* __restrict__ part,
+    float* __restrict__ zero_buf, const float* __restrict__ gamma,
+    const float* __restrict__ stats, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    u16* __restrict__ dx, u16* __restrict__ dres, long long M, int C) {
+  __shared__ float lS[CS], lQ[CS], lC[CS];
+  const int t = threadIdx.x;
+  const int cs0 = blockIdx.y * CS;
+  slice_slot_sums<CS>(part, C, cs0, lS, lQ);
+  if (t < CS) {
+    const int c = cs0 + t;
+    const float db = lS[t];   // sum dz
+    const float dg = lQ[t];   // sum dz * xhat
+    if (blockIdx.x == 0) {
+      if (dgamma) dgamma[c] += dg;
+      if (dbeta) dbeta[c] += db;
+    }
+    const float mean = stats[c], inv = stats[C + c];
+    const float k1 = (gamma ? gamma[c] : 1.f) * inv;
+    const float invM = 1.f / (float)M;
+    const float Cc = -k1 * inv * dg * invM;
+    lS[t] = k1;
+    lQ[t] = -k1 * db * invM - Cc * mean;
+    lC[t] = Cc;
+  }
+  slice_zero<CS>(zero_buf, C, cs0);
+  __syncthreads();
+  constexpr int TPR = CS / 8, RPI = 256 / TPR;
+  const int cg = t % TPR, r0 = t / TPR;
+  const int cofs = cs0 + cg * 8;
+  float ka[8], kb[8], kc[8], msc[8], msh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    ka[k] = lS[cg * 8 + k];
+    kb[k] = lQ[cg * 8 + k];
+    kc[k] = lC[cg * 8 + k];
+    if (RELU == 2) { msc[k] = stats[2 * C + cofs + k]; msh[k] = stats[3 * C + cofs + k]; }
+  }
+  const long long rows_per_blk = (M + gridDim.x - 1) / gridDim.x;
+  const long long start = (long long)blockIdx.x * rows_per_blk;
+  const long long end = min(M, start + rows_per_blk);
+  auto one = [&](const bf16x8& xr, const bf16x8& dr, const bf16x8& yr, unsigned mb,
+                 long long off) {
+    float xv[8], g[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      xv[k] = bf2f(xr.v[k]);
+      g[k] = bf2f(dr.v[k]);
+      if (RELU == 1) g[k] = bf2f(yr.v[k]) > 0.f ? g[k] : 0.f;
+      if (RELU == 2) {
+        const float yy = fmaxf(bn_pre(xv[k], msc[k], msh[k]), 0.f);
+        g[k] = bf2f(f2bf(yy)) > 0.f ? g[k] : 0.f;
+      }
+    }
+    if (RELU == 3) relu_mask_bits(mb, g);
+    if (WRITE_DRES) store8(dres + off, g);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = ka[k] * g[k] + kc[k] * xv[k] + kb[k];
+    store8(dx + off, o);
+  };
+  constexpr int U = 4;
+  long long row = start + r0;
+  for (; row + (U - 1) * RPI < end; row += U * RPI) {
+    bf16x8 xr[U], dr[U], yr[U];
+    unsigned mb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long off = (row + u * RPI) * C + cofs;
+      xr[u] = *reinterpret_cast<const bf16x8*>(x + off);
+      dr[u] = *reinterpret_cast<const bf16x8*>(dy + off);
+      if (RELU == 1) yr[u] = *reinterpret_cast<const bf16x8*>(y + off);
+      if (RELU == 3) mb[u] = mask[off >> 3];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(xr[u], dr[u], yr[u], mb[u], (row + u * RPI) * C + cofs);
+  }
+  for (; row < end; row += RPI) {
+    const long long off = row * C + cofs;
+    bf16x8 xr = *reinterpret_cast<const bf16x8*>(x + off);
+    bf16x8 dr = *reinterpret_cast<const bf16x8*>(dy + off), yr;
+    unsigned mb = 0;
+    if (RELU == 1) yr = *reinterpret_cast<const bf16x8*>(y + off);
+    if (RELU == 3) mb = mask[off >> 3];
+    one(xr, dr, yr, mb, off);
+  }
+}
+
+static int fold_cs(int C) { return C % 64 == 0 ? 64 : C % 32 == 0 ? 32 : C % 16 == 0 ? 16 : 8; }
+
+// row blocks per slice: >= 4 vectors per thread (DMP_BN_FOLD_VPT), at most 2048
+// blocks in all.  The per-block slot reduction is CS x 128 floats from L2; the
+// streaming pass needs the blocks: ResNet-18 bs512 3.77 ms/step unfolded, 4.15
+// at 32 vectors per thread, 3.66 at 8, 3.65 at 4 (profiles/bn_fold_stem3_r2.txt)
+static dim3 fold_grid(long long M, int C, int cs) {
+  static const long long vpt = [] {
+    const char* e = std::getenv("DMP_BN_FOLD_VPT");
+    return e ? std::max(1, std::atoi(e)) : 4;
+  }();
+  const long long nsl = C / cs;
+  long long nrb = (M * (cs / 8) + 256 * vpt - 1) / (256 * vpt);
+  const long long cap = std::max<long long>(1, 2048 / nsl);
+  nrb = std::max<long long>(1, std::min(nrb, std::min(cap, M)));
+  return dim3((unsigned)nrb, (unsigned)nsl);
+}
+
+void launch_bn_fwd_fold(const u16* x, const u16* res, u16* y, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var, float* stats,
+                        float* part, float* zero_buf, long long M, int C, float momentum,
+                        float eps, bool relu, bool have_partials, hipStream_t s, uint8_t* mask) {
+  if (!have_partials) {
+    const int G = bn_num_partials(M, C);
+    const int rpi = 256 / (C / 8);
+    const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
+    hipLaunchKernelGGL((bn_partial_kernel<0, 0>), dim3(G), dim3(256), lds, s, x, nullptr,
+                       nullptr, nullptr, nullptr, part, M, C);
+  }
+  const int cs = fold_cs(C);
+  const dim3 grid = fold_grid(M, C, cs);
+#define DMP_FOLD_F(CS, R, S, K)                                                              \
+  hipLaunchKernelGGL((bn_apply_fold_kernel<CS, R, S, K>), grid, dim3(256), 0, s, x, res, part, \
+                     zero_buf, gamma, beta, running_mean, running_var, momentum, eps, stats, y, \
+                     mask, M, C)
+#define DMP_FOLD_FV(CS)                                       \
+  if (relu && mask) {                                          \
+    if (res) DMP_FOLD_F(CS, true, true, true);                 \
+    else DMP_FOLD_F(CS, true, false, true);                    \
+  } else if (relu) {                                           \
+    if (res) DMP_FOLD_F(CS, true, true, false);                \
+    else DMP_FOLD_F(CS, true, false, false);                   \
+  } else {                                                     \
+    if (res) DMP_FOLD_F(CS, false, true, false);               \
+    else DMP_FOLD_F(CS, false, false, false);                  \
+  }
+  if (cs == 64) { DMP_FOLD_FV(64) }
+  else if (cs == 32) { DMP_FOLD_FV(32) }
+  else if (cs == 16) { DMP_FOLD_FV(16) }
+  else { DMP_FOLD_FV(8) }
+#undef DMP_FOLD_FV
+#undef DMP_FOLD_F
+}
+
+void launch_bn_bwd_fold(const u16* x, const u16* dy, const u16* y, const float* gamma,
+                        const float* stats, float* dgamma, float* dbeta, float* part,
+                        float* zero_buf, u16* dx, u16* dres, long long M, int C, bool relu,
+                        hipStream_t s, const uint8_t* mask) {
+  const int G = bn_num_partials(M, C);
+  const int rpi = 256 / (C / 8);
+  const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
+  const int mode = !relu ? 0 : (mask ? 3 : (y ? 1 : 2));
+#define DMP_BN_PART(R)                                                                          \
+  hipLaunchKernelGGL((bn_partial_kernel<1, R>), dim3(G), dim3(256), lds, s, x, dy, y, mask, stats, \
+                     part, M, C)
+  if (mode == 0) DMP_BN_PART(0);
+  else if (mode == 1) DMP_BN_PART(1);
+  else if (mode == 2) DMP_BN_PART(2);
+  else DMP_BN_PART(3);
+#undef DMP_BN_PART
+  const int cs = fold_cs(C);
+  const dim3 grid = fold_grid(M, C, cs);
+#define DMP_FOLD_B(CS, R, D)                                                                   \
+  hipLaunchKernelGGL((bn_bwd_apply_fold_kernel<CS, R, D>), grid, dim3(256), 0, s, x, dy, y, mask, \
+                     part, zero_buf, gamma, stats, dgamma, dbeta, dx, dres, M, C)
+#define DMP_FOLD_BV(CS)                                                    \
+  if (dres) {                                                              \
+    if (mode == 0) DMP_FOLD_B(CS, 0, true);                                \
+    else if (mode == 1) DMP_FOLD_B(CS, 1, true);                           \
+    else if (mode == 2) DMP_FOLD_B(CS, 2, true);                           \
+    else DMP_FOLD_B(CS, 3, true);                                          \
+  } else {                                                                 \
+    if (mode == 0) DMP_FOLD_B(CS, 0, false);                               \
+    else if (mode == 1) DMP_FOLD_B(CS, 1, false);                          \
+    else if (mode == 2) DMP_FOLD_B(CS, 2, false);                          \
+    else DMP_FOLD_B(CS, 3, false);                                         \
+  }
+  if (cs == 64) { DMP_FOLD_BV(64) }
+  else if (cs == 32) { DMP_FOLD_BV(32) }
+  else if (cs == 16) { DMP_FOLD_BV(16) }
+  else { DMP_FOLD_BV(8) }
+#undef DMP_FOLD_BV
+#undef DMP_FOLD_B
 }
 
 }  // namespace dmp

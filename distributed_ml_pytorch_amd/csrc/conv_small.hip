@@ -407,4 +407,286 @@ void launch_conv_small_wgrad(const u16* dy, const u16* x, int xbytes, int sb, in
                      G);
 }
 
+
+// ------------------------------------------------------------------------------
+// CIFAR-style stem on the matrix cores: 3x3, stride 1, pad 1, CI <= 3 (K = 9*CI
+// <= 27 padded to one 32-deep MFMA k-step), CO = 64.  The VALU kernels above spend
+// ~60 us per ResNet-18 bs512 step in each direction on 1.8 GFLOP; here both
+// passes are a handful of v_mfma_f32_16x16x32_bf16 per 16 / 32 pixels and run at
+// the output / dY streaming rate.
+//
+// forward: D[co][px] = W[co][k] X[k][px].  The four 16-row weight fragments (all
+//   64 output channels) live in registers for the whole block; a lane gathers its
+//   B fragment (8 taps k = 8*(lane>>4)+i of pixel lane & 15) straight from the
+//   L2-resident input through the buffer unit (padding taps read 0 via an
+//   out-of-range offset).  The D layout gives a lane 4 consecutive channels of one
+//   pixel: 8-B stores, and the BN partial sums of the stored (bf16-rounded)
+//   values accumulate in registers, reduced once per block over the 16 pixel
+//   lanes (xor shuffles) and the 4 waves (LDS) into slot blockIdx % kBnSlots.
+// wgrad: D[co][k] = dY^T[co][px] X[px][k] over 32-pixel k-steps.  dY[32 px][64]
+//   is staged row-major into a [32][128] LDS image (chunk-swizzled like the GEMM's
+//   transposed operands, gemm.hip toff) and read with ds_read_b64_tr_b16, which
+//   hands a lane 8 consecutive pixels of one channel; X fragments (8 consecutive
+//   pixels of one tap: one image row when W % 8 == 0) are gathered from L2.  Each
+//   wave owns a 32-pixel slice of a 128-pixel step, 8 MFMAs; the 4 waves' 64 x 32
+//   tiles are summed in LDS and flushed with one fp32 atomic per weight per block.
+typedef __bf16 bf16x8_t_ __attribute__((ext_vector_type(8)));
+typedef short s16x4_t_ __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 s3_mfma(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t_, a),
+                                                 __builtin_bit_cast(bf16x8_t_, b), c, 0, 0, 0);
+}
+
+struct Stem3Args {
+  const u16* x;
+  const u16* w;     // [64][3][3][CI] bf16
+  const u16* dy;    // [P][64]
+  u16* y;           // [P][64]
+  float* part;      // [2][kBnSlots][64]
+  float* dw;        // [64][K] fp32 (+=)
+  int sb, sh, sw, sc, xbytes;
+  int H, W, CI, K;
+  long long P;
+  int groups;       // forward: 16-pixel groups per wave; wgrad: 128-pixel steps per block
+};
+
+// per-lane tap table for k = 8*(lane>>4) + i: (dr, ds) in [-1, 1], ci; invalid k -> r = 9
+__device__ __forceinline__ void s3_taps(int CI, int K, int kg, int dr[8], int ds[8], int ci[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int k = kg * 8 + i;
+    const int c = k % CI, rs = k / CI;
+    dr[i] = k < K ? rs / 3 - 1 : 9;
+    ds[i] = rs % 3 - 1;
+    ci[i] = c;
+  }
+}
+
+__global__ void __launch_bounds__(256) stem3_fwd_kernel(Stem3Args a) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, a.xbytes, 0x00020000);
+  // weight fragments: row co = 16j + col, k = 8kg..8kg+7
+  bf16x8 wf[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = kg * 8 + i;
+      wf[j].v[i] = k < a.K ? a.w[(16 * j + col) * a.K + k] : (u16)0;
+    }
+  int dr[8], ds[8], ci[8];
+  s3_taps(a.CI, a.K, kg, dr, ds, ci);
+  float s[4][4], q[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s[j][r] = 0.f; q[j][r] = 0.f; }
+  const long long base = ((long long)blockIdx.x * 4 + wid) * a.groups * 16;
+  for (int gi = 0; gi < a.groups; ++gi) {
+    const long long px = base + gi * 16 + col;
+    const bool pv = px < a.P;
+    const int p32 = pv ? (int)px : 0;
+    const int ow = p32 % a.W, t = p32 / a.W;
+    const int oh = t % a.H, b = t / a.H;
+    const int boff = b * a.sb;
+    bf16x8 xf;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ih = oh + dr[i], iw = ow + ds[i];
+      const bool ok = pv && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const int off = ok ? 2 * (boff + ih * a.sh + iw * a.sw + ci[i] * a.sc) : 0x7ffffff0;
+      xf.v[i] = __builtin_bit_cast(u16, __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = s3_mfma(wf[j], xf, f32x4{0.f, 0.f, 0.f, 0.f});
+    // D: lane holds channels 16j + 4kg + r of pixel `col`... of THIS group's pixel px
+    // (D row = co, D col = pixel: lane = (row block kg, col))
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        o.v[r] = f2bf(acc[j][r]);
+        const float v = pv ? bf2f(o.v[r]) : 0.f;
+        s[j][r] += v;
+        q[j][r] += v * v;
+      }
+      if (pv) *reinterpret_cast<bf16x4*>(a.y + px * 64 + 16 * j + 4 * kg) = o;
+    }
+  }
+  if (a.part == nullptr) return;
+  // reduce over the 16 pixel lanes sharing kg
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s[j][r] += __shfl_xor(s[j][r], o, 64);
+        q[j][r] += __shfl_xor(q[j][r], o, 64);
+      }
+  __shared__ float red[4][2][64];
+  if (col == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[wid][0][16 * j + 4 * kg + r] = s[j][r];
+        red[wid][1][16 * j + 4 * kg + r] = q[j][r];
+      }
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int c = threadIdx.x & 63, h = threadIdx.x >> 6;
+    const float v = red[0][h][c] + red[1][h][c] + red[2][h][c] + red[3][h][c];
+    const int slot = blockIdx.x % kBnSlots;
+    atomicAdd(a.part + (long long)(h * kBnSlots + slot) * 64 + c, v);
+  }
+}
+
+// [32][128] bf16 transposed-read image: 32-B granule u of row r holds logical
+// granule u ^ tf(r) (gemm.hip toff<128>)
+__device__ __forceinline__ int s3_tf(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
+__device__ __forceinline__ int s3_toff(int row, int col) {
+  return row * 128 + (((col >> 4) ^ s3_tf(row)) << 4) + (col & 15);
+}
+
+__global__ void __launch_bounds__(256) stem3_wgrad_kernel(Stem3Args a) {
+  __shared__ __attribute__((aligned(16))) u16 img[4][32 * 128];
+  __shared__ float tile[64][33];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, a.xbytes, 0x00020000);
+  // this lane's two B columns: taps 16t + col, t = 0, 1
+  int tdr[2], tds[2], tci[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = 16 * t + col;
+    tdr[t] = k < a.K ? (k / a.CI) / 3 - 1 : 9;
+    tds[t] = (k / a.CI) % 3 - 1;
+    tci[t] = k % a.CI;
+  }
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { acc[j][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[j][1] = acc[j][0]; }
+  u16* im = img[wid];
+  const long long blk0 = (long long)blockIdx.x * a.groups * 128;
+  for (int st = 0; st < a.groups; ++st) {
+    const long long p0 = blk0 + (long long)st * 128 + wid * 32;   // this wave's 32 pixels
+    // stage dY[p0 .. p0+32)[0..64) : 256 real 16-B chunks per wave image, 4 per lane
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = u * 64 + lane;              // logical chunk: row e >> 3, cols (e & 7) * 8
+      const int row = e >> 3, c0 = (e & 7) * 8;
+      const long long p = p0 + row;
+      bf16x8 v;
+      if (p < a.P) v = *reinterpret_cast<const bf16x8*>(a.dy + p * 64 + c0);
+      else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v.v[i] = 0;
+      }
+      *reinterpret_cast<bf16x8*>(im + s3_toff(row, c0)) = v;   // 8 cols stay in one granule
+    }
+    // X fragments: pixels p0 + 8kg + i (one image row when W % 8 == 0), taps 16t + col
+    bf16x8 xf[2];
+    {
+      const long long pb = p0 + 8 * kg;
+      const bool pv = pb < a.P;
+      const int p32 = pv ? (int)pb : 0;
+      const int ow0 = p32 % a.W, t0 = p32 / a.W;
+      const int oh = t0 % a.H, b = t0 / a.H;
+      const int boff = b * a.sb;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ih = oh + tdr[t];
+        const bool rok = pv && (unsigned)ih < (unsigned)a.H;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int iw = ow0 + i + tds[t];
+          const bool ok = rok && (unsigned)iw < (unsigned)a.W && pb + i < a.P;
+          const int off = ok ? 2 * (boff + ih * a.sh + iw * a.sw + tci[t] * a.sc) : 0x7ffffff0;
+          xf[t].v[i] = __builtin_bit_cast(u16, __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS image writes landed
+    __builtin_amdgcn_wave_barrier();
+    // A fragments (co tile j): lane row co = 16j + col... read transposed: 8 consecutive
+    // pixels (k) 8kg..8kg+7 of channel column
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+      const int row = 8 * g + qq;
+      const s16x4_t_ lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4_t_*)(im + s3_toff(row, 16 * j + 4 * pp)));
+      const s16x4_t_ hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4_t_*)(im + s3_toff(row + 4, 16 * j + 4 * pp)));
+      const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      acc[j][0] = s3_mfma(af, xf[0], acc[j][0]);
+      acc[j][1] = s3_mfma(af, xf[1], acc[j][1]);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // sum the 4 waves' [64 co][32 k] tiles, one atomic per weight per block
+  // D: lane holds rows co = 16j + 4kg + r, column k = 16t + col
+  for (int w = 0; w < 4; ++w) {
+    if (wid == w) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float& d = tile[16 * j + 4 * kg + r][16 * t + col];
+            d = (w == 0 ? 0.f : d) + acc[j][t][r];
+          }
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < 64 * a.K; e += 256) {
+    const int co = e / a.K, k = e % a.K;
+    atomicAdd(a.dw + e, tile[co][k]);
+  }
+}
+
+bool stem3_supported(int CI, int R, int S, int CO, int stride, int pad, int W) {
+  return CI >= 1 && CI <= 3 && R == 3 && S == 3 && CO == 64 && stride == 1 && pad == 1 &&
+         W % 8 == 0;
+}
+
+void launch_stem3_fwd(const u16* x, int xbytes, int sb, int sh, int sw, int sc, const u16* w,
+                      u16* y, float* part, int B, int H, int W, int CI, hipStream_t s) {
+  Stem3Args a{};
+  a.x = x; a.w = w; a.y = y; a.part = part;
+  a.sb = sb; a.sh = sh; a.sw = sw; a.sc = sc; a.xbytes = xbytes;
+  a.H = H; a.W = W; a.CI = CI; a.K = 9 * CI;
+  a.P = (long long)B * H * W;
+  // 16 groups of 16 pixels per wave (1024 pixels per block) unless that leaves
+  // fewer than ~2 blocks per CU
+  int groups = 16;
+  while (groups > 1 && (a.P + 64LL * groups - 1) / (64LL * groups) < 512) groups >>= 1;
+  a.groups = groups;
+  const long long nb = (a.P + 64LL * groups - 1) / (64LL * groups);
+  hipLaunchKernelGGL(stem3_fwd_kernel, dim3((unsigned)nb), dim3(256), 0, s, a);
+}
+
+void launch_stem3_wgrad(const u16* dy, const u16* x, int xbytes, int sb, int sh, int sw, int sc,
+                        float* dw, int B, int H, int W, int CI, hipStream_t s) {
+  Stem3Args a{};
+  a.x = x; a.dy = dy; a.dw = dw;
+  a.sb = sb; a.sh = sh; a.sw = sw; a.sc = sc; a.xbytes = xbytes;
+  a.H = H; a.W = W; a.CI = CI; a.K = 9 * CI;
+  a.P = (long long)B * H * W;
+  // ~512 blocks: 128-pixel steps per block
+  const long long steps = (a.P + 127) / 128;
+  long long per = (steps + 511) / 512;
+  if (per < 1) per = 1;
+  a.groups = (int)per;
+  const long long nb = (steps + per - 1) / per;
+  hipLaunchKernelGGL(stem3_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a);
+}
+
 }  // namespace dmp

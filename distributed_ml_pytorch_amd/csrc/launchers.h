@@ -42,6 +42,15 @@ void launch_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const fl
 void launch_bn_bwd_from_partials(const uint16_t* x, const uint16_t* dz, const float* gamma,
                                  const float* stats, float* dgamma, float* dbeta, float* coef,
                                  float* part, uint16_t* dx, long long M, int C, hipStream_t s);
+// finalize folded into the apply passes (zero_buf: the other direction's slots)
+void launch_bn_fwd_fold(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var, float* stats,
+                        float* part, float* zero_buf, long long M, int C, float momentum,
+                        float eps, bool relu, bool have_partials, hipStream_t s, uint8_t* mask);
+void launch_bn_bwd_fold(const uint16_t* x, const uint16_t* dy, const uint16_t* y,
+                        const float* gamma, const float* stats, float* dgamma, float* dbeta,
+                        float* part, float* zero_buf, uint16_t* dx, uint16_t* dres, long long M,
+                        int C, bool relu, hipStream_t s, const uint8_t* mask);
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const float* gamma,
                    const float* stats, float* dgamma, float* dbeta, float* coef, float* part,
                    uint16_t* dx, uint16_t* dres, long long M, int C, bool relu, hipStream_t s,
@@ -131,6 +140,13 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int B, 
                        int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s, float* dbias = nullptr, float* slab = nullptr);
 
+// conv_small.hip: 3x3/s1/p1 stems with CI <= 3 and CO = 64 on MFMA
+bool stem3_supported(int CI, int R, int S, int CO, int stride, int pad, int W);
+void launch_stem3_fwd(const uint16_t* x, int xbytes, int sb, int sh, int sw, int sc,
+                      const uint16_t* w, uint16_t* y, float* part, int B, int H, int W, int CI,
+                      hipStream_t s);
+void launch_stem3_wgrad(const uint16_t* dy, const uint16_t* x, int xbytes, int sb, int sh, int sw,
+                        int sc, float* dw, int B, int H, int W, int CI, hipStream_t s);
 // conv_small.hip: few-input-channel (stem) convolutions, VALU
 int conv_small_max_k();
 long long conv_small_fwd_blocks(long long P);

@@ -554,13 +554,21 @@ BN_SLOTS = 64   # csrc/bn_slots.h kBnSlots
 BN_TAIL = 4     # csrc/bn_slots.h kBnTail (arrival ticket)
 
 
-def bn_slot_buffer(owner, attr: str, channels: int, device):
-    """Persistent zeroed ``[2][BN_SLOTS][channels] + BN_TAIL`` fp32 slot buffer on ``owner``."""
+def bn_slot_buffer(owner, attr: str, channels: int, device, fresh: bool = True):
+    """Persistent zeroed ``[2][BN_SLOTS][channels] + BN_TAIL`` fp32 slot buffer on ``owner``.
+
+    ``fresh``: the caller is about to accumulate into it, so sums a folded BN
+    forward left behind without a matching backward (``mark_slots``, see
+    ``ops.functional._BNAct``) are zeroed first."""
     n = 2 * BN_SLOTS * channels + BN_TAIL
     buf = getattr(owner, attr, None)
     if buf is None or buf.device != device or buf.numel() != n:
         buf = torch.zeros(n, dtype=torch.float32, device=device)
         object.__setattr__(owner, attr, buf)
+    elif fresh:
+        from .functional import clean_slots
+
+        clean_slots(buf)
     return buf
 
 

@@ -121,6 +121,38 @@ def softmax_cross_entropy(logits, labels, label_smoothing: float = 0.0, ignore_i
 _BN_BWD_FUSE = os.environ.get("DMP_BN_BWD_FUSE", "0")
 BN_BWD_FUSE_STATS = {"fused": 0, "fallback": 0}
 _BN_BITMASK = os.environ.get("DMP_BN_BITMASK", "1") != "0"   # backward passes by path (diagnostics)
+# BatchNorm finalize folded into the apply passes (csrc/bn.hip fold kernels): no
+# separate finalize launch per BN and direction.  Slot hygiene: the forward apply
+# zeroes the layer's backward slots and the backward apply the forward slot sums
+# it read, so a buffer left holding sums (an unpaired pass) is flagged
+# dirty (``mark_slots``) and zeroed by the next producer (``ops.conv.bn_slot_buffer``) or
+# backward before it accumulates again.
+_BN_FOLD = os.environ.get("DMP_BN_FOLD", "1") != "0"
+# data_ptrs of slot buffers holding sums nobody will zero (keyed by storage, not
+# by Python object: a buffer comes back from an autograd Function as a new
+# wrapper of the same storage)
+_SLOTS_DIRTY: set = set()
+
+
+def mark_slots(buf, dirty: bool):
+    if dirty:
+        _SLOTS_DIRTY.add(buf.data_ptr())
+    else:
+        _SLOTS_DIRTY.discard(buf.data_ptr())
+
+
+def clean_slots(buf):
+    """Zero ``buf`` if it holds leftover sums (see ``_BN_FOLD``)."""
+    if buf.data_ptr() in _SLOTS_DIRTY:
+        buf.zero_()
+        _SLOTS_DIRTY.discard(buf.data_ptr())
+    return buf
+
+
+def _fresh_slots(buf, C, device):
+    if buf is None:
+        return torch.zeros(2 * 64 * C + 4, dtype=torch.float32, device=device)
+    return clean_slots(buf)
 
 
 class BNLink:
@@ -161,13 +193,32 @@ class _BNAct(Function):
         # BN + residual + ReLU: the backward's ReLU mask depends on the residual;
         # keep it as 1 bit per element (written by the apply) instead of y
         want_mask = bool(relu and residual is not None and _BN_BITMASK)
-        if part is not None and training:
+        ctx.fold = bool(_BN_FOLD and training and x.is_cuda and _BN_BWD_FUSE in ("0", False))
+        ctx.fpart = None
+        if ctx.fold:
+            C = x.shape[1]
+            bslots = slots[1] if slots is not None else None
+            src = part if part is not None else _fresh_slots(
+                slots[0] if slots is not None else None, C, x.device)
+            y, stats, mask = native().bn_fwd_fold(
+                x, src, part is not None, residual, gamma, beta, running_mean, running_var,
+                float(momentum), float(eps), bool(relu), want_mask, bslots)
+            mark_slots(src, True)          # read here, zeroed by the backward apply
+            if bslots is not None:
+                mark_slots(bslots, False)  # zeroed by this apply
+            ctx.fpart = src
+        elif part is not None and training:
+            if slots is not None:          # sums a folded pass left behind (mode switch)
+                clean_slots(slots[1])
             # statistics already reduced per block by the producing conv's epilogue
             C = x.shape[1]
             y, stats, mask = native().bn_fwd_from_partials(
                 x, part, (part.numel() - 4) // (2 * C), residual, gamma, beta, running_mean,
                 running_var, float(momentum), float(eps), bool(relu), want_mask)
         else:
+            if slots is not None and training:
+                clean_slots(slots[0])
+                clean_slots(slots[1])
             y, stats, mask = native().bn_fwd(x, residual, gamma, beta, running_mean, running_var,
                                              float(momentum), float(eps), bool(training),
                                              bool(relu), slots[0] if slots is not None else None,
@@ -210,7 +261,18 @@ class _BNAct(Function):
             BN_BWD_FUSE_STATS["fused" if fused else "fallback"] += 1
             if not fused:
                 link.part.zero_()        # partial sums of an incomplete gradient
-        if fused:
+        if ctx.fold:
+            if x.dim() == 4:
+                dy = dy.contiguous(memory_format=CL)
+            else:
+                dy = dy.contiguous()
+            bs = _fresh_slots(ctx.bslots, x.shape[1], x.device)
+            dx, dres = native().bn_bwd_fold(x, dy, y, gamma, stats, dg, db, ctx.relu, ctx.has_res,
+                                            bs, mask, ctx.fpart)
+            mark_slots(bs, True)
+            mark_slots(ctx.fpart, False)
+            ctx.fpart = None
+        elif fused:
             # the consuming conv's dgrad already masked dz and reduced it
             dx = native().bn_bwd_from_partials(x, dy, gamma, stats, dg, db, link.part)
             dres = dy if ctx.has_res else None

@@ -63,7 +63,7 @@ def _bn_slots(mod, x):
     if not x.is_cuda:
         return None
     return (bn_slot_buffer(mod, "_dmp_fslots", mod.num_features, x.device),
-            bn_slot_buffer(mod, "_dmp_bslots", mod.num_features, x.device))
+            bn_slot_buffer(mod, "_dmp_bslots", mod.num_features, x.device, fresh=False))
 
 
 class BatchNorm2d(nn.BatchNorm2d):

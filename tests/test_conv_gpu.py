@@ -183,6 +183,8 @@ SMALL_SHAPES = [
     (2, 3, 67, 67, 64, 11, 4, 2),
     (3, 1, 28, 28, 128, 5, 1, 2),
     (5, 3, 9, 11, 64, 3, 1, 1),        # pixel count not a multiple of 256
+    (3, 3, 8, 16, 64, 3, 1, 1),        # MFMA stem (stem3_*): 384 pixels, partial blocks
+    (2, 1, 16, 8, 64, 3, 1, 1),        # MFMA stem with CI = 1 (K = 9)
 ]
 
 

@@ -159,6 +159,72 @@ def test_bn_act_fwd_bwd(shape, relu, res):
         torch.testing.assert_close(rb.grad.float(), rr.grad, rtol=2e-2, atol=2e-2)
 
 
+def _bn_ref(xb, mod, rb=None, relu=True):
+    xr = xb.detach().float().requires_grad_(True)
+    g2 = mod.weight.detach().clone().requires_grad_(True)
+    b2 = mod.bias.detach().clone().requires_grad_(True)
+    yr = F.batch_norm(xr, None, None, g2, b2, True, 0.1, mod.eps)
+    if rb is not None:
+        yr = yr + rb.detach().float()
+    return (F.relu(yr) if relu else yr), xr, g2, b2
+
+
+@pytest.mark.parametrize("C,res", [(64, False), (128, True), (24, False), (80, True), (96, False)])
+def test_bn_fold_persistent_slots_multi_step(C, res):
+    """Finalize folded into the apply passes with the layer's persistent slot
+    buffers: the forward apply zeroes the backward slots and vice versa, so
+    several steps in a row -- with a forward-only (no backward) pass in between --
+    must each match an fp32 reference (stale sums would shift the statistics)."""
+    from distributed_ml_pytorch_amd.ops import functional as DF
+    from distributed_ml_pytorch_amd.ops import layers as L
+
+    assert DF._BN_FOLD, "fold path is the default"
+    torch.manual_seed(C)
+    bn = L.BatchNorm2d(C, relu=True).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_()
+    for it in range(4):
+        x = _bf(torch.randn(6, C, 9, 7, device="cuda") * (1 + it) + it).contiguous(
+            memory_format=CL).requires_grad_(True)
+        rb = _bf(torch.randn(6, C, 9, 7, device="cuda")).contiguous(memory_format=CL) if res else None
+        bn.weight.grad = None
+        bn.bias.grad = None
+        y = bn(x, residual=rb)
+        yr, xr, g2, b2 = _bn_ref(x, bn, rb)
+        torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+        if it == 1:
+            continue            # forward only: its slot sums stay behind (dirty)
+        dy = torch.randn_like(yr)
+        (y.float() * dy).sum().backward()
+        (yr * dy).sum().backward()
+        torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=3e-2)
+        torch.testing.assert_close(bn.weight.grad, g2.grad, rtol=2e-2, atol=2e-1)
+        torch.testing.assert_close(bn.bias.grad, b2.grad, rtol=2e-2, atol=2e-1)
+
+
+def test_bn_fold_with_conv_producer_multi_step():
+    """Conv epilogue BN partials -> folded BN apply, three steps with a
+    forward-only pass in between (the conv's slot buffer is re-zeroed)."""
+    from distributed_ml_pytorch_amd.ops import layers as L
+
+    torch.manual_seed(3)
+    conv = L.Conv2d(64, 64, 3, padding=1, bias=False).cuda()
+    conv.emit_bn_stats = True
+    bn = L.BatchNorm2d(64, relu=True).cuda()
+    w16 = conv.weight.detach().to(torch.bfloat16).float()
+    for it in range(4):
+        x = _bf(torch.randn(8, 64, 12, 12, device="cuda")).contiguous(memory_format=CL)
+        h = conv(x)
+        assert getattr(h, "_dmp_bn_part", None) is not None, "conv did not emit BN partials"
+        y = bn(h)
+        hr = F.conv2d(x.float(), w16, padding=1)
+        yr = F.relu(F.batch_norm(hr, None, None, bn.weight.detach(), bn.bias.detach(), True))
+        torch.testing.assert_close(y.float(), yr, rtol=3e-2, atol=3e-2)
+        if it != 1:
+            y.float().sum().backward()
+
+
 def test_bn_eval_uses_running_stats():
     from distributed_ml_pytorch_amd.ops.functional import batch_norm_act
 
