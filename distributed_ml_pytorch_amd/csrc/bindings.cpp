@@ -495,7 +495,7 @@ void conv_weight_transpose_batched(Tensor src, Tensor dst, Tensor table, int64_t
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
                   int64_t cfg, optional<Tensor> wt_pre, optional<Tensor> addend,
                   optional<Tensor> bn_x, optional<Tensor> bn_mask, optional<Tensor> bn_stats,
-                  optional<Tensor> bn_part, int64_t bn_relu) {
+                  optional<Tensor> bn_part, int64_t bn_relu, bool addend_sub) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc_bf16(dy, "dy");
   check_gpu(w, "w");
@@ -528,7 +528,16 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   if (addend.has_value() && addend->defined()) {
     add_t = addend->contiguous(at::MemoryFormat::ChannelsLast);
     check_nhwc_bf16(add_t, "addend");
-    TORCH_CHECK(add_t.sizes() == dx.sizes(), "dgrad: addend must have the input's shape");
+    if (addend_sub) {
+      // gradient of x[:, :, ::2, ::2] (a 1x1 / stride-2 shortcut's input): added on
+      // the stride-2 data gradient's parity class (0, 0)
+      TORCH_CHECK(stride == 2, "dgrad: a subsampled addend needs stride 2");
+      TORCH_CHECK(add_t.size(0) == B && add_t.size(1) == g.CI && add_t.size(2) == (g.H + 1) / 2 &&
+                      add_t.size(3) == (g.W + 1) / 2,
+                  "dgrad: subsampled addend must be [B, CI, ceil(H/2), ceil(W/2)]");
+    } else {
+      TORCH_CHECK(add_t.sizes() == dx.sizes(), "dgrad: addend must have the input's shape");
+    }
     add_ptr = reinterpret_cast<const uint16_t*>(add_t.data_ptr());
   }
   // fused backward of the BatchNorm(+ReLU) that produced the conv input (bn_relu >= 0)
@@ -564,8 +573,21 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
                          reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                          reinterpret_cast<uint16_t*>(dx.data_ptr()), B, g.H, g.W, g.CI, g.OH,
                          g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream(),
-                         add_ptr, fuse ? &bnf : nullptr);
+                         add_ptr, fuse ? &bnf : nullptr, add_ptr != nullptr && addend_sub);
   return dx;
+}
+
+// x[:, :, ::2, ::2] of a channels_last bf16 activation, gathered (channels_last out)
+Tensor subsample2(Tensor x) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(1) % 8 == 0, "subsample2: [B, C, H, W] with C % 8 == 0");
+  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  auto xs = at::empty({B, C, (H + 1) / 2, (W + 1) / 2},
+                      x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dmp::launch_subsample2(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                         reinterpret_cast<uint16_t*>(xs.data_ptr()), (int)B, (int)H, (int)W,
+                         (int)C, cur_stream());
+  return xs;
 }
 
 void conv_wgrad(Tensor dy, Tensor x, Tensor dw, int64_t stride, int64_t pad, int64_t cfg,
@@ -1341,7 +1363,9 @@ PYBIND11_MODULE(_native, m) {
         py::arg("cfg") = -1, py::arg("wt") = py::none(), py::arg("addend") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
         py::arg("bn_stats") = py::none(), py::arg("bn_part") = py::none(),
-        py::arg("bn_relu") = -1);
+        py::arg("bn_relu") = -1, py::arg("addend_sub") = false);
+  m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of a channels_last bf16 activation",
+        py::arg("x"));
   m.def("bn_bwd_from_partials", &bn_bwd_from_partials,
         "BN backward from conv-dgrad-epilogue partials (dz already ReLU-masked)", py::arg("x"),
         py::arg("dz"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"),

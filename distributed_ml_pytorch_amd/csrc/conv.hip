@@ -56,6 +56,10 @@ struct ConvArgs {
                         // bnrelu 3: bn.hip's 1-bit ReLU mask [pixels][CI/8] bytes
   const float* bnstat;  // the BN's [4][CI] mean | invstd | scale | shift
   int bnrelu;           // 0 no ReLU, 1 / 3 mask from bnmask, 2 mask recomputed from bnx
+  // dgrad, stride 2: the addend is the gradient of the stride-2 SUBSAMPLED input
+  // [B][ceil(H/2)][ceil(W/2)][CI] (a 1x1 / stride-2 shortcut that read x[::2, ::2]):
+  // it lands on parity class (0, 0) only, indexed by the class-local row
+  int addend_sub;
 };
 
 // Data-gradient epilogue fused with the backward of the BatchNorm(+ReLU) whose
@@ -334,7 +338,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
       (void*)a.y, 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
   // dgrad accumulate: dX = dgrad + addend (the residual branch's gradient of the
   // same input, fused here instead of an autograd add over the whole tensor)
-  const bool add_in = MODE == 1 && a.addend != nullptr;
+  const bool add_in = MODE == 1 && a.addend != nullptr && (!a.addend_sub || blockIdx.z == 0);
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
   constexpr bool BNB = MODE == 1 && STATS;   // fused BN(+ReLU) backward
@@ -390,8 +394,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
       const bool ok = mok && nok[j];
       float ad[4] = {0.f, 0.f, 0.f, 0.f};
       if (add_in) {
+        const unsigned aoff = a.addend_sub ? 2u * (unsigned)(m * a.CO) : rowoff;
         const u32x2_t av =
-            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? rowoff + 2u * n : kOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? aoff + 2u * n : kOOB, 0, 0);
         ad[0] = __uint_as_float(av.x << 16);
         ad[1] = __uint_as_float(av.x & 0xffff0000u);
         ad[2] = __uint_as_float(av.y << 16);
@@ -714,8 +719,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
       const bool ok = mok && nok[j];
       float ad[4] = {0.f, 0.f, 0.f, 0.f};
       if (add_in) {
+        const unsigned aoff = a.addend_sub ? 2u * (unsigned)(m * a.CO) : rowoff;
         const u32x2_t av =
-            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? rowoff + 2u * n : kOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? aoff + 2u * n : kOOB, 0, 0);
         ad[0] = __uint_as_float(av.x << 16);
         ad[1] = __uint_as_float(av.x & 0xffff0000u);
         ad[2] = __uint_as_float(av.y << 16);
@@ -1391,10 +1397,12 @@ void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int
 // dX (B,H,W,CI) from dY (B,OH,OW,CO) and Wt [CI][R][S][CO]; stride*stride parity classes.
 void launch_conv_dgrad(const u16* dy, const u16* wt, u16* dx, int B, int H, int W, int CI,
                        int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                       hipStream_t s, const u16* addend, const BnBwdFuse* bnf) {
+                       hipStream_t s, const u16* addend, const BnBwdFuse* bnf,
+                       bool addend_sub) {
   const long long rows = (long long)B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
   ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad, rows, nullptr,
              addend};
+  a.addend_sub = addend_sub ? 1 : 0;
   if (bnf) {
     a.part = bnf->part;
     a.bnx = bnf->x;
@@ -1410,6 +1418,32 @@ void launch_conv_dgrad(const u16* dy, const u16* wt, u16* dx, int B, int H, int 
   if (cfg < 0 || cfg >= kNumConvConfigs) cfg = conv_default_config(rows * stride * stride, CI);
   if (bnf) dispatch<1, true>(a, cfg, stride * stride, s);
   else dispatch<1, false>(a, cfg, stride * stride, s);
+}
+
+// x_sub[b][i][j][c] = x[b][2i][2j][c] (NHWC bf16, C % 8 == 0): the input of a
+// 1x1 / stride-2 shortcut, gathered once so the shortcut runs as a stride-1 GEMM
+__global__ void __launch_bounds__(256) subsample2_kernel(const u16* __restrict__ x,
+                                                         u16* __restrict__ xs, int H, int W,
+                                                         int C, int OH, int OW, long long nvec) {
+  const int cv = C / 8;
+  const long long step = (long long)gridDim.x * blockDim.x;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += step) {
+    const int c8 = (int)(v % cv);
+    const long long pix = v / cv;
+    const int j = (int)(pix % OW);
+    const long long t = pix / OW;
+    const int i = (int)(t % OH);
+    const long long b = t / OH;
+    const long long src = ((b * H + 2 * i) * W + 2 * j) * C + c8 * 8;
+    *reinterpret_cast<bf16x8*>(xs + v * 8) = *reinterpret_cast<const bf16x8*>(x + src);
+  }
+}
+
+void launch_subsample2(const u16* x, u16* xs, int B, int H, int W, int C, hipStream_t s) {
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2;
+  const long long nvec = (long long)B * OH * OW * (C / 8);
+  hipLaunchKernelGGL(subsample2_kernel, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, x, xs, H,
+                     W, C, OH, OW, nvec);
 }
 
 void launch_conv_weight_transpose(const u16* w, u16* wt, int CO, int RS, int CI, hipStream_t s) {

@@ -13,10 +13,17 @@ block output ``relu(bn2(conv2(h)) + shortcut)`` is ONE kernel on GPU.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from ..ops import layers as L
+
+
+# 1x1 / stride-2 shortcuts on conv1's subsampled alias (DMP_SC_SUB=0: full-res
+# alias and a stride-2 shortcut conv, for A/B)
+_SC_SUB = os.environ.get("DMP_SC_SUB", "1") != "0"
 
 
 class BasicBlock(nn.Module):
@@ -35,10 +42,21 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         # the shortcut reads x through conv1's alias: its gradient is summed into
-        # x's gradient by conv1's dgrad epilogue (no autograd add)
-        h, xa = self.conv1(x, alias=True)
+        # x's gradient by conv1's dgrad epilogue (no autograd add).  A 1x1 /
+        # stride-2 shortcut takes conv1's subsampled alias x[:, :, ::2, ::2] and
+        # runs at stride 1 (a plain GEMM; its gradient lands on conv1's stride-2
+        # dgrad parity class (0, 0)) when conv1 is native; else the full x.
+        sub = self.shortcut is not None and _SC_SUB and self.conv1.stride == (2, 2) \
+            and self.shortcut[0].kernel_size == (1, 1) and self.shortcut[0].stride == (2, 2) \
+            and self.shortcut[0].padding == (0, 0)
+        h, xa = self.conv1(x, alias="sub" if sub else True)
         h = self.bn1(h)
-        sc = xa if self.shortcut is None else self.shortcut(xa)
+        if self.shortcut is None:
+            sc = xa
+        elif sub and xa.shape[-1] != x.shape[-1]:
+            sc = self.shortcut[1](self.shortcut[0](xa, stride=1))
+        else:
+            sc = self.shortcut(xa)
         return self.bn2(self.conv2(h), residual=sc)
 
 

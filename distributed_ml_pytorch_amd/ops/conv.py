@@ -277,7 +277,14 @@ class _NativeConv(Function):
         # here) -- a block routes its shortcut through it, so the shortcut's
         # gradient is added inside this conv's dgrad epilogue instead of by an
         # autograd add over the whole activation
-        xa = x if alias else None
+        # alias == "sub" (stride 2): hand back x[:, :, ::2, ::2] instead -- the input
+        # of a 1x1 / stride-2 shortcut, which then runs as a stride-1 GEMM; its
+        # gradient lands on the stride-2 dgrad's parity class (0, 0)
+        ctx.alias_sub = alias == "sub" and stride == 2 and x.shape[1] % 8 == 0
+        if ctx.alias_sub:
+            xa = native().subsample2(x)
+        else:
+            xa = x if alias else None
         if want_stats:
             ctx.mark_non_differentiable(part)
             return y, part, xa
@@ -294,6 +301,12 @@ class _NativeConv(Function):
             dy = native().relu_bwd(dy, y)
         dx = None
         master = ctx.master
+        sub = ctx.alias_sub and dxa is not None
+        if sub and not ctx.needs_input_grad[0]:
+            dx = torch.zeros(x.shape, dtype=dxa.dtype, device=dxa.device).contiguous(
+                memory_format=torch.channels_last)
+            dx[:, :, ::2, ::2] = dxa
+            dxa = None
         if ctx.needs_input_grad[0] and _dgrad_cfg(dy, w16, H, W, stride, pad) == _GEMM_ROUTE:
             dx = _gemm1x1_dgrad(dy, w16, dxa)
         elif ctx.needs_input_grad[0]:
@@ -309,10 +322,12 @@ class _NativeConv(Function):
                 dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt, dxa, bn_x=bn.x,
                                          bn_mask=(x if bn.relu == 1 else
                                                   bn.mask if bn.relu == 3 else None),
-                                         bn_stats=bn.stats, bn_part=bn.part, bn_relu=bn.relu)
+                                         bn_stats=bn.stats, bn_part=bn.part, bn_relu=bn.relu,
+                                         addend_sub=sub)
                 bn.fused = (dx, dx._version)
             else:
-                dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt, dxa)
+                dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt, dxa,
+                                         addend_sub=sub)
         elif dxa is not None:
             dx = dxa
         gw = None
@@ -601,7 +616,9 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
     ``slots``: the layer's persistent ``[2][64][CO]`` fp32 BN slot buffer (zeroed;
     the consuming BatchNorm's finalize re-zeroes it); a fresh one when None.
     ``alias``: return ``(y, x_alias)``; gradients reaching ``x_alias`` are summed
-    into this conv's input gradient by the dgrad kernel itself.
+    into this conv's input gradient by the dgrad kernel itself.  ``alias="sub"``
+    (native stride-2 convs): ``x_alias`` is ``x[:, :, ::2, ::2]`` (gathered), the
+    input of a 1x1 / stride-2 shortcut run at stride 1; other routes hand back x.
     """
     if x.is_cuda and x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
@@ -614,7 +631,8 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
             y, part, xa = _NativeConv.apply(x, w16, master, _pair(stride)[0], _pair(padding)[0],
                                             bool(want_stats and not relu),
                                             slots if want_stats and not relu else None, b,
-                                            bool(alias), bool(relu))
+                                            alias if alias == "sub" else bool(alias),
+                                            bool(relu))
             if part is not None:
                 y._dmp_bn_part = part
             return (y, xa) if alias else y

@@ -28,24 +28,27 @@ class Conv2d(nn.Conv2d):
 
     emit_bn_stats = False
 
-    def forward(self, x, alias: bool = False, relu: bool = False):
+    def forward(self, x, alias=False, relu: bool = False, stride=None):
         """``alias=True`` returns ``(y, x_alias)``: route the block's shortcut
-        through ``x_alias`` and its gradient is added in this conv's dgrad."""
+        through ``x_alias`` and its gradient is added in this conv's dgrad
+        (``alias="sub"``: see ``ops.conv.conv2d``).  ``stride`` overrides the
+        module's stride (a stride-2 shortcut applied to an already subsampled x)."""
+        st = self.stride if stride is None else (stride, stride)
         if x.is_cuda and x.dtype == torch.bfloat16 and (
-                native_conv_supported(x, self.weight, self.stride, self.padding, self.dilation,
+                native_conv_supported(x, self.weight, st, self.padding, self.dilation,
                                       self.groups)
-                or small_conv_supported(x, self.weight, self.stride, self.padding,
+                or small_conv_supported(x, self.weight, st, self.padding,
                                         self.dilation, self.groups)
-                or im2col_conv_supported(x, self.weight, self.stride, self.padding,
+                or im2col_conv_supported(x, self.weight, st, self.padding,
                                          self.dilation, self.groups)):
             want = self.emit_bn_stats and self.training and not relu
             slots = bn_slot_buffer(self, "_dmp_slots", self.out_channels, x.device) if want else None
-            return _conv2d(x, None, self.bias, self.stride, self.padding, self.dilation,
+            return _conv2d(x, None, self.bias, st, self.padding, self.dilation,
                            self.groups, master=self.weight, want_stats=want, slots=slots,
                            alias=alias, relu=relu)
         w = DF.compute_weight(self.weight, x.dtype)
         b = DF.compute_weight(self.bias, x.dtype)
-        return _conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups,
+        return _conv2d(x, w, b, st, self.padding, self.dilation, self.groups,
                        alias=alias, relu=relu)
 
 

@@ -263,16 +263,22 @@ def test_conv_layer_bias_native():
     assert _rel(x.grad, xr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("stride,cin,planes", [(1, 64, 64), (2, 64, 128)])
-def test_resnet_block_alias_shortcut_grad(stride, cin, planes):
+@pytest.mark.parametrize("stride,cin,planes,hw", [(1, 64, 64, 16), (2, 64, 128, 16),
+                                                  (2, 128, 256, 15)])
+def test_resnet_block_alias_shortcut_grad(stride, cin, planes, hw):
     """BasicBlock on the native path (the shortcut's gradient is summed inside
-    conv1's dgrad epilogue through the alias output) vs an fp32 functional
-    reference of the same block."""
+    conv1's dgrad epilogue through the alias output; at stride 2 the 1x1
+    shortcut reads conv1's subsampled alias and its gradient lands on parity
+    class (0, 0), odd sizes included) vs an fp32 functional reference."""
     from distributed_ml_pytorch_amd.models.resnet import BasicBlock
 
     torch.manual_seed(0)
     blk = BasicBlock(cin, planes, stride).cuda()
-    x = torch.randn(4, cin, 16, 16, device="cuda").to(torch.bfloat16)
+    if stride == 2:
+        _, xa = blk.conv1(torch.zeros(1, cin, hw, hw, device="cuda", dtype=torch.bfloat16)
+                          .contiguous(memory_format=CL), alias="sub")
+        assert xa.shape[-1] == (hw + 1) // 2, "native stride-2 conv did not subsample its alias"
+    x = torch.randn(4, cin, hw, hw, device="cuda").to(torch.bfloat16)
     x = x.contiguous(memory_format=CL).requires_grad_(True)
     y = blk(x)
     g = torch.randn(y.shape, device="cuda")
