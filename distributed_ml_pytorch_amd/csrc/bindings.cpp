@@ -577,6 +577,19 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   return dx;
 }
 
+// dx[:, :, ::2, ::2] += xs in place (both channels_last bf16)
+void add_subsampled2(Tensor dx, Tensor xs) {
+  check_nhwc_bf16(dx, "dx");
+  check_nhwc_bf16(xs, "xs");
+  TORCH_CHECK(dx.dim() == 4 && dx.size(1) % 8 == 0 && xs.size(0) == dx.size(0) &&
+                  xs.size(1) == dx.size(1) && xs.size(2) == (dx.size(2) + 1) / 2 &&
+                  xs.size(3) == (dx.size(3) + 1) / 2,
+              "add_subsampled2: xs must be [B, C, ceil(H/2), ceil(W/2)] of dx [B, C, H, W]");
+  dmp::launch_add_subsampled2(reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                              reinterpret_cast<const uint16_t*>(xs.data_ptr()), (int)dx.size(0),
+                              (int)dx.size(2), (int)dx.size(3), (int)dx.size(1), cur_stream());
+}
+
 // x[:, :, ::2, ::2] of a channels_last bf16 activation, gathered (channels_last out)
 Tensor subsample2(Tensor x) {
   check_nhwc_bf16(x, "x");
@@ -1366,6 +1379,8 @@ PYBIND11_MODULE(_native, m) {
         py::arg("bn_relu") = -1, py::arg("addend_sub") = false);
   m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of a channels_last bf16 activation",
         py::arg("x"));
+  m.def("add_subsampled2", &add_subsampled2, "dx[:, :, ::2, ::2] += xs in place",
+        py::arg("dx"), py::arg("xs"));
   m.def("bn_bwd_from_partials", &bn_bwd_from_partials,
         "BN backward from conv-dgrad-epilogue partials (dz already ReLU-masked)", py::arg("x"),
         py::arg("dz"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"),

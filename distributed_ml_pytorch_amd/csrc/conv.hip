@@ -1439,6 +1439,38 @@ __global__ void __launch_bounds__(256) subsample2_kernel(const u16* __restrict__
   }
 }
 
+// dx[b][2i][2j][c] += xs[b][i][j][c] in place: the gradient of a subsampled alias
+// added back onto a full-resolution data gradient (bf16, fp32 add, one rounding)
+__global__ void __launch_bounds__(256) add_subsampled2_kernel(u16* __restrict__ dx,
+                                                              const u16* __restrict__ xs, int H,
+                                                              int W, int C, int OH, int OW,
+                                                              long long nvec) {
+  const int cv = C / 8;
+  const long long step = (long long)gridDim.x * blockDim.x;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += step) {
+    const int c8 = (int)(v % cv);
+    const long long pix = v / cv;
+    const int j = (int)(pix % OW);
+    const long long t = pix / OW;
+    const int i = (int)(t % OH);
+    const long long b = t / OH;
+    u16* d = dx + ((b * H + 2 * i) * W + 2 * j) * C + c8 * 8;
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(d);
+    const bf16x8 e = *reinterpret_cast<const bf16x8*>(xs + v * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(bf2f(a.v[k]) + bf2f(e.v[k]));
+    *reinterpret_cast<bf16x8*>(d) = o;
+  }
+}
+
+void launch_add_subsampled2(u16* dx, const u16* xs, int B, int H, int W, int C, hipStream_t s) {
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2;
+  const long long nvec = (long long)B * OH * OW * (C / 8);
+  hipLaunchKernelGGL(add_subsampled2_kernel, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, dx,
+                     xs, H, W, C, OH, OW, nvec);
+}
+
 void launch_subsample2(const u16* x, u16* xs, int B, int H, int W, int C, hipStream_t s) {
   const int OH = (H + 1) / 2, OW = (W + 1) / 2;
   const long long nvec = (long long)B * OH * OW * (C / 8);

@@ -136,6 +136,9 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int
 // x_sub = x[:, ::2, ::2, :] (NHWC bf16, C % 8 == 0), [B][ceil(H/2)][ceil(W/2)][C]
 void launch_subsample2(const uint16_t* x, uint16_t* xs, int B, int H, int W, int C,
                        hipStream_t s);
+// dx[:, ::2, ::2, :] += xs in place (NHWC bf16)
+void launch_add_subsampled2(uint16_t* dx, const uint16_t* xs, int B, int H, int W, int C,
+                            hipStream_t s);
 void launch_conv_weight_transpose(const uint16_t* w, uint16_t* wt, int CO, int RS, int CI,
                                   hipStream_t s);
 // dbias: optional fp32 [CO] += column sums of dY (gather kernel only; halo cfgs fall back)

@@ -26,6 +26,12 @@ from ..ops import layers as L
 _SC_SUB = os.environ.get("DMP_SC_SUB", "1") != "0"
 
 
+def _sc_sub(shortcut) -> bool:
+    """A 1x1 / stride-2 / unpadded shortcut conv that can run on x[:, :, ::2, ::2]."""
+    return (shortcut is not None and _SC_SUB and shortcut[0].kernel_size == (1, 1)
+            and shortcut[0].stride == (2, 2) and shortcut[0].padding == (0, 0))
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -46,9 +52,7 @@ class BasicBlock(nn.Module):
         # stride-2 shortcut takes conv1's subsampled alias x[:, :, ::2, ::2] and
         # runs at stride 1 (a plain GEMM; its gradient lands on conv1's stride-2
         # dgrad parity class (0, 0)) when conv1 is native; else the full x.
-        sub = self.shortcut is not None and _SC_SUB and self.conv1.stride == (2, 2) \
-            and self.shortcut[0].kernel_size == (1, 1) and self.shortcut[0].stride == (2, 2) \
-            and self.shortcut[0].padding == (0, 0)
+        sub = self.conv1.stride == (2, 2) and _sc_sub(self.shortcut)
         h, xa = self.conv1(x, alias="sub" if sub else True)
         h = self.bn1(h)
         if self.shortcut is None:
@@ -78,9 +82,18 @@ class Bottleneck(nn.Module):
                 L.Conv2d(cin, out, 1, stride=stride, bias=False), L.BatchNorm2d(out))
 
     def forward(self, x):
-        h, xa = self.conv1(x, alias=True)
+        # a 1x1 / stride-2 shortcut reads conv1's subsampled alias and runs at
+        # stride 1 (a GEMM); its gradient is added onto dX's even pixels after
+        # conv1's dgrad (see BasicBlock)
+        sub = _sc_sub(self.shortcut)
+        h, xa = self.conv1(x, alias="sub" if sub else True)
         h = self.bn2(self.conv2(self.bn1(h)))
-        sc = xa if self.shortcut is None else self.shortcut(xa)
+        if self.shortcut is None:
+            sc = xa
+        elif sub and xa.shape[-1] != x.shape[-1]:
+            sc = self.shortcut[1](self.shortcut[0](xa, stride=1))
+        else:
+            sc = self.shortcut(xa)
         return self.bn3(self.conv3(h), residual=sc)
 
 

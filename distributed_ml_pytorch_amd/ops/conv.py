@@ -277,10 +277,11 @@ class _NativeConv(Function):
         # here) -- a block routes its shortcut through it, so the shortcut's
         # gradient is added inside this conv's dgrad epilogue instead of by an
         # autograd add over the whole activation
-        # alias == "sub" (stride 2): hand back x[:, :, ::2, ::2] instead -- the input
-        # of a 1x1 / stride-2 shortcut, which then runs as a stride-1 GEMM; its
-        # gradient lands on the stride-2 dgrad's parity class (0, 0)
-        ctx.alias_sub = alias == "sub" and stride == 2 and x.shape[1] % 8 == 0
+        # alias == "sub": hand back x[:, :, ::2, ::2] instead -- the input of a 1x1 /
+        # stride-2 shortcut, which then runs as a stride-1 GEMM; its gradient lands
+        # on the stride-2 dgrad's parity class (0, 0) (this conv has stride 2) or
+        # is added onto the strided positions of dX after the dgrad (stride 1)
+        ctx.alias_sub = alias == "sub" and x.shape[1] % 8 == 0
         if ctx.alias_sub:
             xa = native().subsample2(x)
         else:
@@ -302,11 +303,14 @@ class _NativeConv(Function):
         dx = None
         master = ctx.master
         sub = ctx.alias_sub and dxa is not None
+        sub_after = None          # subsampled alias gradient added after the dgrad
         if sub and not ctx.needs_input_grad[0]:
             dx = torch.zeros(x.shape, dtype=dxa.dtype, device=dxa.device).contiguous(
                 memory_format=torch.channels_last)
             dx[:, :, ::2, ::2] = dxa
             dxa = None
+        elif sub and (stride != 2 or _dgrad_cfg(dy, w16, H, W, stride, pad) == _GEMM_ROUTE):
+            sub_after, dxa, sub = dxa.contiguous(memory_format=torch.channels_last), None, False
         if ctx.needs_input_grad[0] and _dgrad_cfg(dy, w16, H, W, stride, pad) == _GEMM_ROUTE:
             dx = _gemm1x1_dgrad(dy, w16, dxa)
         elif ctx.needs_input_grad[0]:
@@ -330,6 +334,15 @@ class _NativeConv(Function):
                                          addend_sub=sub)
         elif dxa is not None:
             dx = dxa
+        if sub_after is not None:
+            dx = dx.contiguous(memory_format=torch.channels_last)
+            native().add_subsampled2(dx, sub_after)
+            link = ctx.bnlink
+            if link is not None and link.fused is not None:
+                # the native in-place add does not bump autograd's version counter:
+                # invalidate the BN partials the fused dgrad epilogue recorded (they
+                # miss the added gradient) so the BN backward redoes its reduce
+                link.fused = (link.fused[0], -1)
         gw = None
         if master is not None and master.requires_grad:
             wcfg = _wgrad_cfg(dy, x, tuple(master.shape), stride, pad)
