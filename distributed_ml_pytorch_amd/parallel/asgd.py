@@ -87,7 +87,9 @@ class Asynchronous(Optimizer):
         return self.acc
 
     def zero_grad(self, set_to_none: bool = False):
-        """Zero the flat grad arena (views stay attached; ``set_to_none`` ignored)."""
+        """Zero the flat grad arena (views stay attached; ``set_to_none`` ignored).
+        Opens the compute half of a step (closed by ``local_step``)."""
+        self.client.in_compute = True
         self.arena.ensure_grads_attached()
         self.arena.zero_grad()
 
@@ -130,6 +132,7 @@ class Asynchronous(Optimizer):
         """Device-only half of a step (graph-capturable): fused accumulate + SGD."""
         self._local_update(self.param_groups[0]["lr"])
         self.arena.bump()
+        self.client.in_compute = False
 
     @torch.no_grad()
     def comm_step(self):

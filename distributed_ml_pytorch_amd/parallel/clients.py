@@ -23,6 +23,7 @@ never blocks and forward/backward of steps k+1..k+s overlap the transfer.
 from __future__ import annotations
 
 import logging
+import os
 from collections import deque
 
 import torch
@@ -60,6 +61,12 @@ class PSClient:
         self.pulls = 0
         self.bytes_sent = 0
         self.bytes_recv = 0
+        # SURVEY §5.2 debug check: a pulled snapshot may only land between steps
+        # (the reference's listener thread overwrote parameters mid-step).  The
+        # optimizer flags the compute half of a step (zero_grad .. local_step);
+        # DMP_DEBUG_LANDING=1 turns a landing inside it into an error.
+        self.debug_landing = os.environ.get("DMP_DEBUG_LANDING", "0") == "1"
+        self.in_compute = False
 
     # -- wiring ------------------------------------------------------------
     def attach(self, opt):
@@ -111,6 +118,10 @@ class PSClient:
 
     # -- landing -----------------------------------------------------------
     def _land(self, pend: _Pending):
+        if self.debug_landing and self.in_compute:
+            raise RuntimeError(
+                f"pull of step {pend.step} landed inside a training step (between zero_grad "
+                "and local_step): parameters would change under forward/backward")
         arena = self.arena
         acc = self.opt.acc if self.pull_mode == "rebase" else None
         src = pend.buf

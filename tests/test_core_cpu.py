@@ -118,6 +118,25 @@ def test_staleness_bound_delays_landing():
     assert torch.all(opt.arena.p32 == 0.5)
 
 
+def test_debug_landing_rejects_a_pull_inside_a_step(monkeypatch):
+    """with DMP_DEBUG_LANDING=1 a pulled snapshot landing between
+    zero_grad and local_step (mid forward/backward) is an error; the normal
+    step-boundary landing of Asynchronous.step passes."""
+    monkeypatch.setenv("DMP_DEBUG_LANDING", "1")
+    m, _, _ = build_model("mlp")
+    client = LocalPSClient(staleness=0)
+    opt = Asynchronous(m.parameters(), lr=0.1, n_push=1000, n_pull=1, model=m, client=client)
+    assert client.debug_landing
+    x, y = torch.randn(4, 1, 28, 28), torch.randint(0, 10, (4,))
+    opt.zero_grad()
+    client.request_pull(step=0)
+    with pytest.raises(RuntimeError, match="inside a training step"):
+        client.land_due(1)
+    nn.functional.cross_entropy(m(x), y).backward()
+    opt.step()                      # local_step closes the compute half, then lands
+    assert not client.pending
+
+
 def test_asgd_rejects_bad_args():
     m, _, _ = build_model("mlp")
     with pytest.raises(ValueError):
