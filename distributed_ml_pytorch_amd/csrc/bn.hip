@@ -320,10 +320,19 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
 
 // ---------------------------------------------------------------- launchers
 int bn_num_partials(long long M, int C) {
+  // DMP_BN_PART_VPT / DMP_BN_PART_CAP: A/B knobs of the reduce grid
+  static const long long vpt = [] {
+    const char* e = std::getenv("DMP_BN_PART_VPT");
+    return e ? std::max(1, std::atoi(e)) : 8;
+  }();
+  static const long long cap = [] {
+    const char* e = std::getenv("DMP_BN_PART_CAP");
+    return e ? std::max(1, std::atoi(e)) : 2048;
+  }();
   long long vecs = M * (C / 8);
-  long long g = vecs / (256 * 8);   // >= 8 rows (two 4-row trips) per thread
+  long long g = vecs / (256 * vpt);   // >= 8 rows (two 4-row trips) per thread
   if (g < 1) g = 1;
-  if (g > 2048) g = 2048;
+  if (g > cap) g = cap;
   if (g > M) g = M;
   return (int)g;
 }
