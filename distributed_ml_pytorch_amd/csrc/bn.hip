@@ -654,9 +654,13 @@ static dim3 fold_grid(long long M, int C, int cs) {
     const char* e = std::getenv("DMP_BN_FOLD_VPT");
     return e ? std::max(1, std::atoi(e)) : 4;
   }();
+  static const long long total = [] {
+    const char* e = std::getenv("DMP_BN_FOLD_CAP");
+    return e ? std::max(1, std::atoi(e)) : 2048;
+  }();
   const long long nsl = C / cs;
   long long nrb = (M * (cs / 8) + 256 * vpt - 1) / (256 * vpt);
-  const long long cap = std::max<long long>(1, 2048 / nsl);
+  const long long cap = std::max<long long>(1, total / nsl);
   nrb = std::max<long long>(1, std::min(nrb, std::min(cap, M)));
   return dim3((unsigned)nrb, (unsigned)nsl);
 }
