@@ -13,8 +13,11 @@ Topologies (``--ps``):
 * ``sharded`` (N > 1 default): every rank is a worker and owns 1/N of the fp32
   master; push = reduce-scatter of the accumulated deltas + apply, pull =
   all-gather, both on a side HIP stream over RCCL/xGMI, landed with
-  staleness <= 1 step.  Simultaneous pushes are SUMMED, as a central Downpour
-  PS adds every worker's delta (``--delta-scale mean`` averages instead).
+  staleness <= 1 step.  Simultaneous pushes are AVERAGED by default at N > 1
+  (``--delta-scale auto`` = ``mean``): summing them as a central Downpour PS adds
+  every worker's delta (``--delta-scale sum``) multiplies the step by N, and at
+  N = 8 with lr 0.05 the ResNet-18 time-to-target run collapsed to a uniform
+  predictor (loss ln 10, profiles/ttl_n8_delta_scale_r2.txt).
   The collectives make it lock-step at pull time (bounded drift).
 * ``sharded_async``: the same 1/N shards, each served by its own PS thread
   (point-to-point gloo push/pull, host-staged payloads): no collective after
@@ -68,8 +71,9 @@ def parse(argv=None):
                          "(/root/reference/example/main.py:142); 0 skips")
     ap.add_argument("--mode", default="asgd", choices=["asgd", "sync", "single"])
     ap.add_argument("--ps", default="auto", choices=["auto", "local", "sharded", "sharded_async", "central"])
-    ap.add_argument("--delta-scale", default="sum",
-                    help="sharded PS: 'sum' of simultaneous pushes (Downpour PS), 'mean', or x")
+    ap.add_argument("--delta-scale", default="auto",
+                    help="sharded PS: 'sum' of simultaneous pushes (Downpour PS), 'mean', or x; "
+                         "'auto' = mean for the sharded PS at N > 1, else sum")
     ap.add_argument("--n-push", type=int, default=10)
     ap.add_argument("--n-pull", type=int, default=10)
     ap.add_argument("--staleness", type=int, default=1)
@@ -237,6 +241,9 @@ def time_to_target(a, cfg, ctx, mode=None):
             # training would block in a push the others never join
             m = ctx.worker_mean(torch.stack(window).mean().reshape(1))
             window.clear()
+            if steps % 200 == 0 and info.rank == 0:   # progress for long (multi-rank) runs
+                print(f"[ttl] {mode or cfg.mode} step {steps} mean loss {float(m.item()):.4f}",
+                      file=sys.stderr, flush=True)
             if float(m.item()) <= a.ttl_target:
                 reached = True
                 break
@@ -258,6 +265,9 @@ def run(a):
     world = info.world_size
     if a.mode == "asgd" and a.ps == "auto":
         a.ps = "sharded" if world > 1 else "local"
+    if a.delta_scale == "auto":
+        a.delta_scale = "mean" if a.mode == "asgd" and a.ps.startswith("sharded") and world > 1 \
+            else "sum"
     if a.mode == "asgd" and a.ps == "local" and world > 1:
         raise SystemExit("--ps local is the 1-GPU in-process PS; with N > 1 use sharded/central")
     if a.mode == "asgd" and a.ps == "central" and world < 2:
