@@ -266,8 +266,7 @@ def run(a):
     if a.mode == "asgd" and a.ps == "auto":
         a.ps = "sharded" if world > 1 else "local"
     if a.delta_scale == "auto":
-        a.delta_scale = "mean" if a.mode == "asgd" and a.ps.startswith("sharded") and world > 1 \
-            else "sum"
+        a.delta_scale = "mean" if a.mode == "asgd" and a.ps != "local" and world > 1 else "sum"
     if a.mode == "asgd" and a.ps == "local" and world > 1:
         raise SystemExit("--ps local is the 1-GPU in-process PS; with N > 1 use sharded/central")
     if a.mode == "asgd" and a.ps == "central" and world < 2:
@@ -359,7 +358,7 @@ def run(a):
                        "seq_len": None, "image": "x".join(map(str, in_shape)),
                        "parallelism": par, "n_push": a.n_push, "n_pull": a.n_pull,
                        "staleness": a.staleness, "lr": a.lr,
-                       "push_combine": a.delta_scale if a.ps.startswith("sharded") else "sum",
+                       "push_combine": a.delta_scale,
                        "hip_graph": bool(graphed), "master_dtype": "fp32"},
             "world_size": world,
             "backend": info.backend,

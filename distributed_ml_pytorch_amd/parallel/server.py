@@ -61,13 +61,24 @@ class ParameterServer:
     def __init__(self, model=None, numel: int | None = None, workers=None, control_group=None,
                  pair_groups=None, payload: str = "auto", device=None, init_policy: str = "first",
                  checkpoint_path: str | None = None, checkpoint_every: int = 0,
-                 worker_timeout: float | None = None):
+                 worker_timeout: float | None = None, delta_scale: str | float = "sum"):
+        """``delta_scale``: factor on every pushed delta -- ``"sum"`` (1.0, the
+        reference Downpour PS: /root/reference/asgd/optim/Asynchronous.py:48-55
+        ships raw accumulated updates that the PS adds), ``"mean"`` (1 / #workers:
+        the W workers' concurrent deltas average instead of adding up, which keeps
+        many-worker runs stable; profiles/ttl_n8_delta_scale_r2.txt), or a float."""
         if not dist.is_initialized():
             raise RuntimeError("ParameterServer needs torch.distributed to be initialised")
         self.rank = dist.get_rank()
         world = dist.get_world_size()
         self.workers = list(workers) if workers is not None else [
             r for r in range(world) if r != self.rank]
+        if delta_scale == "sum":
+            self.delta_scale = 1.0
+        elif delta_scale == "mean":
+            self.delta_scale = 1.0 / max(1, len(self.workers))
+        else:
+            self.delta_scale = float(delta_scale)
         if payload == "auto":
             payload = "rccl" if dist.get_backend() == "nccl" else "gloo"
         self.payload = payload
@@ -166,9 +177,10 @@ class ParameterServer:
     def _apply(self, delta: torch.Tensor):
         if self._native is not None:
             with torch.cuda.stream(self.stream):
-                self._native.ps_apply(self.shard, delta, None, 1.0)
+                self._native.ps_apply(self.shard, delta, None, self.delta_scale)
         else:
-            self.shard[: self.numel].add_(delta[: self.numel].to(torch.float32))
+            self.shard[: self.numel].add_(delta[: self.numel].to(torch.float32),
+                                          alpha=self.delta_scale)
         self.version += 1
 
     def _set(self, params: torch.Tensor):

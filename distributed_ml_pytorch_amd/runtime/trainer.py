@@ -79,7 +79,7 @@ class TrainConfig:
     checkpoint_every: int = 0
     resume: str | None = None         # base path: workers read <base>.worker<rank>.pt, the PS <base>
     ps_resume: str | None = None      # explicit PS checkpoint (overrides <base> for the PS)
-    delta_scale: str = "sum"          # sharded PS: "sum" (Downpour PS semantics) | "mean" | float
+    delta_scale: str = "sum"          # PS push combine: "sum" (Downpour PS semantics) | "mean" | float
     ps_worker_timeout: float = 0.0    # central PS: drop a worker silent this long (0 = never)
     bucket_mb: float = 32.0
     label_smoothing: float = 0.0
@@ -325,7 +325,8 @@ def run_server(cfg: TrainConfig, info: DistInfo, ps_groups):
                              device=info.device if payload == "rccl" else "cpu",
                              checkpoint_path=cfg.checkpoint,
                              checkpoint_every=cfg.checkpoint_every,
-                             worker_timeout=cfg.ps_worker_timeout or None)
+                             worker_timeout=cfg.ps_worker_timeout or None,
+                             delta_scale=cfg.delta_scale)
     ps_path = _ps_resume_path(cfg)
     if ps_path:
         server.load_checkpoint(ps_path)

@@ -59,6 +59,7 @@ def test_bench_central_ps_three_ranks():
     assert out["n_gpus"] == 3 and out["workers"] == 2
     assert out["config"]["global_batch"] == 16
     assert out["config"]["parallelism"] == "asgd-central-ps 1ps+2w"
+    assert out["config"]["push_combine"] == "mean"     # --delta-scale auto at N > 1
     ps = out["ps"]
     # 8 steps per worker, push/pull at idx 0,2,4,6
     assert ps["counts"] == {"ParameterUpdate": 2, "GradientUpdate": 8, "ParameterRequest": 8}

@@ -94,6 +94,26 @@ def test_central_ps_one_server_two_workers():
         assert out[r]["test_accuracy"] > 0.3       # learnable synthetic task
 
 
+def _ps_delta_scale(rank, world):
+    from distributed_ml_pytorch_amd.parallel.server import ParameterServer
+
+    out = {}
+    for mode, expect in (("sum", 1.0), ("mean", 1.0 / 3), (0.25, 0.25)):
+        ps = ParameterServer(numel=10, workers=[1, 2, 3], delta_scale=mode)
+        before = ps.shard[:10].clone()
+        d = torch.arange(10, dtype=torch.float32)
+        ps._apply(d)
+        out[str(mode)] = float((ps.shard[:10] - before - expect * d).abs().max())
+    return out
+
+
+def test_ps_delta_scale_sum_mean_float():
+    """Central PS push combine: the reference's raw sum (1.0), the mean over its
+    workers (1/W) or a given factor, applied to every pushed delta."""
+    out = _run(_ps_delta_scale, 1)
+    assert all(v < 1e-6 for v in out[0].values()), out
+
+
 # --------------------------------------------------------------- sharded PS
 def _sharded(rank, world):
     from distributed_ml_pytorch_amd.models import build_model
