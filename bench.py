@@ -25,7 +25,8 @@ Topologies (``--ps``):
 * ``central``: the reference topology (/root/reference/Makefile:13-20,
   example/main.py:135-138): rank 0 is the parameter server (fp32 master on its
   GPU, payloads over one RCCL communicator per (PS, worker) pair, headers on a
-  gloo control group), ranks 1..N-1 are workers.  Whole-node samples/s counts
+  gloo control group), ranks 1..N-1 are workers; pushed deltas are averaged
+  over the workers by default (``--delta-scale auto``; ``sum`` = the reference).  Whole-node samples/s counts
   the workers' samples only (the PS GPU trains nothing).
 
 Per-GPU batch is fixed as N grows (weak scaling).
