@@ -225,9 +225,16 @@ def time_to_target(a, cfg, ctx, mode=None):
     torch.manual_seed(1000 + info.rank)
     w = Worker(cfg, info, ctx.ps_groups)
     w.enable_graph(bool(a.graph))
+    # one fixed dataset of --ttl-batches batches for every N (seed shared by all
+    # ranks), each worker starting at its own offset into it: with per-rank
+    # datasets, N workers saw N x the distinct samples and the training loss fell
+    # later simply because there was less to memorise (sync DP at N = 8 took
+    # 2200 steps against 970 at N = 1 in the 8-rank rehearsal)
     pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device,
                            n_batches=a.ttl_batches, dtype=w.compute_dtype,
-                           seed=100 + info.rank, learnable=True, signal=a.ttl_signal)
+                           seed=100, learnable=True, signal=a.ttl_signal)
+    widx = info.rank - 1 if ctx.central else info.rank
+    pool.i = (widx * a.ttl_batches // max(1, ctx.n_workers)) % a.ttl_batches
     ctx.worker_barrier()
     _sync()
     t0 = time.perf_counter()
