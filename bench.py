@@ -93,7 +93,7 @@ def parse(argv=None):
     ap.add_argument("--ttl-signal", type=float, default=0.05,
                     help="class-template amplitude of the time-to-target images (0.05: ~1000 "
                          "steps to loss 0.5 at N=1, profiles/ttl_calibration_r2.txt)")
-    ap.add_argument("--ttl-batches", type=int, default=128, help="distinct TTL batches per rank")
+    ap.add_argument("--ttl-batches", type=int, default=128, help="distinct TTL batches (one dataset, all ranks)")
     ap.add_argument("--ttl-compare-sync", type=int, default=1,
                     help="also measure time-to-target of sync all-reduce DP at the same N")
     return ap.parse_args(argv)
@@ -393,8 +393,8 @@ def run(a):
             out.update(ttl)
             out.update({"ttl_target_loss": a.ttl_target,
                         "ttl_data": f"synthetic class-template images (signal {a.ttl_signal} "
-                                    f"+ N(0,1) noise), {a.ttl_batches} distinct batches per "
-                                    "worker"})
+                                    f"+ N(0,1) noise), one dataset of {a.ttl_batches} "
+                                    "batches shared by all workers (per-worker offsets)"})
         if ttl_sync is not None:
             out["ttl_sync_dp"] = ttl_sync
         print(json.dumps(out), flush=True)
