@@ -51,9 +51,10 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-# per-shape kernel picks measured offline on MI355X (ops/tuner.py); set before the
+# per-shape kernel picks measured offline on MI355X (ops/tuner.py), loaded as a
+# READ-ONLY seed (a bench run never rewrites the committed file); set before the
 # package is imported
-os.environ.setdefault("DMP_CONV_TUNE_CACHE", os.path.join(
+os.environ.setdefault("DMP_CONV_TUNE_SEED", os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "tuning", "mi355x_tune_cache.json"))
 
 METRIC = "samples/sec (whole node) ResNet-18 ASGD at 1/2/4/8 MI355X; time-to-target-loss"
@@ -73,8 +74,12 @@ def parse(argv=None):
     ap.add_argument("--mode", default="asgd", choices=["asgd", "sync", "single"])
     ap.add_argument("--ps", default="auto", choices=["auto", "local", "sharded", "sharded_async", "central"])
     ap.add_argument("--delta-scale", default="auto",
-                    help="sharded PS: 'sum' of simultaneous pushes (Downpour PS), 'mean', or x; "
-                         "'auto' = mean for the sharded PS at N > 1, else sum")
+                    help="PS push combine: 'sum' (Downpour PS), 'mean' over workers, or x; "
+                         "'auto' = mean for the sharded PSs at N > 1 (their pushes are applied "
+                         "together), sum for the central PS (the reference, applied one by one)")
+    ap.add_argument("--wire-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="push/pull payload dtype (master stays fp32; bf16 deltas are "
+                         "reduced in fp32 by the sharded PS)")
     ap.add_argument("--n-push", type=int, default=10)
     ap.add_argument("--n-pull", type=int, default=10)
     ap.add_argument("--staleness", type=int, default=1)
@@ -163,6 +168,16 @@ class _Ctx:
             dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM,
                             group=self.cpu_group)
         return t.tolist()
+
+    def gather(self, obj):
+        """Every rank's ``obj`` (host side), in rank order."""
+        import torch.distributed as dist
+
+        if not self.info.is_distributed:
+            return [obj]
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.cpu_group)
+        return out
 
     def worker_mean(self, t):
         """Mean of a device scalar over the workers (a TTL stop decision)."""
@@ -274,17 +289,26 @@ def run(a):
     if a.mode == "asgd" and a.ps == "auto":
         a.ps = "sharded" if world > 1 else "local"
     if a.delta_scale == "auto":
-        a.delta_scale = "mean" if a.mode == "asgd" and a.ps != "local" and world > 1 else "sum"
+        # the sharded PSs apply the W simultaneous pushes together ('sum' collapsed
+        # the N=8 TTL run, profiles/ttl_n8_delta_scale_r2.txt); the central PS
+        # applies each push as it arrives, as the reference's Downpour PS does
+        a.delta_scale = "mean" if (a.mode == "asgd" and a.ps in ("sharded", "sharded_async")
+                                   and world > 1) else "sum"
     if a.mode == "asgd" and a.ps == "local" and world > 1:
         raise SystemExit("--ps local is the 1-GPU in-process PS; with N > 1 use sharded/central")
     if a.mode == "asgd" and a.ps == "central" and world < 2:
         raise SystemExit("--ps central needs >= 2 ranks (rank 0 = PS, ranks 1.. = workers)")
     ctx = _Ctx(a, info)
+    from distributed_ml_pytorch_amd.runtime.dist import preflight
+
+    # observed, not configured: the ranks a collective reached, distinct devices,
+    # every (PS, worker) payload communicator answering (raises on a mismatch)
+    pf = preflight(info, ctx.cpu_group, ctx.ps_groups[1] if ctx.ps_groups else None, 0)
     cfg = TrainConfig(model=a.model, batch_size=a.batch, lr=a.lr, momentum=a.momentum,
                       n_push=a.n_push, n_pull=a.n_pull, staleness=a.staleness, mode=a.mode,
                       ps=a.ps if a.mode == "asgd" else "local", dtype=a.dtype, cuda=True,
                       evaluate=False, verbose=False, bucket_mb=a.bucket_mb,
-                      delta_scale=a.delta_scale, payload="auto")
+                      delta_scale=a.delta_scale, payload="auto", wire_dtype=a.wire_dtype)
     res = {}
     ps_stats = None
     if ctx.is_ps:
@@ -337,6 +361,12 @@ def run(a):
     else:
         shape_src = ctx.host_reduce(list(map(float, in_shape)))
     in_shape = tuple(int(v) for v in shape_src)
+    # per-rank worker facts (graph capture, host phases, device comm spans) gathered
+    # onto rank 0: in the central topology rank 0 is the PS and trains nothing
+    mine = None if ctx.is_ps else {"rank": info.rank, "hip_graph": bool(graphed),
+                                   "phases_host_ms": res.get("phases_host_ms"),
+                                   "comm": res.get("comm")}
+    ranks = ctx.gather(mine)
     if info.rank == 0:
         nw = ctx.n_workers
         global_batch = a.batch * nw
@@ -346,6 +376,8 @@ def run(a):
         if ctx.central:
             par = f"asgd-central-ps 1ps+{nw}w"
         on_gpu = cuda
+        workers = [r for r in ranks if r is not None]
+        graphed = bool(workers) and all(r["hip_graph"] for r in workers)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -367,19 +399,28 @@ def run(a):
                        "parallelism": par, "n_push": a.n_push, "n_pull": a.n_pull,
                        "staleness": a.staleness, "lr": a.lr,
                        "push_combine": a.delta_scale,
-                       "hip_graph": bool(graphed), "master_dtype": "fp32"},
+                       "hip_graph": bool(graphed), "master_dtype": "fp32",
+                       "wire_dtype": a.wire_dtype},
             "world_size": world,
             "backend": info.backend,
-            "rccl_ranks": world if info.backend == "nccl" else 0,
+            "rccl_ranks": pf["rccl_ranks"],
+            "preflight": {k: pf[k] for k in ("ranks_observed", "devices_distinct",
+                                             "pairs_pinged") if k in pf},
             "workers": nw,
             "device": dev_name if on_gpu else "cpu",
             "ms_per_step_fastest_rank": round(1e3 * min_elapsed / a.steps, 4),
             "final_loss": round(final_loss, 4),
         }
-        if res.get("phases_host_ms"):
-            out["phases_host_ms"] = res["phases_host_ms"]
-        if res.get("comm"):
-            out["comm_rank0"] = res["comm"]
+        # host phases / comm spans of the first WORKER (rank 0, or rank 1 when
+        # rank 0 is the central PS), plus the per-worker graph flags
+        first = workers[0] if workers else {}
+        if first.get("phases_host_ms"):
+            out["phases_host_ms"] = first["phases_host_ms"]
+        if first.get("comm"):
+            out["comm_first_worker"] = first["comm"]
+            out["comm_first_worker_rank"] = first["rank"]
+        if len(workers) > 1:
+            out["worker_hip_graph"] = [bool(r["hip_graph"]) for r in workers]
         if a.ref_batch and ref_elapsed > 0:
             out["reference_batch"] = {
                 "per_gpu_batch": a.ref_batch, "global_batch": a.ref_batch * nw,

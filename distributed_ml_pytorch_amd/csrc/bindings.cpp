@@ -403,20 +403,34 @@ Tensor col2im(Tensor dcols, int64_t B, int64_t CI, int64_t H, int64_t W, int64_t
 
 // dx = y > 0 ? dy : 0 over dense bf16 tensors of one layout (out may alias dy)
 Tensor relu_bwd(Tensor dy, Tensor y, optional<Tensor> out) {
-  check_gpu(y, "y");
-  TORCH_CHECK(y.scalar_type() == at::kBFloat16, "relu_bwd: bf16 tensors");
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16, "relu_bwd: bf16 GPU tensors");
   const auto mf = y.dim() == 4 && y.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                           !y.is_contiguous()
                       ? at::MemoryFormat::ChannelsLast
                       : at::MemoryFormat::Contiguous;
+  // the kernel reads / writes 16-B vectors over one dense layout: a strided y is
+  // made dense in the layout dy is brought to, and an operand that is dense but
+  // not 16-B aligned (an offset slice such as x[..., 1:]) goes through an aligned
+  // copy (fresh allocations are 256-B aligned)
+  auto aligned = [](const Tensor& t) {
+    return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15u) == 0;
+  };
+  y = y.contiguous(mf);
   dy = dy.contiguous(mf);
+  check_gpu(y, "y");
+  if (!aligned(y)) y = y.clone(mf);
+  if (!aligned(dy)) dy = dy.clone(mf);
   TORCH_CHECK(dy.sizes() == y.sizes() && dy.scalar_type() == at::kBFloat16, "relu_bwd: dy shape");
-  Tensor dx = out.has_value() && out->defined() ? *out : at::empty_like(dy);
-  TORCH_CHECK(dx.sizes() == y.sizes() && dx.is_contiguous(mf), "relu_bwd: out layout");
+  Tensor dst = out.has_value() && out->defined() ? *out : at::empty_like(dy);
+  TORCH_CHECK(dst.sizes() == y.sizes() && dst.is_contiguous(mf) &&
+                  dst.scalar_type() == at::kBFloat16,
+              "relu_bwd: out layout");
+  Tensor dx = aligned(dst) ? dst : at::empty_like(dy);
   dmp::launch_relu_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                        reinterpret_cast<const uint16_t*>(y.data_ptr()),
                        reinterpret_cast<uint16_t*>(dx.data_ptr()), y.numel(), cur_stream());
-  return dx;
+  if (!dx.is_same(dst)) dst.copy_(dx);
+  return dst;
 }
 
 // ---------------------------------------------------------------- convolution

@@ -152,6 +152,9 @@ class AsyncShardedPSClient(PSClient):
         # every rank creates both groups in the same order (torch new_group rule)
         self.req = dist.new_group(list(range(self.world)), backend="gloo")
         self.rep = dist.new_group(list(range(self.world)), backend="gloo")
+        # host barriers (resume) on a group of their own: the shard servers keep an
+        # any-source receive posted on `req` at all times
+        self.ctl = dist.new_group(list(range(self.world)), backend="gloo")
         lo = self.rank * self.shard_n
         init = self.arena.p32.detach()[lo: lo + self.shard_n].cpu()
         self.server = ShardServer(self.rank, self.world, init, self.req, self.rep, scale).start()
@@ -233,6 +236,9 @@ class AsyncShardedPSClient(PSClient):
         with self.server.lock:
             self.server.master.copy_(sd["master"])
             self.server.version = int(sd.get("shard_version", 0))
+        # every shard restored before anyone asks for it: without this barrier a
+        # fast rank's forced pull could be answered with a peer's pre-restore shard
+        dist.barrier(group=self.ctl)
         # re-sync the live parameters from every restored shard
         self.request_pull(0)
         self.land_due(0, force=True)

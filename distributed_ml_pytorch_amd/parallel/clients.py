@@ -496,16 +496,52 @@ class ShardedPSClient(PSClient):
             self.arena.refresh_shadow()
         lo = self.rank * self.shard_n
         self.master = self.arena.p32[lo: lo + self.shard_n].detach().clone()
-        self.delta_shard = torch.zeros(self.shard_n, dtype=self.wire_dtype, device=self.device)
+        # fp32 wire: reduce-scatter the deltas (fp32 sums on the wire).  bf16 wire:
+        # an all-to-all moves the same (W-1)/W of the bytes, but every rank gets
+        # the W bf16 slices of its shard unreduced and adds them to its fp32
+        # master one by one -- no bf16 partial sums (a bf16 reduce-scatter would
+        # round the running sum to 8 bits at every hop of the ring)
+        self.bf16_wire = self.wire_dtype == torch.bfloat16
+        if self.bf16_wire:
+            self.delta_slices = torch.zeros(self.world * self.shard_n, dtype=torch.bfloat16,
+                                            device=self.device)
+            self.master16 = torch.zeros(self.shard_n, dtype=torch.bfloat16, device=self.device)
+        else:
+            self.delta_shard = torch.zeros(self.shard_n, dtype=self.wire_dtype,
+                                           device=self.device)
         self.side = torch.cuda.Stream(self.device) if self.cuda else None
         self._pull_bufs: deque = deque()
         self._push_event = None
 
     def _apply_delta(self):
-        if self.cuda:
+        if self.bf16_wire:
+            sn = self.shard_n
+            for k in range(self.world):            # fp32 accumulation, one slice at a time
+                sl = self.delta_slices[k * sn:(k + 1) * sn]
+                if self.cuda:
+                    self.nat.ps_apply(self.master, sl, None, self.scale)
+                else:
+                    self.master.add_(sl.to(torch.float32), alpha=self.scale)
+        elif self.cuda:
             self.nat.ps_apply(self.master, self.delta_shard, None, self.scale)
         else:
             self.master.add_(self.delta_shard.to(torch.float32), alpha=self.scale)
+
+    def _exchange_deltas(self, buf, async_op: bool):
+        """Deltas of every rank for this rank's shard: reduce-scatter (fp32 wire)
+        or all-to-all of the bf16 slices (bf16 wire)."""
+        gloo = dist.get_backend(self.group) == "gloo"
+        if self.bf16_wire:
+            if gloo:
+                dist.all_to_all_single(self.delta_slices, buf, group=self.group)
+                return None
+            return dist.all_to_all_single(self.delta_slices, buf, group=self.group,
+                                          async_op=async_op)
+        if gloo:
+            self._gloo_reduce_scatter(buf)
+            return None
+        return dist.reduce_scatter_tensor(self.delta_shard, buf, group=self.group,
+                                          async_op=async_op)
 
     def push(self, step: int):
         buf = self._handoff()
@@ -523,16 +559,15 @@ class ShardedPSClient(PSClient):
             with torch.cuda.stream(self.side):
                 self.side.wait_event(ev)
                 with self._timed("push"):
-                    work = dist.reduce_scatter_tensor(self.delta_shard, buf, group=self.group,
-                                                      async_op=True)
-                    work.wait()
+                    work = self._exchange_deltas(buf, async_op=True)
+                    if work is not None:
+                        work.wait()
                     self._apply_delta()
                 done = torch.cuda.Event()
                 done.record()
             self._send_work[self._cur_slot] = _EventWork(done)
         else:
-            dist.reduce_scatter_tensor(self.delta_shard, buf, group=self.group) \
-                if dist.get_backend(self.group) != "gloo" else self._gloo_reduce_scatter(buf)
+            self._exchange_deltas(buf, async_op=False)
             self._apply_delta()
 
     def _gloo_reduce_scatter(self, buf):
@@ -544,9 +579,10 @@ class ShardedPSClient(PSClient):
 
     def request_pull(self, step: int):
         n = self.arena.numel
+        wdt = torch.bfloat16 if self.bf16_wire else torch.float32
         buf, free_ev = self._pull_bufs.popleft() if len(self._pull_bufs) > self.staleness else \
-            (torch.empty(n, dtype=torch.float32, device=self.device), None)
-        self.bytes_recv += n * 4 * (self.world - 1) // max(self.world, 1)
+            (torch.empty(n, dtype=wdt, device=self.device), None)
+        self.bytes_recv += n * buf.element_size() * (self.world - 1) // max(self.world, 1)
         if self.world == 1 and not self.force:
             buf.copy_(self.master)
             self.pending.append(_Pending(step, buf))
@@ -556,21 +592,29 @@ class ShardedPSClient(PSClient):
                 if free_ev is not None:
                     self.side.wait_event(free_ev)   # previous land kernel done reading buf
                 with self._timed("pull"):
-                    work = dist.all_gather_into_tensor(buf, self.master, group=self.group,
+                    src = self.master
+                    if self.bf16_wire:
+                        self.master16.copy_(self.master)    # RNE cast on the side stream
+                        src = self.master16
+                    work = dist.all_gather_into_tensor(buf, src, group=self.group,
                                                        async_op=True)
                     work.wait()
                 ev = torch.cuda.Event()
                 ev.record()
             self.pending.append(_Pending(step, buf, event=ev))
         else:
-            work = dist.all_gather_into_tensor(buf, self.master, group=self.group,
-                                               async_op=True) \
-                if dist.get_backend(self.group) != "gloo" else self._gloo_all_gather(buf)
+            src = self.master
+            if self.bf16_wire:
+                self.master16.copy_(self.master)
+                src = self.master16
+            work = dist.all_gather_into_tensor(buf, src, group=self.group, async_op=True) \
+                if dist.get_backend(self.group) != "gloo" else self._gloo_all_gather(buf, src)
             self.pending.append(_Pending(step, buf, work=work))
 
-    def _gloo_all_gather(self, buf):
+    def _gloo_all_gather(self, buf, src=None):
+        src = self.master if src is None else src
         chunks = list(buf.view(self.world, self.shard_n).unbind(0))
-        return dist.all_gather(chunks, self.master.contiguous(), group=self.group, async_op=True)
+        return dist.all_gather(chunks, src.contiguous(), group=self.group, async_op=True)
 
     def _land(self, pend):
         super()._land(pend)

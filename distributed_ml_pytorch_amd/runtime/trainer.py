@@ -40,7 +40,7 @@ from ..parallel.server import ParameterServer, make_ps_groups
 from ..utils import checkpoint as ckpt
 from ..utils.data import get_datasets, make_loaders
 from ..utils.metrics import IterationLog, StepTimer, Throughput, classification_report
-from .dist import DistInfo
+from .dist import DistInfo, preflight
 
 _LOG = logging.getLogger(__name__)
 
@@ -116,6 +116,12 @@ class Worker:
         # resume the parameters BEFORE the optimizer exists: its PS client seeds the
         # master (local / sharded) or the central PS from the live parameters
         resume = _worker_resume_path(cfg.resume, info.rank) if cfg.resume else None
+        if cfg.resume and info.is_distributed and not (cfg.mode == "asgd" and cfg.ps == "central"):
+            # every rank of a collective topology must take the same decision: the
+            # sharded clients restore through a collective, so one rank starting
+            # fresh while the others resume would hang them (central-PS workers
+            # resume independently: a fresh one adopts the PS params at its pull)
+            _agree_on_resume(resume is not None, info)
         if resume:
             self.step_idx = ckpt.load_worker_model(resume, self.model)
         params = list(self.model.parameters())
@@ -286,7 +292,10 @@ class Worker:
             tot_hits += hits.to(torch.int64)
             if conf is not None:
                 pred = out.float().argmax(1)
-                conf += torch.bincount(yb * c + pred, minlength=c * c)
+                # rows with an ignored / out-of-range label are skipped, as the
+                # loss kernel skips them (bincount rejects negative indices)
+                ok = (yb >= 0) & (yb < c)
+                conf += torch.bincount((yb * c + pred)[ok], minlength=c * c)
             n += yb.numel()
             nb += 1
             if max_batches and nb >= max_batches:
@@ -344,8 +353,13 @@ def run_training(cfg: TrainConfig, info: DistInfo):
     central = cfg.mode == "asgd" and cfg.ps == "central" and info.is_distributed
     if central:
         ps_groups = make_ps_groups(0, _payload(cfg, info))
-        if info.rank == 0:
-            return {"role": "ps", **run_server(cfg, info, ps_groups)}
+    # start-up checks every rank joins: ranks reached by a collective, distinct
+    # devices on RCCL, every (PS, worker) payload communicator answering
+    pf = preflight(info, None, ps_groups[1] if ps_groups else None, 0)
+    if cfg.verbose and info.rank == 0 and info.is_distributed:
+        print(f"[preflight] {pf}", flush=True)
+    if central and info.rank == 0:
+        return {"role": "ps", "preflight": pf, **run_server(cfg, info, ps_groups)}
     w = Worker(cfg, info, ps_groups)
     tr, te, source = get_datasets(cfg.dataset, cfg.data_dir, w.input_shape, w.num_classes,
                                   cfg.n_train, cfg.n_test, seed=cfg.seed)
@@ -412,7 +426,7 @@ def run_training(cfg: TrainConfig, info: DistInfo):
     log.to_csv(path)
     res = {"role": "worker", "rank": info.rank, "steps": w.step_idx, "elapsed_s": elapsed,
            "samples_per_sec": meter.rate(), "test_loss": final[0], "test_accuracy": final[1],
-           "data": source, "log": path}
+           "data": source, "log": path, "preflight": pf}
     if isinstance(w.opt, Asynchronous):
         res.update(w.opt.stats())
     res["phases"] = w.timer.summary()
@@ -423,6 +437,20 @@ def run_training(cfg: TrainConfig, info: DistInfo):
 
 def _worker_ckpt(cfg, info):
     return ckpt.worker_checkpoint_path(cfg.checkpoint, info.rank)
+
+
+def _agree_on_resume(have: bool, info: DistInfo):
+    """Collective check that every rank found (or did not find) its worker
+    checkpoint; raises on disagreement instead of hanging in the restore."""
+    dev = info.device if info.backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([1.0 if have else 0.0, 0.0 if have else 1.0], device=dev)
+    dist.all_reduce(t)
+    n_have, n_miss = int(round(float(t[0]))), int(round(float(t[1])))
+    if n_have and n_miss:
+        raise RuntimeError(
+            f"resume: {n_have} rank(s) found their worker checkpoint and {n_miss} did not "
+            f"(this is rank {info.rank}, {'found' if have else 'missing'}): the sharded / "
+            "sync topologies restore collectively; supply every <base>.worker<r>.pt or none")
 
 
 def _worker_resume_path(base: str, rank: int) -> str | None:

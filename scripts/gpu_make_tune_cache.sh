@@ -2,7 +2,7 @@
 # Build tuning/mi355x_tune_cache.json: every kernel choice of the bench configs, tuned with
 # 4 interleaved rounds x 10 reps (min per candidate), starting from an empty cache.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out tuning && export TMPDIR=/tmp
-export DMP_CONV_TUNE_CACHE=gpurun_out/mi355x_tune_cache.json DMP_CONV_TUNE_ROUNDS=4 DMP_CONV_TUNE_REPS=10
+export DMP_CONV_TUNE_SEED=: DMP_CONV_TUNE_CACHE=gpurun_out/mi355x_tune_cache.json DMP_CONV_TUNE_ROUNDS=4 DMP_CONV_TUNE_REPS=10
 rm -f $DMP_CONV_TUNE_CACHE
 OUT=gpurun_out/tune_cache.log; : > $OUT
 run() { echo "== $*" >> $OUT; timeout -k 10 400 "$@" >> $OUT 2>&1; }

@@ -43,6 +43,8 @@ def test_bench_self_spawns_n_ranks():
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 4 and out["world_size"] == 4 and out["workers"] == 4
+    assert out["preflight"] == {"ranks_observed": 4, "devices_distinct": None,
+                                "pairs_pinged": 0}
     assert out["config"]["global_batch"] == 32
     assert out["backend"] == "gloo" and out["dtype"].startswith("fp32")
     assert "sharded" in out["config"]["parallelism"]
@@ -59,7 +61,11 @@ def test_bench_central_ps_three_ranks():
     assert out["n_gpus"] == 3 and out["workers"] == 2
     assert out["config"]["global_batch"] == 16
     assert out["config"]["parallelism"] == "asgd-central-ps 1ps+2w"
-    assert out["config"]["push_combine"] == "mean"     # --delta-scale auto at N > 1
+    assert out["config"]["push_combine"] == "sum"      # the reference's Downpour PS
+    # worker-side facts on the PS's line (rank 0 trains nothing)
+    assert "push" in out["phases_host_ms"] and "compute_launch" in out["phases_host_ms"]
+    assert out["worker_hip_graph"] == [False, False]   # CPU: no graph capture
+    assert out["preflight"]["ranks_observed"] == 3 and out["rccl_ranks"] == 0
     ps = out["ps"]
     # 8 steps per worker, push/pull at idx 0,2,4,6
     assert ps["counts"] == {"ParameterUpdate": 2, "GradientUpdate": 8, "ParameterRequest": 8}

@@ -77,6 +77,29 @@ def test_native_relu():
     torch.testing.assert_close(x.grad, torch.where(x.detach() > 0, g, torch.zeros_like(g)))
 
 
+@pytest.mark.parametrize("kind", ["transposed", "offset", "nchw_strided"])
+def test_native_relu_noncontiguous_and_offset(kind):
+    """The standalone ReLU on views: a transposed (strided) input, an offset slice
+    whose data pointer is not 16-B aligned, and a strided 4-D view (relu_bwd
+    makes y dense / aligned before the 16-B vector kernel reads it)."""
+    from distributed_ml_pytorch_amd.ops import functional as DF
+
+    base = torch.randn(64, 130, device="cuda").to(torch.bfloat16)
+    if kind == "transposed":
+        x = base.t()
+    elif kind == "offset":
+        x = base.reshape(-1)[1:8001].reshape(100, 80)
+        assert x.data_ptr() % 16 != 0
+    else:
+        x = base.reshape(2, 4, 8, 130)[:, :, ::2, 1:]
+    x = x.detach().requires_grad_(True)
+    y = DF.relu(x)
+    g = torch.randn(y.shape, device="cuda").to(torch.bfloat16)
+    y.backward(g)
+    torch.testing.assert_close(y, torch.relu(x.detach()))
+    torch.testing.assert_close(x.grad, torch.where(x.detach() > 0, g, torch.zeros_like(g)))
+
+
 @pytest.mark.parametrize("name", ["lenet", "alexnet", "mlp"])
 def test_reference_models_step_matches_fp32(name):
     """One training step of the reference models through the native kernels vs
