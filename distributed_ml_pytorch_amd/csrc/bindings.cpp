@@ -1049,6 +1049,52 @@ std::vector<Tensor> layernorm_fwd(Tensor x, optional<Tensor> gamma, optional<Ten
   return {y, mean, rstd};
 }
 
+// ViT token assembly: h [B, N+1, D] = cat(cls, tok) + pos (bf16 operands)
+Tensor vit_embed_fwd(Tensor tok, Tensor cls, Tensor pos) {
+  tok = tok.contiguous();
+  check_rows_bf16(tok, "tok");
+  TORCH_CHECK(tok.dim() == 3, "vit_embed_fwd: tok must be [B, N, D]");
+  const int64_t B = tok.size(0), N = tok.size(1), D = tok.size(2);
+  TORCH_CHECK(D % 8 == 0, "vit_embed_fwd: D must be a multiple of 8");
+  cls = cls.contiguous();
+  pos = pos.contiguous();
+  check_rows_bf16(cls, "cls");
+  check_rows_bf16(pos, "pos");
+  TORCH_CHECK(cls.numel() == D && pos.numel() == (N + 1) * D, "vit_embed_fwd: cls / pos shape");
+  Tensor h = at::empty({B, N + 1, D}, tok.options());
+  dmp::launch_vit_embed_fwd(reinterpret_cast<const uint16_t*>(tok.data_ptr()),
+                            reinterpret_cast<const uint16_t*>(cls.data_ptr()),
+                            reinterpret_cast<const uint16_t*>(pos.data_ptr()),
+                            reinterpret_cast<uint16_t*>(h.data_ptr()), (int)B, (int)N, (int)D,
+                            cur_stream());
+  return h;
+}
+
+// backward: returns dtok [B, N, D] (bf16) and adds the batch sums into the fp32
+// gradients dpos [(N+1) * D] and dcls [D] in place
+Tensor vit_embed_bwd(Tensor dh, optional<Tensor> dpos, optional<Tensor> dcls, bool want_dtok) {
+  dh = dh.contiguous();
+  check_rows_bf16(dh, "dh");
+  TORCH_CHECK(dh.dim() == 3, "vit_embed_bwd: dh must be [B, N+1, D]");
+  const int64_t B = dh.size(0), N = dh.size(1) - 1, D = dh.size(2);
+  TORCH_CHECK(D % 8 == 0 && N >= 0, "vit_embed_bwd: bad shape");
+  for (auto* t : {&dpos, &dcls})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->is_contiguous() &&
+                      reinterpret_cast<uintptr_t>((*t)->data_ptr()) % 16 == 0,
+                  "vit_embed_bwd: fp32 contiguous 16-B aligned parameter gradients");
+  if (dpos.has_value() && dpos->defined())
+    TORCH_CHECK(dpos->numel() == (N + 1) * D, "vit_embed_bwd: dpos shape");
+  if (dcls.has_value() && dcls->defined()) TORCH_CHECK(dcls->numel() == D, "vit_embed_bwd: dcls shape");
+  Tensor dtok;
+  if (want_dtok) dtok = at::empty({B, N, D}, dh.options());
+  dmp::launch_vit_embed_bwd(reinterpret_cast<const uint16_t*>(dh.data_ptr()),
+                            want_dtok ? reinterpret_cast<uint16_t*>(dtok.data_ptr()) : nullptr,
+                            ptr_or_null<float>(dpos), ptr_or_null<float>(dcls), (int)B, (int)N,
+                            (int)D, cur_stream());
+  return dtok;
+}
+
 Tensor layernorm_bwd(Tensor x, Tensor dy, optional<Tensor> gamma, Tensor mean, Tensor rstd,
                      optional<Tensor> dgamma, optional<Tensor> dbeta, optional<Tensor> slots,
                      optional<Tensor> dres) {
@@ -1450,6 +1496,8 @@ PYBIND11_MODULE(_native, m) {
         py::arg("dy"), py::arg("y"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"), py::arg("slots") = py::none(),
         py::arg("mask") = py::none());
+  m.def("vit_embed_fwd", &vit_embed_fwd, "ViT token assembly cat(cls, tok) + pos");
+  m.def("vit_embed_bwd", &vit_embed_bwd, "ViT token assembly backward (dtok + fp32 batch sums)");
   m.def("layernorm_fwd", &layernorm_fwd,
         "row LayerNorm forward -> (y, mean, rstd[, h = x + residual])", py::arg("x"),
         py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("residual") = py::none());

@@ -86,6 +86,10 @@ void launch_softmax_fwd(const uint16_t* sc, uint16_t* p, long long rows, int L, 
                         hipStream_t s);
 void launch_softmax_bwd(const uint16_t* p, const uint16_t* dp, uint16_t* ds, long long rows, int L,
                         float scale, hipStream_t s);
+void launch_vit_embed_fwd(const uint16_t* tok, const uint16_t* cls, const uint16_t* pos,
+                          uint16_t* h, int B, int N, int D, hipStream_t s);
+void launch_vit_embed_bwd(const uint16_t* dh, uint16_t* dtok, float* dpos, float* dcls, int B,
+                          int N, int D, hipStream_t s);
 
 // dropout.hip: Philox4x32-10 dropout
 void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,

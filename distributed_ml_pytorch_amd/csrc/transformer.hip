@@ -429,4 +429,99 @@ void launch_softmax_bwd(const u16* p, const u16* dp, u16* ds, long long rows, in
   else hipLaunchKernelGGL((softmax_bwd_kernel<16>), grid, dim3(256), 0, s, p, dp, ds, rows, L, scale);
 }
 
+// ------------------------------------------------------- ViT token assembly
+// h[b][0] = cls + pos[0]; h[b][1 + i] = tok[b][i] + pos[1 + i]   (bf16, fp32 add)
+// One pass replaces torch.cat([cls.expand(B), tok]) + pos (a concat copy and a
+// broadcast add).  8 bf16 per thread, grid-stride over B * (N + 1) * D / 8.
+__global__ void __launch_bounds__(256) vit_embed_fwd_kernel(const u16* __restrict__ tok,
+                                                            const u16* __restrict__ cls,
+                                                            const u16* __restrict__ pos,
+                                                            u16* __restrict__ h, int B, int N,
+                                                            int D) {
+  const int dv = D / 8, T = N + 1;
+  const long long nvec = (long long)B * T * dv;
+  const long long gs = (long long)gridDim.x * blockDim.x;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gs) {
+    const int d8 = (int)(v % dv);
+    const long long bt = v / dv;
+    const int t = (int)(bt % T);
+    const int b = (int)(bt / T);
+    const bf16x8 pv = reinterpret_cast<const bf16x8*>(pos)[(long long)t * dv + d8];
+    const bf16x8 xv = t == 0 ? reinterpret_cast<const bf16x8*>(cls)[d8]
+                             : reinterpret_cast<const bf16x8*>(tok)[((long long)b * N + t - 1) * dv + d8];
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o.v[e] = f2bf(bf2f(xv.v[e]) + bf2f(pv.v[e]));
+    reinterpret_cast<bf16x8*>(h)[v] = o;
+  }
+}
+
+// Backward of the token assembly: dtok[b][i] = dh[b][1 + i] (bf16 copy), and the
+// batch sums dpos[t] += sum_b dh[b][t], dcls += sum_b dh[b][0] accumulated in
+// fp32 straight into the parameters' fp32 gradients (the flat grad arena).
+// Block = 32 chunks of 8 columns x 8 batch groups of one token row t; the batch
+// groups' partial sums meet in LDS, so every (t, column) is owned by one thread
+// at the end (plain read-add-write, no atomics).
+__global__ void __launch_bounds__(256) vit_embed_bwd_kernel(const u16* __restrict__ dh,
+                                                            u16* __restrict__ dtok,
+                                                            float* __restrict__ dpos,
+                                                            float* __restrict__ dcls, int B, int N,
+                                                            int D) {
+  __shared__ float red[8][32 * 8 + 4];
+  const int dv = D / 8, T = N + 1;
+  const int cx = threadIdx.x & 31, bg = threadIdx.x >> 5;
+  const int t = blockIdx.x;
+  const int d8 = blockIdx.y * 32 + cx;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  if (d8 < dv) {
+    for (int b = bg; b < B; b += 8) {
+      const bf16x8 g = reinterpret_cast<const bf16x8*>(dh)[((long long)b * T + t) * dv + d8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += bf2f(g.v[e]);
+      if (t > 0 && dtok != nullptr)
+        reinterpret_cast<bf16x8*>(dtok)[((long long)b * N + t - 1) * dv + d8] = g;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[bg][cx * 8 + e] = acc[e];
+  __syncthreads();
+  if (bg == 0 && d8 < dv) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += red[k][cx * 8 + e];
+    if (dpos != nullptr) {
+      float4* pp = reinterpret_cast<float4*>(dpos + (long long)t * D + d8 * 8);
+      float4 a0 = pp[0], a1 = pp[1];
+      a0.x += acc[0]; a0.y += acc[1]; a0.z += acc[2]; a0.w += acc[3];
+      a1.x += acc[4]; a1.y += acc[5]; a1.z += acc[6]; a1.w += acc[7];
+      pp[0] = a0;
+      pp[1] = a1;
+    }
+    if (t == 0 && dcls != nullptr) {
+      float4* pc = reinterpret_cast<float4*>(dcls + d8 * 8);
+      float4 a0 = pc[0], a1 = pc[1];
+      a0.x += acc[0]; a0.y += acc[1]; a0.z += acc[2]; a0.w += acc[3];
+      a1.x += acc[4]; a1.y += acc[5]; a1.z += acc[6]; a1.w += acc[7];
+      pc[0] = a0;
+      pc[1] = a1;
+    }
+  }
+}
+
+void launch_vit_embed_fwd(const u16* tok, const u16* cls, const u16* pos, u16* h, int B, int N,
+                          int D, hipStream_t s) {
+  const long long nvec = (long long)B * (N + 1) * (D / 8);
+  hipLaunchKernelGGL(vit_embed_fwd_kernel, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, tok, cls,
+                     pos, h, B, N, D);
+}
+
+void launch_vit_embed_bwd(const u16* dh, u16* dtok, float* dpos, float* dcls, int B, int N, int D,
+                          hipStream_t s) {
+  const dim3 grid((unsigned)(N + 1), (unsigned)((D / 8 + 31) / 32));
+  hipLaunchKernelGGL(vit_embed_bwd_kernel, grid, dim3(256), 0, s, dh, dtok, dpos, dcls, B, N, D);
+}
+
 }  // namespace dmp

@@ -50,7 +50,7 @@ class PatchEmbed(L.Conv2d):
 
     def forward(self, x):
         p = self.kernel_size[0]
-        if self.training and patch_embed_ok(x, self.weight, self.bias, p):
+        if patch_embed_ok(x, self.weight, self.bias, p):
             return patch_embed(x, self.weight, self.bias, p)
         return super().forward(x).flatten(2).transpose(1, 2)
 
@@ -79,7 +79,7 @@ class Block(nn.Module):
         self.fc2 = L.Linear(hidden, dim)
 
     def mlp(self, y):
-        if self.training and mlp_ok(y, self.fc1, self.fc2):
+        if mlp_ok(y, self.fc1, self.fc2):
             return mlp(y, self.fc1, self.fc2)       # GELU fused into the GEMM epilogues
         return self.fc2(DF.gelu(self.fc1(y)))
 
@@ -126,8 +126,7 @@ class VisionTransformer(nn.Module):
 
     def forward(self, x):
         h = self.patch_embed(x)                       # [B, N, D]
-        cls = compute_weight(self.cls_token, h.dtype).expand(h.shape[0], -1, -1)
-        h = torch.cat([cls, h], dim=1) + compute_weight(self.pos_embed, h.dtype)
+        h = DF.vit_embed(h, self.cls_token, self.pos_embed)   # cat(cls, h) + pos
         pending = None
         for blk in self.blocks:
             h, pending = blk.forward_fused(h, pending)

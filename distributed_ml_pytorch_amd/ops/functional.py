@@ -304,10 +304,12 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, m
         part = getattr(x, "_dmp_bn_part", None) if training else None
         return _BNAct.apply(x, weight, bias, residual, running_mean, running_var, training,
                             momentum, eps, relu, part, slots)
-    if x.is_cuda:
+    if x.is_cuda and x.dtype == torch.bfloat16:
         raise RuntimeError(
-            f"batch_norm_act: unsupported GPU input (dtype={x.dtype}, C={x.shape[1]}); "
-            "the native kernel needs bf16 with C % 8 == 0 and C <= 2048")
+            f"batch_norm_act: unsupported bf16 GPU input (C={x.shape[1]}); "
+            "the native kernel needs C % 8 == 0 and C <= 2048")
+    # CPU, or an fp32 GPU run (``--dtype fp32``: the framework's own fp32 oracle
+    # mode -- every op on PyTorch's fp32 kernels, same model / optimizer / PS)
     w = weight.to(x.dtype) if weight is not None else None
     b = bias.to(x.dtype) if bias is not None else None
     y = F.batch_norm(x, running_mean, running_var, w, b, training, momentum, eps)
@@ -559,6 +561,56 @@ def gelu(x):
     if x.is_cuda and x.dtype == torch.bfloat16 and x.numel() % 8 == 0:
         return _GELU.apply(x)
     return F.gelu(x, approximate="tanh")
+
+
+# ------------------------------------------------------- ViT token assembly
+class _VitEmbed(Function):
+    """``cat([cls.expand(B), tok], 1) + pos`` in one native pass; the backward
+    copies the token gradient and adds the batch sums into the fp32 gradients of
+    ``cls`` / ``pos`` (their arena views) -- no concat, broadcast add, expand-sum
+    or per-parameter cast kernels."""
+
+    @staticmethod
+    def forward(ctx, tok, cls, pos, cls16, pos16):
+        ctx.params = (cls, pos)
+        ctx.tok_grad = tok.requires_grad
+        return native().vit_embed_fwd(tok, cls16, pos16)
+
+    @staticmethod
+    def backward(ctx, dh):
+        cls, pos = ctx.params
+        gc, gp = _arena_grad(cls), _arena_grad(pos)
+        tmp_c = gc is None and ctx.needs_input_grad[1]
+        tmp_p = gp is None and ctx.needs_input_grad[2]
+        if tmp_c:
+            gc = torch.zeros(cls.shape, dtype=torch.float32, device=dh.device)
+        if tmp_p:
+            gp = torch.zeros(pos.shape, dtype=torch.float32, device=dh.device)
+        dtok = native().vit_embed_bwd(dh, gp if ctx.needs_input_grad[2] else None,
+                                      gc if ctx.needs_input_grad[1] else None, ctx.tok_grad)
+        if not tmp_c and ctx.needs_input_grad[1]:
+            _notify(cls)
+        if not tmp_p and ctx.needs_input_grad[2]:
+            _notify(pos)
+        return (dtok if ctx.tok_grad else None, gc.to(cls.dtype) if tmp_c else None,
+                gp.to(pos.dtype) if tmp_p else None, None, None)
+
+
+def vit_embed(tok, cls, pos):
+    """``cat([cls.expand(B, 1, D), tok], 1) + pos`` (ViT class token + position
+    embedding): native kernel pair for bf16 GPU tokens, PyTorch otherwise."""
+    if tok.is_cuda and tok.dtype == torch.bfloat16 and tok.shape[-1] % 8 == 0:
+        def shadow(p):
+            w16 = getattr(p, "_dmp_w16", None)
+            return w16 if w16 is not None and w16.dtype == tok.dtype else p.detach().to(tok.dtype)
+
+        cls16, pos16 = shadow(cls), shadow(pos)
+        if torch.is_grad_enabled() and (tok.requires_grad or cls.requires_grad
+                                        or pos.requires_grad):
+            return _VitEmbed.apply(tok, cls, pos, cls16, pos16)
+        return native().vit_embed_fwd(tok, cls16, pos16)
+    c = compute_weight(cls, tok.dtype).expand(tok.shape[0], -1, -1)
+    return torch.cat([c, tok], dim=1) + compute_weight(pos, tok.dtype)
 
 
 # ------------------------------------------------------------------ attention

@@ -302,8 +302,10 @@ class _ArenaLinear(Function):
 
 
 def arena_linear_ok(x, w, b) -> bool:
-    """The weight (and bias) live in an arena with a bf16 shadow matching ``x``."""
-    if not (x.is_cuda and x.dtype == torch.bfloat16 and torch.is_grad_enabled()):
+    """The weight (and bias) live in an arena with a bf16 shadow matching ``x``
+    (training or inference: under ``torch.no_grad()`` the forward runs the same
+    native GEMM on the shadow, without an autograd node)."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16):
         return False
     w16 = getattr(w, "_dmp_w16", None)
     if w16 is None or w16.dtype != x.dtype or not w16.is_contiguous():
@@ -311,9 +313,28 @@ def arena_linear_ok(x, w, b) -> bool:
     return b is None or getattr(b, "_dmp_w16", None) is not None
 
 
+def _infer_linear(x, w16, b16, relu=False):
+    """Forward-only ``x W^T + b`` on the native GEMM (no autograd node, no saved
+    tensors): the eval / inference path of every arena-backed Linear (the
+    reference evaluates the whole test set every log interval,
+    /root/reference/example/main.py:83-84,110-125)."""
+    N, K = w16.shape
+    x2 = _rows(x, K)
+    y = torch.empty(x2.shape[0], N, dtype=x.dtype, device=x.device)
+    gemm(0, 0, x2, w16, y, bias=b16, relu=relu)
+    return y.view(*x.shape[:-1], N)
+
+
+def _needs_graph(x, *params) -> bool:
+    return torch.is_grad_enabled() and (
+        x.requires_grad or any(p is not None and p.requires_grad for p in params))
+
+
 def linear(x, w, b, relu: bool = False):
     w16 = w._dmp_w16
     b16 = b._dmp_w16 if b is not None else None
+    if not _needs_graph(x, w, b):
+        return _infer_linear(x, w16, b16, bool(relu))
     return _ArenaLinear.apply(x, w16, b16, w, b, bool(relu))
 
 
@@ -364,6 +385,16 @@ def mlp_ok(x, fc1, fc2) -> bool:
 def mlp(x, fc1, fc2):
     """``fc2(gelu_tanh(fc1(x)))`` for two arena-backed linear layers."""
     w1, b1, w2, b2 = fc1.weight, fc1.bias, fc2.weight, fc2.bias
+    if not _needs_graph(x, w1, b1, w2, b2):
+        # inference: fc1 with the GELU epilogue (h is written but not kept), fc2
+        H, D = w1._dmp_w16.shape
+        x2 = _rows(x, D)
+        h = torch.empty(x2.shape[0], H, dtype=x.dtype, device=x.device)
+        g = torch.empty_like(h)
+        gemm(0, 1, x2, w1._dmp_w16, h, c2=g, bias=b1._dmp_w16 if b1 is not None else None)
+        del h
+        return _infer_linear(g, w2._dmp_w16, b2._dmp_w16 if b2 is not None else None).view(
+            *x.shape[:-1], w2.shape[0])
     return _ArenaMLP.apply(x, w1._dmp_w16, b1._dmp_w16 if b1 is not None else None,
                            w2._dmp_w16, b2._dmp_w16 if b2 is not None else None, w1, b1, w2, b2)
 
@@ -372,7 +403,7 @@ def mlp(x, fc1, fc2):
 def patch_embed_ok(x, w, b, patch: int) -> bool:
     """Non-overlapping ``patch`` x ``patch`` conv whose weight lives in an arena
     with a channels-last bf16 shadow: computable as one GEMM on patch rows."""
-    if not (x.is_cuda and x.dtype == torch.bfloat16 and torch.is_grad_enabled()
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and not x.requires_grad
             and x.dim() == 4 and x.shape[2] % patch == 0 and x.shape[3] % patch == 0):
         return False
     w16 = getattr(w, "_dmp_w16", None)
@@ -391,10 +422,18 @@ def patch_embed(x, w, b, patch: int):
     no dgrad GEMM.  Replaces a library conv forward + backward-weights pair."""
     B, C, H, W = x.shape
     gh, gw = H // patch, W // patch
-    xp = (x.reshape(B, C, gh, patch, gw, patch).permute(0, 2, 4, 3, 5, 1)
-          .reshape(B, gh * gw, patch * patch * C))
+    K = patch * patch * C
+    if K % 8 == 0:
+        # native patch rows (csrc/im2col.hip: stride = window, k = (kh, kw, Cin))
+        xp = native().im2col(x.contiguous(memory_format=torch.channels_last), patch, patch,
+                             patch, 0, K).view(B, gh * gw, K)
+    else:
+        xp = (x.reshape(B, C, gh, patch, gw, patch).permute(0, 2, 4, 3, 5, 1)
+              .reshape(B, gh * gw, K))
     w16 = w._dmp_w16.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
     b16 = b._dmp_w16 if b is not None else None
+    if not _needs_graph(x, w, b):
+        return _infer_linear(xp, w16, b16)
     return _ArenaLinear.apply(xp, w16, b16, w, b)
 
 

@@ -192,3 +192,28 @@ def test_rccl_sharded_ps_and_bucketed_allreduce_paths():
         assert torch.isfinite(arena.g32).all()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model", ["resnet18", "vit_tiny", "alexnet"])
+def test_fp32_gpu_mode_is_an_oracle(model):
+    """``--dtype fp32`` on the GPU: every op on PyTorch's fp32 kernels (no bf16
+    shadow), same model / optimizer / PS.  Its first-step loss and parameters
+    after a few ASGD steps track the bf16 native run within bf16 noise."""
+    runs = {}
+    for dt in ("fp32", "bf16"):
+        torch.manual_seed(0)
+        w = _worker(model, n_push=2, n_pull=2, lr=0.02, dtype=dt, seed=3)
+        assert (w.arena.w16 is None) == (dt == "fp32")
+        g = torch.Generator().manual_seed(0)
+        x = torch.randn(16, *w.input_shape, generator=g)
+        y = torch.randint(0, w.num_classes, (16,), generator=g)
+        x, y = w.prepare(x, y)
+        losses = [float(w.train_step(x, y)[0].float()) for _ in range(4)]
+        w.finish()
+        torch.cuda.synchronize()
+        runs[dt] = (losses, w.arena.p32.clone())
+    (l32, p32), (l16, p16) = runs["fp32"], runs["bf16"]
+    assert all(v == v for v in l32)
+    assert abs(l32[0] - l16[0]) < 0.05 * abs(l32[0]) + 0.02, (l32, l16)
+    rel = float((p16 - p32).norm() / p32.norm())
+    assert rel < 1e-2, rel
