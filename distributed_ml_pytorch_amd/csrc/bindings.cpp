@@ -417,7 +417,6 @@ Tensor relu_bwd(Tensor dy, Tensor y, optional<Tensor> out) {
   };
   y = y.contiguous(mf);
   dy = dy.contiguous(mf);
-  check_gpu(y, "y");
   if (!aligned(y)) y = y.clone(mf);
   if (!aligned(dy)) dy = dy.clone(mf);
   TORCH_CHECK(dy.sizes() == y.sizes() && dy.scalar_type() == at::kBFloat16, "relu_bwd: dy shape");

@@ -11,24 +11,40 @@ generalised from one PS rank to N co-located shards):
 * a :class:`ShardServer` thread per rank owns ``master[lo_r:hi_r]`` and serves
   ``GradientUpdate`` (``shard += scale * delta``, applied the moment it
   arrives, whoever sent it) and ``ParameterRequest`` (reply with a snapshot
-  and the shard version) to ANY rank's worker, using the typed header/payload
-  protocol of :mod:`.messaging` (any-source header receive, per-sender payload);
+  and the shard version) to ANY rank's worker;
 * a worker's push sends each shard owner its slice of the accumulated delta
-  (point-to-point, fire-and-forget, tracked) and applies its own slice
-  in-process; a pull requests every shard and lands, ``staleness`` steps
-  later, whatever versions the owners had when they answered.
+  and applies its own slice in-process; a pull requests every shard and lands,
+  ``staleness`` steps later, whatever versions the owners had when they
+  answered.
 
-Nothing is a collective after the initial broadcast: a slow or paused rank
-delays only the replies of its own shard (its server thread keeps serving
-while its worker computes) and never blocks another rank's push.  Traffic is
-gloo point-to-point on two dedicated groups (requests, replies); on GPUs the
-payloads are host-staged -- the option trades bandwidth for independence.
+Nothing is a collective after start-up: a slow or paused rank delays only the
+replies of its own shard (its server thread keeps serving while its worker
+computes) and never blocks another rank's push.
+
+Transport (RCCL has no any-source receive and no tags):
+
+* control -- typed headers (:mod:`.messaging`) on one gloo group, received
+  any-source by each shard server;
+* payloads -- point-to-point on dedicated 2-rank groups, ONE PER DIRECTION AND
+  KIND: ``push[s -> o]`` (worker s's delta slice to shard server o) and
+  ``reply[o -> s]`` (server o's snapshot to worker s).  Each group then carries
+  sends of one thread on one side and receives of one thread on the other, in
+  the same order on both (a header precedes its payload), so no two transfers
+  can be matched out of order and no send waits on a receive queued behind it
+  on the same communicator.  On GPUs these are RCCL communicators (xGMI): the
+  master shards are device-resident, pushes are applied with the native
+  ``ps_apply`` kernel on the server's own HIP stream as the receive completes
+  (stream-ordered, no host sync), replies are snapshots taken on that stream,
+  and pulled shards land in device staging buffers through ``pull_land`` at a
+  step boundary -- no host copy anywhere on the payload path, and the server
+  thread never blocks on the device (it only blocks, GIL released, in the gloo
+  header receive).  On CPU the same groups are gloo groups (the tests).
 """
 from __future__ import annotations
 
 import logging
 import threading
-from collections import Counter
+from collections import Counter, deque
 
 import torch
 import torch.distributed as dist
@@ -39,57 +55,176 @@ from .clients import PSClient, _Pending
 _LOG = logging.getLogger(__name__)
 
 
-class ShardServer:
-    """One rank's shard of the master, served to every rank from a thread."""
+def make_p2p_groups(world: int, backend: str):
+    """``push[(s, o)]`` and ``reply[(o, s)]`` 2-rank groups for every ordered pair
+    (every rank must call this, in the same order: torch ``new_group`` rule)."""
+    push, reply = {}, {}
+    for s in range(world):
+        for o in range(world):
+            if s == o:
+                continue
+            push[(s, o)] = dist.new_group(sorted((s, o)), backend=backend)
+            reply[(s, o)] = dist.new_group(sorted((s, o)), backend=backend)
+    return push, reply
 
-    def __init__(self, rank: int, world: int, init_shard: torch.Tensor, req_group, rep_group,
-                 scale: float = 1.0):
+
+def warm_up_p2p(rank: int, groups: dict, device):
+    """One 1-element exchange on every group, in one global order: RCCL
+    communicators are created lazily by their first operation and creation is
+    collective over the pair, so doing it here (from the main thread, all ranks
+    in the same order) keeps it out of the server threads' hot path."""
+    for (s, o), g in sorted(groups.items()):
+        if rank == s:
+            dist.send(torch.ones(1, device=device), o, group=g)
+        elif rank == o:
+            t = torch.zeros(1, device=device)
+            dist.recv(t, s, group=g)
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+class ShardServer:
+    """One rank's shard of the master, served to every rank from a thread.
+
+    ``push_groups[(sender, rank)]`` / ``reply_groups[(rank, dst)]``: the payload
+    groups this server receives pushes on / sends replies on."""
+
+    def __init__(self, rank: int, world: int, init_shard: torch.Tensor, req_group,
+                 push_groups: dict, reply_groups: dict, scale: float = 1.0):
         self.rank, self.world = rank, world
-        self.master = init_shard.detach().to(torch.float32).clone()
-        self.req, self.rep = req_group, rep_group
+        self.device = init_shard.device
+        self.cuda = self.device.type == "cuda"
+        self.stream = torch.cuda.Stream(self.device) if self.cuda else None
+        if self.cuda:
+            from ..ops._ext import native
+
+            self.nat = native()
+            # the shard is a copy of the arena made in the order of the compute stream
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.stream):
+                self.master = init_shard.detach().to(torch.float32).clone()
+        else:
+            self.master = init_shard.detach().to(torch.float32).clone()
+        self.req = req_group
+        self.push_g = push_groups
+        self.reply_g = reply_groups
         self.scale = scale
         self.lock = threading.Lock()
         self.version = 0
         self.counts: Counter = Counter()
         self.staleness: list[int] = []
-        self.tracker = M.SendTracker()
         self.error: BaseException | None = None
+        self.n = self.master.numel()
+        self._rbuf: dict = {}          # (sender, dtype) -> receive buffer
+        self._sbuf: dict = {}          # dst -> reply buffer [n + 1] fp32 (GPU)
+        self._swork: dict = {}         # dst -> in-flight reply send (GPU)
+        self.tracker = M.SendTracker()
         self.thread = threading.Thread(target=self._run, daemon=True, name=f"shard-ps-{rank}")
 
     def start(self):
         self.thread.start()
         return self
 
-    # called from the server thread (remote pushes) and the local worker
-    def apply(self, delta: torch.Tensor, base_version: int | None = None):
-        with self.lock:
-            self.master.add_(delta.to(torch.float32), alpha=self.scale)
-            if base_version is not None:
-                self.staleness.append(self.version - base_version)
-            self.version += 1
+    def _ctx(self):
+        return torch.cuda.stream(self.stream) if self.cuda else _Null()
 
-    def snapshot(self) -> tuple[torch.Tensor, int]:
+    # --------------------------------------------------------------- apply
+    def _apply_locked(self, delta: torch.Tensor, base_version: int | None):
+        if self.cuda:
+            self.nat.ps_apply(self.master, delta, None, self.scale)
+        else:
+            self.master.add_(delta.to(torch.float32), alpha=self.scale)
+        if base_version is not None:
+            self.staleness.append(self.version - base_version)
+        self.version += 1
+
+    def apply(self, delta: torch.Tensor, base_version: int | None = None):
+        """Apply a delta from the calling thread (the co-located worker's own
+        slice): on GPU ordered after the caller's current stream, run on the PS
+        stream."""
         with self.lock:
-            return self.master.clone(), self.version
+            if self.cuda:
+                self.stream.wait_stream(torch.cuda.current_stream(self.device))
+                with self._ctx():
+                    self._apply_locked(delta, base_version)
+                delta.record_stream(self.stream)
+            else:
+                self._apply_locked(delta, base_version)
+
+    def snapshot(self, out: torch.Tensor | None = None):
+        """``(copy of the shard, version, event)``: on GPU the copy is taken on the
+        PS stream after every apply enqueued so far; ``event`` marks it done."""
+        with self.lock:
+            v = self.version
+            if not self.cuda:
+                snap = self.master.clone() if out is None else out.copy_(self.master)
+                return snap, v, None
+            with self._ctx():
+                snap = self.master.clone() if out is None else out.copy_(self.master)
+                ev = torch.cuda.Event()
+                ev.record()
+            return snap, v, ev
+
+    # ---------------------------------------------------------------- serve
+    def _recv_push(self, sender: int, nelem: int, dtype, version: int):
+        if nelem != self.n:
+            raise RuntimeError(f"shard {self.rank}: rank {sender} pushed {nelem} elements, "
+                               f"the shard has {self.n}")
+        key = (sender, dtype)
+        buf = self._rbuf.get(key)
+        if buf is None:
+            buf = torch.empty(nelem, dtype=dtype, device=self.device)
+            self._rbuf[key] = buf
+        g = self.push_g[(sender, self.rank)]
+        if self.cuda:
+            with self.lock, self._ctx():
+                # the receive is ordered after the previous apply out of this
+                # buffer (torch makes the RCCL stream wait on the current = PS
+                # stream) and the apply after the receive (work.wait = a stream wait)
+                work = dist.irecv(buf, sender, group=g)
+                work.wait()
+                self._apply_locked(buf, version)
+        else:
+            dist.recv(buf, sender, group=g)
+            with self.lock:
+                self._apply_locked(buf, version)
+
+    def _reply(self, dst: int):
+        g = self.reply_g[(self.rank, dst)]
+        n = self.n
+        if self.cuda:
+            with self.lock, self._ctx():
+                prev = self._swork.pop(dst, None)
+                if prev is not None:
+                    prev.wait()           # the previous reply has left this buffer
+                buf = self._sbuf.get(dst)
+                if buf is None:
+                    buf = torch.empty(n + 1, dtype=torch.float32, device=self.device)
+                    self._sbuf[dst] = buf
+                buf[:n].copy_(self.master)
+                buf[n:].fill_(float(self.version))
+                self._swork[dst] = dist.isend(buf, dst, group=g)
+        else:
+            with self.lock:
+                out = torch.cat([self.master, torch.tensor([float(self.version)])])
+            self.tracker.add(dist.isend(out, dst, group=g), out)
 
     def _run(self):
         remaining = set(range(self.world)) - {self.rank}
-        n = self.master.numel()
         try:
             while remaining:
                 code, sender, _step, version, nelem, dtype = M.recv_header(None, self.req)
                 self.counts[code.name] += 1
                 if code == M.MessageCode.GradientUpdate:
-                    if nelem != n:
-                        raise RuntimeError(f"shard {self.rank}: rank {sender} pushed {nelem} "
-                                           f"elements, the shard has {n}")
-                    buf = torch.empty(nelem, dtype=dtype)
-                    dist.recv(buf, src=sender, group=self.req, tag=M.TAG_PAYLOAD)
-                    self.apply(buf, version)
+                    self._recv_push(sender, nelem, dtype, version)
                 elif code == M.MessageCode.ParameterRequest:
-                    snap, v = self.snapshot()
-                    out = torch.cat([snap, torch.tensor([float(v)])])
-                    self.tracker.add(dist.isend(out, sender, group=self.rep, tag=M.TAG_REPLY), out)
+                    self._reply(sender)
                 elif code == M.MessageCode.Shutdown:
                     remaining.discard(sender)
         except BaseException as e:   # surfaced by join()
@@ -98,6 +233,12 @@ class ShardServer:
     def join(self):
         self.thread.join()
         self.tracker.drain()
+        if self.cuda:
+            with self._ctx():
+                for w in self._swork.values():
+                    w.wait()
+            self._swork.clear()
+            self.stream.synchronize()
         if self.error is not None:
             raise RuntimeError(f"shard server {self.rank} failed: {self.error!r}")
 
@@ -109,19 +250,19 @@ class ShardServer:
 
 
 class _ShardedPull:
-    """Work over the per-shard replies of one pull: ``wait()`` assembles them
-    (plus the local shard's snapshot, already in place) into the flat buffer."""
+    """The per-shard replies of one pull (plus the local shard's snapshot)."""
 
-    def __init__(self, buf, parts):
-        self.buf, self.parts, self.done = buf, parts, False
-        self.versions: list[int] = []
+    def __init__(self, parts, own):
+        self.parts = parts         # [(lo, hi, rbuf [hi - lo + 1], work)]
+        self.own = own             # (lo, hi, buf, event)
+        self.done = False
 
     def wait(self):
         if not self.done:
-            for lo, hi, rbuf, work in self.parts:
-                work.wait()
-                self.buf[lo:hi].copy_(rbuf[: hi - lo])
-                self.versions.append(int(rbuf[hi - lo].item()))
+            for *_, work in self.parts:
+                work.wait()        # gloo: host wait; RCCL: the current stream waits
+            if self.own[3] is not None:
+                torch.cuda.current_stream().wait_event(self.own[3])
             self.done = True
         return True
 
@@ -149,83 +290,154 @@ class AsyncShardedPSClient(PSClient):
         # identical start everywhere, then no collective ever again
         dist.broadcast(self.arena.p32, 0, group=self.group)
         self.arena.refresh_shadow()
-        # every rank creates both groups in the same order (torch new_group rule)
+        # every rank creates every group in the same order (torch new_group rule)
         self.req = dist.new_group(list(range(self.world)), backend="gloo")
-        self.rep = dist.new_group(list(range(self.world)), backend="gloo")
         # host barriers (resume) on a group of their own: the shard servers keep an
         # any-source receive posted on `req` at all times
         self.ctl = dist.new_group(list(range(self.world)), backend="gloo")
+        backend = dist.get_backend(self.group)
+        if self.cuda and backend != "nccl":
+            raise RuntimeError("sharded_async with GPU payloads needs the RCCL ('nccl') "
+                               "backend: gloo cannot move device tensors point-to-point")
+        self.payload_backend = "rccl" if backend == "nccl" else "gloo"
+        push, reply = make_p2p_groups(self.world, backend)
+        pdev = self.device if backend == "nccl" else torch.device("cpu")
+        warm_up_p2p(self.rank, push, pdev)
+        warm_up_p2p(self.rank, reply, pdev)
+        self.push_out = {k[1]: g for k, g in push.items() if k[0] == self.rank}
+        self.reply_in = {k[0]: g for k, g in reply.items() if k[1] == self.rank}
         lo = self.rank * self.shard_n
-        init = self.arena.p32.detach()[lo: lo + self.shard_n].cpu()
-        self.server = ShardServer(self.rank, self.world, init, self.req, self.rep, scale).start()
+        self.server = ShardServer(
+            self.rank, self.world, self.arena.p32.detach()[lo: lo + self.shard_n], self.req,
+            {k: g for k, g in push.items() if k[1] == self.rank},
+            {k: g for k, g in reply.items() if k[0] == self.rank}, scale).start()
+        self._pull_free: deque = deque()      # reusable reply staging sets (+ free event)
+        self._push_work: list = [[], []]      # per hand-off slot: payload sends
+        self.side = torch.cuda.Stream(self.device) if self.cuda else None
 
     def _bounds(self, o: int):
         return o * self.shard_n, (o + 1) * self.shard_n
 
     def push(self, step: int):
+        slot = self._send_slot               # the hand-off slot _handoff fills next
+        for w in self._push_work[slot]:      # that slot's previous sends are done
+            w.wait()
+        self._push_work[slot] = []
         buf = self._handoff()
         self._resolve_versions()
-        # a private host copy: gloo reads an unbound send buffer only when the
-        # owner posts its receive, and the hand-off slot is refilled two pushes on
-        host = buf.detach().to("cpu", copy=True)
         for o in range(self.world):
             lo, hi = self._bounds(o)
             if o == self.rank:
-                self.server.apply(host[lo:hi], self.version)
-            else:
-                M.send_message(M.MessageCode.GradientUpdate, host[lo:hi], o, step=step,
-                               version=self.version, group=self.req)
+                self.server.apply(buf[lo:hi], self.version)
+                continue
+            header = M.make_header(M.MessageCode.GradientUpdate, self.rank, step, self.version,
+                                   hi - lo, buf.dtype)
+            M.SENDS.add(dist.isend(header, o, group=self.req, tag=M.TAG_HEADER), header)
+            # RCCL: ordered after the hand-off kernel on the compute stream
+            w = dist.isend(buf[lo:hi], o, group=self.push_out[o])
+            self._push_work[slot].append(w if self.cuda else M.OnceWork(w))
         self.pushes += 1
-        self.bytes_sent += host.numel() * host.element_size() * (self.world - 1) // self.world
+        self.bytes_sent += buf.numel() * buf.element_size() * (self.world - 1) // self.world
 
     def request_pull(self, step: int):
-        n = self.arena.numel
-        buf = torch.empty(n, dtype=torch.float32)
+        sn = self.shard_n
+        free = self._pull_free.popleft() if len(self._pull_free) > self.staleness else None
+        if free is None:
+            bufs = {o: torch.empty(sn + (0 if o == self.rank else 1), dtype=torch.float32,
+                                   device=self.device) for o in range(self.world)}
+            free_ev = None
+        else:
+            bufs, free_ev = free
         parts = []
-        for o in range(self.world):
-            lo, hi = self._bounds(o)
-            if o == self.rank:
-                snap, _ = self.server.snapshot()
-                buf[lo:hi].copy_(snap)
-                continue
-            M.send_message(M.MessageCode.ParameterRequest, None, o, step=step, group=self.req)
-            rbuf = torch.empty(hi - lo + 1, dtype=torch.float32)
-            work = M.OnceWork(dist.irecv(rbuf, o, group=self.rep, tag=M.TAG_REPLY))
-            parts.append((lo, hi, rbuf, work))
-        self.pending.append(_Pending(step, buf, work=_ShardedPull(buf, parts)))
-        self.bytes_recv += n * 4 * (self.world - 1) // self.world
+        with (torch.cuda.stream(self.side) if self.cuda else _Null()):
+            if free_ev is not None:
+                self.side.wait_event(free_ev)        # the last land read these buffers
+            for o in range(self.world):
+                if o == self.rank:
+                    continue
+                lo, hi = self._bounds(o)
+                header = M.make_header(M.MessageCode.ParameterRequest, self.rank, step, 0, 0)
+                M.SENDS.add(dist.isend(header, o, group=self.req, tag=M.TAG_HEADER), header)
+                work = dist.irecv(bufs[o], o, group=self.reply_in[o])
+                parts.append((lo, hi, bufs[o], work if self.cuda else M.OnceWork(work)))
+        lo, hi = self._bounds(self.rank)
+        if self.cuda and free_ev is not None:
+            self.server.stream.wait_event(free_ev)
+        _, _, ev = self.server.snapshot(bufs[self.rank])
+        self.pending.append(_Pending(step, bufs, work=_ShardedPull(parts,
+                                                                   (lo, hi, bufs[self.rank], ev))))
+        self.bytes_recv += self.arena.numel * 4 * (self.world - 1) // self.world
 
     def _land(self, pend):
-        pend.work.wait()
-        self.shard_versions = pend.work.versions
-        if pend.work.versions:
-            self.version = max(self.version, min(pend.work.versions))
-        pend.work = None
+        if self.debug_landing and self.in_compute:
+            raise RuntimeError(
+                f"pull of step {pend.step} landed inside a training step (between zero_grad "
+                "and local_step): parameters would change under forward/backward")
+        pull = pend.work
+        pull.wait()
+        arena = self.arena
+        acc = self.opt.acc if self.pull_mode == "rebase" else None
+        pieces = [(lo, hi, rbuf[: hi - lo]) for lo, hi, rbuf, _ in pull.parts]
+        lo, hi, own, _ = pull.own
+        pieces.append((lo, hi, own))
+        with torch.no_grad():
+            for lo, hi, src in pieces:
+                if self.cuda:
+                    self.nat.pull_land(arena.p32[lo:hi], src,
+                                       acc[lo:hi] if acc is not None else None,
+                                       arena.w16[lo:hi] if arena.w16 is not None else None)
+                else:
+                    arena.p32[lo:hi].copy_(src)
+                    if acc is not None:
+                        arena.p32[lo:hi].add_(acc[lo:hi])
+            if not self.cuda and arena.w16 is not None:
+                arena.w16.copy_(arena.p32)
+        vsrcs = [rbuf[hi - lo:] for lo, hi, rbuf, _ in pull.parts]
         if self.cuda:
-            pend.buf = pend.buf.to(self.device, non_blocking=False)
-        super()._land(pend)
+            for v in vsrcs:
+                self._note_version(v)
+            ev = torch.cuda.Event()
+            ev.record()            # the staging set is free once the land kernels ran
+        else:
+            self.shard_versions = [int(v.item()) for v in vsrcs]
+            if self.shard_versions:
+                self.version = max(self.version, min(self.shard_versions))
+            ev = None
+        self.pulls += 1
+        arena.bump()
+        self._pull_free.append((pend.buf, ev))
 
     def finish(self):
         super().finish()                       # lands every requested pull
+        for lst in self._push_work:
+            for w in lst:
+                w.wait()
         for o in range(self.world):
             if o != self.rank:
                 M.send_message(M.MessageCode.Shutdown, None, o, group=self.req)
         M.SENDS.drain()
         self.server.join()                     # returns once every rank has shut down
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.server.stream)
 
     def stats(self) -> dict:
         st = super().stats()
         st.update(self.server.stats())
+        st["payload"] = self.payload_backend
         return st
 
     @property
     def master(self) -> torch.Tensor:
+        if self.cuda:
+            self.server.stream.synchronize()
         return self.server.master
 
     def state_dict(self) -> dict:
-        snap, v = self.server.snapshot()
+        snap, v, ev = self.server.snapshot()
+        if ev is not None:
+            ev.synchronize()
         return {"kind": "sharded_async", "rank": self.rank, "world": self.world,
-                "master": snap, "shard_version": v}
+                "master": snap.detach().cpu(), "shard_version": v}
 
     def load_state_dict(self, sd: dict):
         if sd.get("kind") != "sharded_async":
@@ -234,8 +446,11 @@ class AsyncShardedPSClient(PSClient):
             raise ValueError(f"sharded PS checkpoint is for rank {sd['rank']}/{sd['world']}, "
                              f"this is rank {self.rank}/{self.world}")
         with self.server.lock:
-            self.server.master.copy_(sd["master"])
+            with self.server._ctx():
+                self.server.master.copy_(sd["master"].to(self.server.device))
             self.server.version = int(sd.get("shard_version", 0))
+        if self.cuda:
+            self.server.stream.synchronize()
         # every shard restored before anyone asks for it: without this barrier a
         # fast rank's forced pull could be answered with a peer's pre-restore shard
         dist.barrier(group=self.ctl)

@@ -7,7 +7,9 @@ import sys
 
 LIB = ("Cijk_", "miopen", "MIOpen", "igemm_", "naive_conv", "gridwise_")
 ATEN = "at::native::"
-BENIGN = ("FillFunctor", "copy_kernel", "direct_copy", "CatArrayBatchedCopy", "rocclr_copyBuffer")
+# fills / copies, and the random input generation of the driver script itself
+BENIGN = ("FillFunctor", "copy_kernel", "direct_copy", "CatArrayBatchedCopy", "rocclr_copyBuffer",
+          "distribution_elementwise")
 
 
 def main(path):
@@ -18,7 +20,7 @@ def main(path):
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
         n = r["Name"]
         tag = ""
-        if any(k in n for k in LIB):
+        if "dmp::" not in n and any(k in n for k in LIB):
             lib.append(n)
             tag = "  <-- LIBRARY"
         elif ATEN in n and not any(k in n for k in BENIGN):

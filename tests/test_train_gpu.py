@@ -217,3 +217,52 @@ def test_fp32_gpu_mode_is_an_oracle(model):
     assert abs(l32[0] - l16[0]) < 0.05 * abs(l32[0]) + 0.02, (l32, l16)
     rel = float((p16 - p32).norm() / p32.norm())
     assert rel < 1e-2, rel
+
+
+def test_rccl_world1_device_async_shards_and_bf16_wire():
+    """World-size-1 NCCL group: the non-lock-step sharded PS runs its GPU
+    transport (device-resident shard, PS-stream apply / snapshot, per-slice
+    pull landing) and the collective sharded PS its bf16 wire (all-to-all of
+    bf16 slices + fp32 apply); both track the in-process PS run."""
+    import torch.distributed as dist
+
+    from distributed_ml_pytorch_amd.models import build_model
+    from distributed_ml_pytorch_amd.ops.functional import softmax_cross_entropy
+    from distributed_ml_pytorch_amd.parallel.asgd import Asynchronous
+    from distributed_ml_pytorch_amd.parallel.async_sharded import AsyncShardedPSClient
+    from distributed_ml_pytorch_amd.parallel.clients import LocalPSClient, ShardedPSClient
+
+    _nccl_world1()
+    try:
+        g = torch.Generator().manual_seed(5)
+        xs = [torch.randn(16, 3, 32, 32, generator=g) for _ in range(6)]
+        ys = [torch.randint(0, 10, (16,), generator=g) for _ in range(6)]
+        finals = {}
+        for kind in ("local", "async", "sharded_bf16"):
+            torch.manual_seed(0)
+            m, _, _ = build_model("resnet18")
+            m = m.cuda()
+            client = {"local": lambda: LocalPSClient(staleness=1),
+                      "async": lambda: AsyncShardedPSClient(staleness=1),
+                      "sharded_bf16": lambda: ShardedPSClient(
+                          staleness=1, force_collectives=True, wire_dtype=torch.bfloat16)}[kind]()
+            opt = Asynchronous(m.parameters(), lr=0.05, n_push=2, n_pull=2, model=m,
+                               client=client)
+            for x, y in zip(xs, ys):
+                x = x.cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                opt.zero_grad()
+                loss, _ = softmax_cross_entropy(m(x), y.cuda())
+                loss.backward()
+                opt.step()
+            opt.finish()
+            torch.cuda.synchronize()
+            finals[kind] = (opt.arena.p32.clone(), opt.stats())
+        ref = finals["local"][0]
+        for kind in ("async", "sharded_bf16"):
+            rel = float((finals[kind][0] - ref).norm() / ref.norm())
+            assert rel < 1e-2, (kind, rel)
+        st = finals["async"][1]
+        assert st["pushes"] == 3 and st["pulls"] == 3 and st["shard_version"] == 3
+        assert st["payload"] == "rccl"
+    finally:
+        dist.destroy_process_group()
