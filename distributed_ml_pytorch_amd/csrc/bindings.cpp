@@ -1196,8 +1196,9 @@ std::vector<Tensor> dropout_fwd(Tensor x, double p, int64_t seed, Tensor offset,
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat,
               "dropout: bf16 or fp32 input");
   TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout: p must be in [0, 1)");
-  TORCH_CHECK(offset.is_cuda() && offset.scalar_type() == at::kLong && offset.numel() >= 1,
-              "dropout: offset must be an int64 GPU tensor");
+  TORCH_CHECK(offset.is_cuda() && offset.scalar_type() == at::kLong && offset.numel() >= 2 &&
+                  offset.is_contiguous(),
+              "dropout: offset must be an int64 GPU tensor [offset, ticket] (zeros at creation)");
   TORCH_CHECK(mode >= 0 && mode <= 2, "dropout: bad mode");
   long long inner = 1, nmask = x.numel();
   int C = 1;
@@ -1218,16 +1219,12 @@ std::vector<Tensor> dropout_fwd(Tensor x, double p, int64_t seed, Tensor offset,
   }
   auto mask = at::empty({nmask}, x.options().dtype(at::kByte));
   auto y = at::empty_like(x);
-  const float scale = (float)(1.0 / (1.0 - p));
-  dmp::launch_dropout_mask(mask.data_ptr<uint8_t>(), nmask, (float)p, (unsigned long long)seed,
-                           reinterpret_cast<const long long*>(offset.data_ptr<int64_t>()), cur_stream());
-  if (x.scalar_type() == at::kBFloat16)
-    dmp::launch_dropout_apply_bf16(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                                   mask.data_ptr<uint8_t>(), reinterpret_cast<uint16_t*>(y.data_ptr()),
-                                   x.numel(), scale, (int)mode, inner, C, cur_stream());
-  else
-    dmp::launch_dropout_apply_f32(x.data_ptr<float>(), mask.data_ptr<uint8_t>(), y.data_ptr<float>(),
-                                  x.numel(), scale, (int)mode, inner, C, cur_stream());
+  // one launch: draw + mask + scaled product; it advances offset[0] itself
+  dmp::launch_dropout_fwd_fused(x.data_ptr(), mask.data_ptr<uint8_t>(), y.data_ptr(),
+                                x.scalar_type() == at::kBFloat16, x.numel(), (float)p, (int)mode,
+                                inner, C, (unsigned long long)seed,
+                                reinterpret_cast<long long*>(offset.data_ptr<int64_t>()),
+                                cur_stream());
   return {y, mask};
 }
 

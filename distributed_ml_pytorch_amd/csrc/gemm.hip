@@ -585,6 +585,74 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------- skinny weight gradient
+// C[M][N] (fp32, ldc) += sum_k A(k, m) B(k, n), A = [K][lda], B = [K][ldb] (both
+// k-strided), for a SMALL output (M*N <= kSkinnyMaxOut: the LeNet / CIFAR-stem
+// convs' weight gradients over B*OH*OW patch rows, 6 x 75 over 50,176 rows) and
+// a LONG reduction.  The 64x64-tile fallback above spends 89 % of its MACs on
+// padding there and walks 32-row stages with one scalar load per element per
+// stage (~27 us per LeNet conv1 wgrad); here every block reduces TR-row tiles
+// of ITS chunk of k into all M*N outputs held in registers (an output per
+// thread and pass), each tile staged once into LDS as fp32 by all 256 threads,
+// and the block's partial sums leave through one fp32 atomic per output (and
+// per dbias row).  Blocks = enough chunks to cover every CU a few times.
+constexpr int kSkinnyMaxOut = 4096, kSkinnyTR = 32;
+
+__global__ void __launch_bounds__(256) gemm_skinny_wgrad_kernel(GemmArgs g, int chunk) {
+  constexpr int OPT = kSkinnyMaxOut / 256;                // outputs per thread (max)
+  extern __shared__ float sk_lds[];                       // [TR][M] A, then [TR][N] B
+  const int M = g.M, N = g.N;
+  float* As = sk_lds;
+  float* Bs = sk_lds + kSkinnyTR * M;
+  const int tid = threadIdx.x;
+  const int k0 = blockIdx.x * chunk;
+  const int k1 = min(g.K, k0 + chunk);
+  if (k0 >= k1) return;
+  const int MN = M * N;
+  float acc[OPT];
+  float bsum = 0.f;                                       // dbias row sums (tid < M)
+#pragma unroll
+  for (int q = 0; q < OPT; ++q) acc[q] = 0.f;
+  for (int kt = k0; kt < k1; kt += kSkinnyTR) {
+    const int rows = min(kSkinnyTR, k1 - kt);
+    __syncthreads();                                      // previous tile consumed
+    for (int e = tid; e < kSkinnyTR * M; e += 256) {
+      const int r = e / M, m = e - r * M;
+      As[e] = r < rows ? bf2f(g.a[(long long)(kt + r) * g.lda + m]) : 0.f;
+    }
+    for (int e = tid; e < kSkinnyTR * N; e += 256) {
+      const int r = e / N, n = e - r * N;
+      Bs[e] = r < rows ? bf2f(g.b[(long long)(kt + r) * g.ldb + n]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < OPT; ++q) {
+      const int o = tid + 256 * q;
+      if (o < MN) {
+        const int m = o / N, n = o - m * N;
+        float t = acc[q];
+#pragma unroll 8
+        for (int r = 0; r < kSkinnyTR; ++r) t = fmaf(As[r * M + m], Bs[r * N + n], t);
+        acc[q] = t;
+      }
+    }
+    if (g.dbias != nullptr && tid < M) {
+#pragma unroll 8
+      for (int r = 0; r < kSkinnyTR; ++r) bsum += As[r * M + tid];
+    }
+  }
+  float* C = reinterpret_cast<float*>(g.c);
+#pragma unroll
+  for (int q = 0; q < OPT; ++q) {
+    const int o = tid + 256 * q;
+    if (o < MN) {
+      const int m = o / N, n = o - m * N;
+      atomicAdd(C + (long long)m * g.ldc + n, acc[q]);
+    }
+  }
+  if (g.dbias != nullptr && tid < M) atomicAdd(g.dbias + tid, bsum);
+}
+
 // C[m][n] (ldc) += sum over the splits of slab[s][m][n]; 4 columns per thread
 // when rows are whole float4s
 __global__ void __launch_bounds__(256) gemm_slab_reduce_kernel(const float* __restrict__ slab,
@@ -684,6 +752,7 @@ int gemm_num_configs() { return kNumCfgs; }
 
 bool gemm_config_ok(int mode, int cfg) {
   if (cfg == -1) return true;
+  if (cfg == -2) return mode == 2;   // skinny weight gradient
   if (cfg < 0 || cfg >= kNumCfgs) return false;
   return cfg_ok(kCfgs[cfg], mode == 2, mode >= 1);
 }
@@ -717,6 +786,16 @@ void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const u
   } else if (mode == 1) {
     if (epi == EPI_DGELU) launch_mode<false, true, EPI_DGELU>(cfg, g, 1, s);
     else launch_mode<false, true, EPI_STORE>(cfg, g, 1, s);
+  } else if (cfg == -2) {
+    if ((long long)M * N > kSkinnyMaxOut || M > 256 || N > 1024)
+      throw std::runtime_error("gemm: skinny wgrad needs M*N <= 4096 (M <= 256, N <= 1024)");
+    // ~1024 blocks over the reduction, whole TR-row tiles per chunk
+    int chunk = (K + 1023) / 1024;
+    chunk = std::max(kSkinnyTR, (chunk + kSkinnyTR - 1) / kSkinnyTR * kSkinnyTR);
+    const int blocks = (K + chunk - 1) / chunk;
+    const size_t lds = (size_t)kSkinnyTR * (M + N) * sizeof(float);
+    hipLaunchKernelGGL(gemm_skinny_wgrad_kernel, dim3((unsigned)blocks), dim3(256), lds, s, g,
+                       chunk);
   } else {
     // slab split-K only for the MFMA tiles with more than one split
     if (slab != nullptr && splits > 1 && cfg >= 0) g.slab = slab;

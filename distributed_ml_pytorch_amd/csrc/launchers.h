@@ -92,6 +92,9 @@ void launch_vit_embed_bwd(const uint16_t* dh, uint16_t* dtok, float* dpos, float
                           int N, int D, hipStream_t s);
 
 // dropout.hip: Philox4x32-10 dropout
+void launch_dropout_fwd_fused(const void* x, uint8_t* mask, void* y, bool bf16, long long n,
+                              float p, int mode, long long inner, int C, unsigned long long seed,
+                              long long* ctr, hipStream_t s);
 void launch_dropout_mask(uint8_t* mask, long long nmask, float p, unsigned long long seed,
                          const long long* offset, hipStream_t s);
 void launch_dropout_apply_bf16(const uint16_t* x, const uint8_t* mask, uint16_t* y, long long n,

@@ -76,6 +76,27 @@ def compute_weight(p: torch.Tensor | None, dtype: torch.dtype):
 
 
 # --------------------------------------------------------------- cross entropy
+_UNIT = {}          # device -> persistent fp32 scalar 1.0 (the loss's seed gradient)
+
+
+def unit_grad(like: torch.Tensor) -> torch.Tensor:
+    """A persistent ``1.0`` to seed ``loss.backward(unit_grad(loss))`` with: the
+    cross-entropy backward recognises it (by storage) and hands back its
+    precomputed dlogits untouched -- no ones-fill, cast and multiply kernels per
+    step (autograd's default seed is a fresh ``ones_like``)."""
+    key = (like.device, like.dtype)
+    u = _UNIT.get(key)
+    if u is None:
+        u = torch.ones((), dtype=like.dtype, device=like.device)
+        _UNIT[key] = u
+    return u
+
+
+def _is_unit(g) -> bool:
+    u = _UNIT.get((g.device, g.dtype))
+    return u is not None and g.data_ptr() == u.data_ptr() and g.dim() == 0
+
+
 class _SoftmaxXent(Function):
     @staticmethod
     def forward(ctx, logits, labels, smoothing, ignore_index):
@@ -91,6 +112,8 @@ class _SoftmaxXent(Function):
         (dlogits,) = ctx.saved_tensors
         if gloss is None:
             return None, None, None, None
+        if _is_unit(gloss):
+            return dlogits, None, None, None
         return dlogits * gloss.to(dlogits.dtype), None, None, None
 
 
@@ -393,10 +416,9 @@ def relu(x):
 class _Dropout(Function):
     @staticmethod
     def forward(ctx, x, p, seed, offset, mode):
+        # the kernel advances the layer's device-side Philox offset itself (last
+        # block, arrival ticket): a captured hipGraph replay draws a fresh mask
         y, mask = native().dropout_fwd(x, float(p), int(seed), offset, int(mode))
-        # advance the layer's device-side Philox offset in-stream: a captured
-        # hipGraph replays this add, so every replay draws a fresh mask
-        offset.add_(1)
         ctx.save_for_backward(mask)
         ctx.p, ctx.mode = p, mode
         return y
@@ -411,7 +433,7 @@ def dropout(x, p: float, training: bool, channelwise: bool = False, state=None, 
     """Dropout (``channelwise``: Dropout2d, one draw per (n, c) plane).
 
     GPU: Philox4x32-10 kernel (``csrc/dropout.hip``) keyed by ``seed`` and the
-    device int64 counter ``state`` (advanced in-stream after each call).
+    device int64 ``state`` = [offset, ticket] (the kernel advances the offset).
     Reference: ``nn.Dropout2d`` / ``F.dropout`` in LeNet
     (/root/reference/example/models.py:10,17,20).
     """

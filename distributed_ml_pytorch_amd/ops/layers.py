@@ -161,7 +161,8 @@ class _DropoutBase(nn.Module):
         state = None
         if x.is_cuda:
             if self._state is None or self._state.device != x.device:
-                self._state = torch.zeros(1, dtype=torch.int64, device=x.device)
+                # [Philox offset, arrival ticket of the launch advancing it]
+                self._state = torch.zeros(2, dtype=torch.int64, device=x.device)
             state = self._state
         return DF.dropout(x, self.p, self.training, self.channelwise, state, self.seed)
 

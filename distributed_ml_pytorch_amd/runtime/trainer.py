@@ -30,7 +30,7 @@ import torch
 import torch.distributed as dist
 
 from ..models import build_model
-from ..ops.functional import softmax_cross_entropy
+from ..ops.functional import softmax_cross_entropy, unit_grad
 from ..parallel.arena import attach_arena
 from ..parallel.asgd import Asynchronous
 from ..parallel.async_sharded import AsyncShardedPSClient
@@ -199,7 +199,7 @@ class Worker:
         self.opt.zero_grad()
         logits = self.model(self._gx)
         loss, hits = softmax_cross_entropy(logits, self._gy, self.cfg.label_smoothing)
-        loss.backward()
+        loss.backward(unit_grad(loss))
         if self.ddp is not None:
             self.ddp.synchronize()
         self.opt.local_step()
@@ -254,7 +254,7 @@ class Worker:
             self.opt.zero_grad()
             logits = self.model(x)
             loss, hits = softmax_cross_entropy(logits, y, self.cfg.label_smoothing)
-            loss.backward()
+            loss.backward(unit_grad(loss))
         if self.ddp is not None:
             with self.timer.time("allreduce_wait"):
                 self.ddp.synchronize()

@@ -300,6 +300,8 @@ def test_dropout_kernel(mode, dtype):
     # the device offset advances: a second call draws a different mask
     y2 = layer(x.detach())
     assert not torch.equal(y2 != 0, y != 0)
+    # the fused kernel advanced its own offset (last block) and reset the ticket
+    assert layer._state.tolist() == [2, 0]
     layer.eval()
     assert layer(x) is x
 
