@@ -505,6 +505,28 @@ void conv_weight_transpose_batched(Tensor src, Tensor dst, Tensor table, int64_t
                                             cur_stream());
 }
 
+void pad_rows_batched(Tensor src, Tensor dst, Tensor table, int64_t max_elems) {
+  check_gpu(src, "src");
+  check_gpu(dst, "dst");
+  TORCH_CHECK(src.scalar_type() == at::kBFloat16 && dst.scalar_type() == at::kBFloat16,
+              "pad_rows_batched: bf16 buffers");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.dim() == 2 &&
+                  table.size(1) == 5 && table.is_contiguous(),
+              "pad_rows_batched: table must be a [n, 5] int64 GPU tensor");
+  dmp::launch_pad_rows_batched(reinterpret_cast<const uint16_t*>(src.data_ptr()),
+                               reinterpret_cast<uint16_t*>(dst.data_ptr()),
+                               reinterpret_cast<const long long*>(table.data_ptr()),
+                               (int)table.size(0), (long long)max_elems, cur_stream());
+}
+
+// hipMemsetAsync zero of a dense tensor (graph-capturable memset node; the grad
+// arena zeroing every step: no ATen fill kernel)
+void zero_(Tensor t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_: a contiguous GPU tensor");
+  TORCH_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream()) ==
+                  hipSuccess, "zero_: hipMemsetAsync failed");
+}
+
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
                   int64_t cfg, optional<Tensor> wt_pre, optional<Tensor> addend,
                   optional<Tensor> bn_x, optional<Tensor> bn_mask, optional<Tensor> bn_stats,
@@ -1441,6 +1463,8 @@ PYBIND11_MODULE(_native, m) {
         "BN backward from conv-dgrad-epilogue partials (dz already ReLU-masked)", py::arg("x"),
         py::arg("dz"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"),
         py::arg("part"));
+  m.def("pad_rows_batched", &pad_rows_batched, "padded-row copies of im2col conv weights");
+  m.def("zero_", &zero_, "hipMemsetAsync zero of a dense GPU tensor");
   m.def("conv_weight_transpose_batched", &conv_weight_transpose_batched,
         "transpose every conv weight of a flat bf16 shadow in one launch");
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient (fp32 accumulate)",

@@ -11,6 +11,8 @@
 // multiple of 8) so every GEMM operand row is whole 16-B pieces.
 #include "common.h"
 
+#include <algorithm>
+
 namespace dmp {
 
 // one lane = 8 consecutive k of one row m (one 16-B store); the (r, s, ci)
@@ -118,6 +120,31 @@ void launch_col2im(const u16* dcols, u16* dx, int B, int H, int W, int CI, int O
 void launch_relu_bwd(const u16* dy, const u16* y, u16* dx, long long n, hipStream_t st) {
   hipLaunchKernelGGL(relu_bwd_kernel, dim3(stream_grid((n + 7) / 8, 256)), dim3(256), 0, st, dy, y,
                      dx, n);
+}
+
+// All padded-row weight copies of a model in ONE launch: table[i] = {src_off,
+// dst_off, rows, K, Kp}; dst[dst_off + r*Kp + k] = src[src_off + r*K + k] for
+// k < K (the pad columns were zeroed once at allocation and are never
+// written).  The im2col GEMMs read a conv weight [CO][R*S*CI] whose row length
+// is not a multiple of 8 (LeNet: 75 / 150) from this padded image.
+__global__ void __launch_bounds__(256) pad_rows_batched_kernel(const u16* __restrict__ src,
+                                                               u16* __restrict__ dst,
+                                                               const long long* __restrict__ tab) {
+  const long long* t = tab + 5 * blockIdx.y;
+  const long long so = t[0], d_o = t[1], rows = t[2], K = t[3], Kp = t[4];
+  const long long n = rows * K;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long r = e / K, k = e - r * K;
+    dst[d_o + r * Kp + k] = src[so + e];
+  }
+}
+
+void launch_pad_rows_batched(const u16* src, u16* dst, const long long* table, int n,
+                             long long max_elems, hipStream_t st) {
+  if (n <= 0) return;
+  const dim3 grid((unsigned)std::min<long long>((max_elems + 255) / 256, 64), (unsigned)n);
+  hipLaunchKernelGGL(pad_rows_batched_kernel, grid, dim3(256), 0, st, src, dst, table);
 }
 
 }  // namespace dmp

@@ -215,6 +215,8 @@ void launch_im2col(const uint16_t* x, uint16_t* cols, int B, int H, int W, int C
                    int R, int S, int stride, int pad, int K, int Kp, hipStream_t st);
 void launch_col2im(const uint16_t* dcols, uint16_t* dx, int B, int H, int W, int CI, int OH,
                    int OW, int R, int S, int stride, int pad, int Kp, hipStream_t st);
+void launch_pad_rows_batched(const uint16_t* src, uint16_t* dst, const long long* table, int n,
+                             long long max_elems, hipStream_t st);
 void launch_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long long n,
                      hipStream_t st);
 

@@ -119,6 +119,7 @@ def _wgrad_candidates(K: int, CO: int | None = None):
 
 
 _HALO_ENABLED = os.environ.get("DMP_CONV_HALO", "1") != "0"
+_WH_BASE = 1000     # csrc/conv_wgrad.hip kWhBase: halo wgrad cfg ids start here
 
 
 def _halo_candidates(H, W, C, R, S, stride, pad):
@@ -344,9 +345,20 @@ class _NativeConv(Function):
                 # miss the added gradient) so the BN backward redoes its reduce
                 link.fused = (link.fused[0], -1)
         gw = None
+        bias = ctx.bias
+        # a conv bias gradient (AlexNet) summed by the gather wgrad kernel from the
+        # dY tiles it already stages (no separate column-sum launches)
+        bias_in_wgrad = False
         if master is not None and master.requires_grad:
             wcfg = _wgrad_cfg(dy, x, tuple(master.shape), stride, pad)
             g = master.grad if getattr(master, "_dmp_arena", False) else None
+            bias_in_wgrad = (bias is not None and bias.requires_grad and wcfg < _WH_BASE
+                             and wcfg != _GEMM_ROUTE and getattr(bias, "_dmp_arena", False)
+                             and bias.grad is not None and bias.grad.is_contiguous()
+                             and bias.grad.dtype == torch.float32
+                             and g is not None and g.is_contiguous(
+                                 memory_format=torch.channels_last)
+                             and getattr(master, "_dmp_grad_ready", None) is None)
             if wcfg == _GEMM_ROUTE:
                 gg = g if g is not None and g.is_contiguous(
                     memory_format=torch.channels_last) else None
@@ -363,6 +375,8 @@ class _NativeConv(Function):
                         _gemm1x1_wgrad(dy, x, gg)
                         if cb is not None:
                             cb(master)
+            elif bias_in_wgrad:
+                native().conv_wgrad(dy, x, g, stride, pad, wcfg, bias.grad)
             elif g is not None and g.is_contiguous(memory_format=torch.channels_last):
                 cb = getattr(master, "_dmp_grad_ready", None)
                 if cb is None and _WG_STREAM_ENABLED:
@@ -378,8 +392,7 @@ class _NativeConv(Function):
                 native().conv_wgrad(dy, x, gw, stride, pad, wcfg)
                 gw = gw.to(master.dtype)
         gb = None
-        bias = ctx.bias
-        if bias is not None and bias.requires_grad:
+        if bias is not None and bias.requires_grad and not bias_in_wgrad:
             if (getattr(bias, "_dmp_arena", False) and bias.grad is not None
                     and dy.shape[1] % 8 == 0):
                 from .linear import bias_grad_acc
@@ -416,11 +429,19 @@ class _Im2colConv(Function):
         Kp = _ceil8(K)
         cols = native().im2col(x, R, S, stride, pad, Kp)
         wmat = w16.permute(0, 2, 3, 1).reshape(CO, K)       # channels_last: [CO][R][S][CI]
+        wp = wmat
         if Kp != K:
-            wp = torch.zeros(CO, Kp, dtype=w16.dtype, device=w16.device)
-            wp[:, :K] = wmat
-        else:
-            wp = wmat
+            # the arena's batched padded-row image (one launch per step for every
+            # such layer), else a one-off padded copy
+            ref = getattr(master, "_dmp_arena_ref", None)
+            arena = ref() if ref is not None else None
+            shadow = getattr(master, "_dmp_w16", None)
+            wp = None
+            if arena is not None and shadow is not None and shadow.data_ptr() == w16.data_ptr():
+                wp = arena.padded_rows_shadow(master, Kp)
+            if wp is None:
+                wp = torch.zeros(CO, Kp, dtype=w16.dtype, device=w16.device)
+                wp[:, :K] = wmat
         OH = (H + 2 * pad - R) // stride + 1
         OW = (W + 2 * pad - S) // stride + 1
         y2 = torch.empty(B * OH * OW, CO, dtype=x.dtype, device=x.device)

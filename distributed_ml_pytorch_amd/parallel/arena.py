@@ -144,6 +144,44 @@ class FlatArena:
         co, ci, r, k = s.shape
         return self._wt[s.offset:s.offset + s.numel].view(ci, r, k, co)
 
+    def padded_rows_shadow(self, p: torch.Tensor, kp: int):
+        """bf16 ``[CO, Kp]`` image of conv weight ``p``'s shadow with its rows
+        (channels-last ``(r, s, ci)`` order, ``K = R*S*CI``) padded to ``kp``
+        columns -- the operand of the im2col GEMM when ``K % 8 != 0`` (LeNet).
+
+        Every such weight lives in one buffer whose pad columns are zeroed once;
+        all of them are refreshed by ONE native launch the first time this is
+        called after the shadow changed (no per-step fill + copy kernels)."""
+        if self.w16 is None or not self.w16.is_cuda:
+            return None
+        if getattr(self, "_pad", None) is None:
+            rows, self._pad_index, off, mx = [], {}, 0, 0
+            for s, q in zip(self.slots, self.params):
+                if len(s.shape) == 4:
+                    co, ci, r, k = s.shape
+                    K = ci * r * k
+                    Kp = (K + 7) // 8 * 8
+                    if K != Kp:
+                        self._pad_index[id(q)] = (off, co, Kp)
+                        rows.append([s.offset, off, co, K, Kp])
+                        off += co * Kp
+                        mx = max(mx, co * K)
+            self._pad = torch.zeros(max(off, 8), dtype=self.w16.dtype, device=self.device)
+            self._pad_table = (torch.tensor(rows, dtype=torch.int64).reshape(-1, 5)
+                               .to(self.device))
+            self._pad_max = mx
+            self._pad_version = -1
+        ent = self._pad_index.get(id(p))
+        if ent is None or ent[2] != kp:
+            return None
+        if self._pad_version != self.version:
+            from ..ops._ext import native
+
+            native().pad_rows_batched(self.w16, self._pad, self._pad_table, self._pad_max)
+            self._pad_version = self.version
+        off, co, Kp = ent
+        return self._pad[off:off + co * Kp].view(co, Kp)
+
     def refresh_shadow(self):
         self.bump()
         if self.w16 is None:
@@ -161,7 +199,12 @@ class FlatArena:
         # a pull landing since the last backward
         self.bump()
         if self.g32 is not None:
-            self.g32.zero_()
+            if self.g32.is_cuda:
+                from ..ops._ext import native
+
+                native().zero_(self.g32)      # a memset node, not an ATen fill kernel
+            else:
+                self.g32.zero_()
 
     def ensure_grads_attached(self):
         """Re-attach grad views if user code set ``p.grad = None``."""
