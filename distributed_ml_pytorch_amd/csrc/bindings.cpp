@@ -328,7 +328,7 @@ Tensor gap_bwd(Tensor dy, int64_t H, int64_t W) {
   return dx;
 }
 
-std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K, int64_t S, int64_t P) {
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K, int64_t S, int64_t P, bool nchw_out) {
   if (S < 0) S = K;
   check_nhwc_bf16(x, "x");
   TORCH_CHECK(x.dim() == 4, "maxpool expects 4-D input");
@@ -339,19 +339,29 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K, int64_t S, int64_t P) {
   const int Wo = dmp::maxpool_out(W, (int)K, (int)S, (int)P);
   TORCH_CHECK(Ho > 0 && Wo > 0, "maxpool: window larger than input");
   auto mf = at::MemoryFormat::ChannelsLast;
-  auto y = at::empty({N, C, Ho, Wo}, x.options().memory_format(mf));
+  const bool nchw = nchw_out && C % 8 == 0;
+  auto y = at::empty({N, C, Ho, Wo},
+                     x.options().memory_format(nchw ? at::MemoryFormat::Contiguous : mf));
   auto idx = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(mf));
   dmp::launch_maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                           reinterpret_cast<uint16_t*>(y.data_ptr()), idx.data_ptr<uint8_t>(), N, H,
-                          W, C, (int)K, (int)S, (int)P, cur_stream());
+                          W, C, (int)K, (int)S, (int)P, cur_stream(), nchw);
+  if (nchw_out && !nchw) y = y.contiguous();
   return {y, idx};
 }
 
 Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t K, int64_t S, int64_t P) {
   if (S < 0) S = K;
   auto mf = at::MemoryFormat::ChannelsLast;
-  dy = dy.contiguous(mf);
-  check_nhwc_bf16(dy, "dy");
+  // an NCHW-contiguous dy (gradient of an nchw_out forward) is read in place
+  const bool nchw = dy.dim() == 4 && dy.size(1) % 8 == 0 && dy.is_contiguous() &&
+                    !dy.is_contiguous(mf);
+  if (!nchw) {
+    dy = dy.contiguous(mf);
+    check_nhwc_bf16(dy, "dy");
+  } else {
+    check_gpu(dy, "dy");
+  }
   TORCH_CHECK(idx.sizes() == dy.sizes() && idx.is_contiguous(mf), "maxpool idx mismatch");
   const int N = (int)dy.size(0), C = (int)dy.size(1);
   TORCH_CHECK(dy.size(2) == dmp::maxpool_out((int)H, (int)K, (int)S, (int)P) &&
@@ -361,7 +371,7 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t K, int64
   Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(mf));
   dmp::launch_maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
                           reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)H, (int)W, C, (int)K,
-                          (int)S, (int)P, cur_stream());
+                          (int)S, (int)P, cur_stream(), nchw);
   return dx;
 }
 
@@ -1555,7 +1565,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("gap_fwd", &gap_fwd, "NHWC global average pool forward");
   m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC KxK / stride S / pad P max pool forward",
-        py::arg("x"), py::arg("K"), py::arg("S") = -1, py::arg("P") = 0);
+        py::arg("x"), py::arg("K"), py::arg("S") = -1, py::arg("P") = 0,
+        py::arg("nchw_out") = false);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC KxK / stride S / pad P max pool backward",
         py::arg("dy"), py::arg("idx"), py::arg("H"), py::arg("W"), py::arg("K"),
         py::arg("S") = -1, py::arg("P") = 0);

@@ -51,6 +51,9 @@ __global__ void __launch_bounds__(256) gap_bwd_kernel(const u16* __restrict__ dy
 
 // Max pool, window K x K, stride S, zero..K/2 padding (padded taps never win),
 // floor mode; the argmax tap (i*K + j, K <= 15) is kept as uint8 per element.
+// NCHW_OUT: y is written NCHW-contiguous (a pool feeding a flatten + Linear in
+// the reference's (c, h, w) order: LeNet), idx stays NHWC.
+template <bool NCHW_OUT>
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const u16* __restrict__ x,
                                                           u16* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H,
@@ -87,7 +90,12 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const u16* __restrict_
     bf16x8 o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) o.v[k] = f2bf(best[k]);
-    *reinterpret_cast<bf16x8*>(y + t * 8) = o;
+    if constexpr (NCHW_OUT) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) y[((n * C + cg * 8 + k) * Ho + ho) * Wo + wo] = o.v[k];
+    } else {
+      *reinterpret_cast<bf16x8*>(y + t * 8) = o;
+    }
     uint2 packed;
     packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((u32)bi[3] << 24);
     packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((u32)bi[7] << 24);
@@ -97,6 +105,8 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const u16* __restrict_
 
 // Gather form (no atomics, no zero fill): every input element sums dy over the
 // outputs whose window covers it and whose saved argmax is this tap.
+// NCHW_DY: dy arrives NCHW-contiguous (the gradient of an NCHW_OUT forward)
+template <bool NCHW_DY>
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const u16* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx,
                                                           u16* __restrict__ dx, int N, int H,
@@ -119,7 +129,13 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const u16* __restrict_
       for (int wo = wlo; wo <= whi; ++wo) {
         const uint8_t me = (uint8_t)((h - (ho * S - P)) * K + (w - (wo * S - P)));
         const long long o = ((n * Ho + ho) * Wo + wo) * C + cg * 8;
-        const bf16x8 g = *reinterpret_cast<const bf16x8*>(dy + o);
+        bf16x8 g;
+        if constexpr (NCHW_DY) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g.v[k] = dy[((n * C + cg * 8 + k) * Ho + ho) * Wo + wo];
+        } else {
+          g = *reinterpret_cast<const bf16x8*>(dy + o);
+        }
         const uint2 packed = *reinterpret_cast<const uint2*>(idx + o);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -207,7 +223,7 @@ void launch_gap_bwd(const u16* dy, u16* dx, int N, int HW, int C, hipStream_t s)
 int maxpool_out(int H, int K, int S, int P) { return (H + 2 * P - K) / S + 1; }
 
 void launch_maxpool_fwd(const u16* x, u16* y, uint8_t* idx, int N, int H, int W, int C, int K,
-                        int S, int P, hipStream_t s) {
+                        int S, int P, hipStream_t s, bool nchw_out) {
   const int Ho = maxpool_out(H, K, S, P), Wo = maxpool_out(W, K, S, P);
   if (C % 8) {
     const long long n1 = (long long)N * Ho * Wo * C;
@@ -216,12 +232,16 @@ void launch_maxpool_fwd(const u16* x, u16* y, uint8_t* idx, int N, int H, int W,
     return;
   }
   const long long total = (long long)N * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, x, y, idx,
-                     N, H, W, C, K, S, P, Ho, Wo);
+  if (nchw_out)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(stream_grid(total, 256)), dim3(256), 0, s, x,
+                       y, idx, N, H, W, C, K, S, P, Ho, Wo);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(stream_grid(total, 256)), dim3(256), 0, s,
+                       x, y, idx, N, H, W, C, K, S, P, Ho, Wo);
 }
 
 void launch_maxpool_bwd(const u16* dy, const uint8_t* idx, u16* dx, int N, int H, int W, int C,
-                        int K, int S, int P, hipStream_t s) {
+                        int K, int S, int P, hipStream_t s, bool nchw_dy) {
   const int Ho = maxpool_out(H, K, S, P), Wo = maxpool_out(W, K, S, P);
   if (C % 8) {
     const long long n1 = (long long)N * H * W * C;
@@ -230,8 +250,12 @@ void launch_maxpool_bwd(const u16* dy, const uint8_t* idx, u16* dx, int N, int H
     return;
   }
   const long long total = (long long)N * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy, idx,
-                     dx, N, H, W, C, K, S, P, Ho, Wo);
+  if (nchw_dy)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy,
+                       idx, dx, N, H, W, C, K, S, P, Ho, Wo);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<false>, dim3(stream_grid(total, 256)), dim3(256), 0, s,
+                       dy, idx, dx, N, H, W, C, K, S, P, Ho, Wo);
 }
 
 }  // namespace dmp

@@ -36,7 +36,8 @@ class LeNet(nn.Module):
     def forward(self, x):
         # relu(pool(c)) == pool(relu(c)); relu(pool(drop(c))) == pool(drop(relu(c)))
         h = DF.max_pool2d(self.conv1(x, relu=True), 2)
-        h = DF.max_pool2d(self.conv2_drop(self.conv2(h, relu=True)), 2)
+        # the pool writes (c, h, w) order directly: flatten is a view
+        h = DF.max_pool2d(self.conv2_drop(self.conv2(h, relu=True)), 2, nchw_out=True)
         h = torch.flatten(h.contiguous(), 1)
         h = self.fc1_drop(self.fc1(h, relu=True))
         h = self.fc2(h, relu=True)

@@ -363,9 +363,9 @@ def global_avg_pool(x):
 
 class _MaxPool(Function):
     @staticmethod
-    def forward(ctx, x, k, s, p):
+    def forward(ctx, x, k, s, p, nchw_out=False):
         x = x.contiguous(memory_format=CL)
-        y, idx = native().maxpool_fwd(x, k, s, p)
+        y, idx = native().maxpool_fwd(x, k, s, p, nchw_out)
         ctx.save_for_backward(idx)
         ctx.meta = (x.shape[2], x.shape[3], k, s, p)
         return y
@@ -374,18 +374,21 @@ class _MaxPool(Function):
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
         H, W, k, s, p = ctx.meta
-        return native().maxpool_bwd(dy, idx, H, W, k, s, p), None, None, None
+        return native().maxpool_bwd(dy, idx, H, W, k, s, p), None, None, None, None
 
 
-def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0):
+def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0,
+               nchw_out: bool = False):
     """Max pool (floor mode): native NHWC kernel for bf16 GPU input (any channel
-    count, window <= 15, stride, padding <= window/2), PyTorch otherwise."""
+    count, window <= 15, stride, padding <= window/2), PyTorch otherwise.
+    ``nchw_out``: write the output NCHW-contiguous (a pool that feeds a flatten
+    in the reference's (c, h, w) order: no layout copy either way)."""
     stride = kernel_size if stride is None else stride
     if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and 1 <= kernel_size <= 15 and stride >= 1 and 0 <= 2 * padding <= kernel_size
             and x.shape[2] + 2 * padding >= kernel_size
             and x.shape[3] + 2 * padding >= kernel_size):
-        return _MaxPool.apply(x, int(kernel_size), int(stride), int(padding))
+        return _MaxPool.apply(x, int(kernel_size), int(stride), int(padding), bool(nchw_out))
     return F.max_pool2d(x, kernel_size, stride, padding)
 
 

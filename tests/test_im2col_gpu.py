@@ -49,6 +49,28 @@ def test_im2col_conv_matches_fp32(B, CI, H, CO, k, st, pd, bias, relu, xgrad):
         assert _rel(x.grad, xr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("C", [16, 6])
+def test_maxpool_nchw_out_feeds_flatten(C):
+    """``nchw_out``: the pool writes (c, h, w) order (LeNet's pool -> flatten ->
+    fc1) and its backward reads the NCHW gradient in place."""
+    from distributed_ml_pytorch_amd.ops import functional as DF
+
+    torch.manual_seed(2)
+    x = torch.randn(8, C, 10, 10, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = DF.max_pool2d(x, 2, nchw_out=True)
+    assert y.is_contiguous()
+    f = torch.flatten(y, 1)
+    assert f.data_ptr() == y.data_ptr()
+    g = torch.randn_like(f)
+    f.backward(g)
+    xr = x.detach().float().requires_grad_(True)
+    fr = torch.flatten(F.max_pool2d(xr, 2), 1)
+    fr.backward(g.float())
+    torch.testing.assert_close(f.float(), fr)
+    torch.testing.assert_close(x.grad.float(), xr.grad)
+
+
 @pytest.mark.parametrize("C", [6, 16, 3])
 def test_maxpool_any_channels(C):
     from distributed_ml_pytorch_amd.ops import functional as DF
