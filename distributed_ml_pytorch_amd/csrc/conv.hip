@@ -826,6 +826,15 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
 // (the host routes addend dgrads to conv_halo_kernel).
 struct HaloPGeom {
   int TH, TB, HROWS, APW, AINS, ntiles;   // APW: pieces per wave (>= AINS / NW), AINS: exact
+  // DIAGNOSTIC (DMP_HALO64P_XFORM=1, forward only): the cost of applying a
+  // per-channel BatchNorm scale / shift + clamp to the staged input tile in LDS
+  // ("apply-in-consumer"): every wave rewrites its own landed halo pieces,
+  // x -> max(x * xs + xh, xlo), before the tile's barrier.  Run with the
+  // identity (xs 1, xh 0, xlo -inf: outputs unchanged, the work is not
+  // foldable: runtime values) to price the transform against the BN apply
+  // pass it would replace (profiles/bn_consumer_fusion_r3.txt).
+  int xform;
+  float xs, xh, xlo;
 };
 
 constexpr int kHpAPW = 12;   // max halo DMA pieces per wave per tile
@@ -1022,9 +1031,33 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) stage(s, s);
   const int vm_wait = (NS - 2) * APW;
+  // diagnostic transform of this wave's own landed pieces of tile k (see HaloPGeom)
+  auto xform_tile = [&](int k) {
+    u16* As = Hs + (k % NS) * STAGE;
+    const int t = tile_of(k);
+    const int m0 = t * BM;
+    const int b0 = m0 / img, h0 = (m0 - b0 * img) / W;
+#pragma unroll
+    for (int j = 0; j < kHpAPW; ++j) {
+      if (j < APW && (NS != 2 || wid + j * NW < hg.AINS)) {
+        const unsigned inf = x_inf[j];
+        const int tb = (int)((inf >> 16) & 0x7fff), dh = (int)((inf >> 8) & 255) - 64;
+        const bool ok = (inf >> 31) && b0 + tb < a.B && (unsigned)(h0 + dh) < (unsigned)H;
+        if (ok) {   // halo / padding positions stay exactly zero
+          bf16x8* q = reinterpret_cast<bf16x8*>(As + (wid + j * NW) * 512 + lane * 8);
+          bf16x8 v = *q;
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v.v[e] = f2bf(fmaxf(__fmaf_rn(bf2f(v.v[e]), hg.xs, hg.xh), hg.xlo));
+          *q = v;
+        }
+      }
+    }
+  };
   for (int k = 0; k < nt; ++k) {
     if (NS == 2) wait_vm<0>();
     else wait_vm_n(vm_wait);            // tile k (and, at k = 0, the weights) landed ...
+    if (!FLIP && hg.xform) xform_tile(k);
     __builtin_amdgcn_s_barrier();       // ... for every wave; slot (k-1) % NS is free
     asm volatile("" ::: "memory");
     stage((k + NS - 1) % NS, k + NS - 1);
@@ -1353,6 +1386,14 @@ static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
     if (!halop_geom(cfg, a.B, a.GH, a.GW, a.CI, a.R, a.S, a.stride, a.pad, &pg, &bm, &ns, &nw,
                     &plds))
       return false;
+    static const int xform_env = [] {
+      const char* e = getenv("DMP_HALO64P_XFORM");
+      return e && e[0] == '1' ? 1 : 0;
+    }();
+    pg.xform = xform_env;
+    pg.xs = 1.f;
+    pg.xh = 0.f;
+    pg.xlo = -INFINITY;
     if constexpr (!(FLIP && STATS)) {
       if (nw == 8) launch_halop_t<256, 2, 8, FLIP, STATS>(a, pg, plds, s);
       else if (bm == 256) launch_halop_t<256, 2, 4, FLIP, STATS>(a, pg, plds, s);
