@@ -179,13 +179,24 @@ __device__ __forceinline__ bf16x8 frag(const u16* img, int r, int ks, int lane) 
 // One output tile per block (a persistent variant whose DMA ring ran across
 // tile boundaries measured no faster on the ViT shapes and 15-70 % slower on
 // the wgrad tiles: profiles/gemm_vs_hipblaslt_r2.txt).
-template <int BM, int BN, int BK, int WM, int WN, int NS, bool AT, bool BT, int EPI>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
-  constexpr int NW = WM * WN;
+//
+// KG = 2 (weight gradients only): two groups of WM x WN waves share the block's
+// output tile and split every staged 2*BK-deep k-tile between them (group g
+// takes k-rows g*BK .. g*BK + BK - 1 of the [2*BK][rows] images); at the end
+// group 1 parks its fp32 accumulators in the drained ring and group 0 adds them
+// before the single flush.  One 8-wave block per CU then does the work of two
+// 4-wave blocks with HALF the split-K partials through the fp32 atomics / slab
+// (the ViT weight gradients spend ~25-30 % of their time there).
+template <int BM, int BN, int BK, int WM, int WN, int NS, bool AT, bool BT, int EPI, int KG = 1>
+__global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
+  constexpr int NWG = WM * WN, NW = NWG * KG;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "wave tiles of 16x16 MFMAs");
-  using SA = Stager<BM, AT, NW, BK>;
-  using SB = Stager<BN, BT, NW, BK>;
+  static_assert(KG == 1 || (KG == 2 && EPI == EPI_ACC32 && AT && BT),
+                "k-groups only for the weight gradient (both operands k-strided)");
+  constexpr int BKS = BK * KG;                      // k-rows per staged k-tile
+  using SA = Stager<BM, AT, NW, BKS>;
+  using SB = Stager<BN, BT, NW, BKS>;
   constexpr int STAGE = SA::EL + SB::EL;
   constexpr int INS_MIN = SA::PW_MIN + SB::PW_MIN;   // DMAs every wave issues per stage
   static_assert(NS >= 2 && (NS - 2) * INS_MIN < 64, "pipeline depth");
@@ -194,7 +205,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
+  const int kg = KG == 1 ? 0 : wid / NWG, wq = KG == 1 ? wid : wid % NWG;
+  const int wm = wq / WN, wn = wq % WN;
 
   // XCD-aware bijective remap of the tile id: blocks sharing an XCD take
   // consecutive tiles (neighbouring N tiles of one M panel)
@@ -206,7 +218,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
   const int kbase = blockIdx.y * g.k_chunk;
   const int kend = min(g.K, kbase + g.k_chunk) - kbase;
   if (kend <= 0) return;
-  const int KT = (kend + BK - 1) / BK;
+  const int KT = (kend + BKS - 1) / BKS;
 
   SA sa;
   SB sb;
@@ -218,8 +230,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
       (void*)g.b, 0, BT ? (int)(2LL * g.K * g.ldb) : (int)(2LL * g.N * g.ldb), 0x00020000);
   auto stage = [&](int buf, int kt) {
     u16* As = lds + buf * STAGE;
-    sa.issue(rsA, As, wid, kt * BK, kend, g.lda);
-    sb.issue(rsB, As + SA::EL, wid, kt * BK, kend, g.ldb);
+    sa.issue(rsA, As, wid, kt * BKS, kend, g.lda);
+    sb.issue(rsB, As + SA::EL, wid, kt * BKS, kend, g.ldb);
   };
 
   f32x4 acc[TM][TN];
@@ -234,12 +246,13 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
     const u16* As = lds + buf * STAGE;
     const u16* Bs = As + SA::EL;
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
+    for (int ks0 = 0; ks0 < BK / 32; ++ks0) {
+      const int ks = kg * (BK / 32) + ks0;          // this k-group's rows of the image
       bf16x8 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag<BM, AT, BK>(As, ra + i * 16, ks, lane);
+      for (int i = 0; i < TM; ++i) af[i] = frag<BM, AT, BKS>(As, ra + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = frag<BN, BT, BK>(Bs, rb + j * 16, ks, lane);
+      for (int j = 0; j < TN; ++j) bf[j] = frag<BN, BT, BKS>(Bs, rb + j * 16, ks, lane);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -476,6 +489,31 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_kernel(GemmArgs g) {
     if (kt + NS - 1 < KT) stage((kt + NS - 1) % NS, kt + NS - 1);
     compute(kt % NS);
   }
+  if constexpr (KG == 2) {
+    // group 1 parks its partial sums in the drained ring, group 0 adds them
+    gwait_vm<0>();
+    __syncthreads();
+    float* park = reinterpret_cast<float*>(lds);   // [NWG][TM*TN (+TM)][64 lanes] f32x4
+    constexpr int PT = TM * TN + TM;
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          *reinterpret_cast<f32x4*>(park + ((wq * PT + i * TN + j) * 64 + lane) * 4) = acc[i][j];
+        *reinterpret_cast<f32x4*>(park + ((wq * PT + TM * TN + i) * 64 + lane) * 4) = accb[i];
+      }
+    }
+    __syncthreads();
+    if (kg == 1) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] += *reinterpret_cast<const f32x4*>(park + ((wq * PT + i * TN + j) * 64 + lane) * 4);
+      accb[i] += *reinterpret_cast<const f32x4*>(park + ((wq * PT + TM * TN + i) * 64 + lane) * 4);
+    }
+  }
   epilogue(m0, n0);
 }
 
@@ -692,7 +730,7 @@ void launch_small(const GemmArgs& g, int splits, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ configs
-struct Cfg { int bm, bn, bk, wm, wn, ns; };
+struct Cfg { int bm, bn, bk, wm, wn, ns, kg = 1; };
 // LDS = ns * (bm + bn) * bk * 2 B.  Tile heights 160 / 192 exist for tile
 // counts: M = 12608 tokens x N = 768 is 150 tiles of 256x256 (59 % of 256 CUs)
 // but 237 of 160x256.  A k-strided (transposed) operand needs a tile side that
@@ -707,13 +745,14 @@ constexpr Cfg kCfgs[] = {
     {256, 192, 64, 2, 4, 2},   // 6: 112 KiB, 8 waves (128x48)
     {128, 128, 32, 2, 2, 4},   // 7:  64 KiB, 4 waves, 2 blocks/CU, 3 k-tiles in flight
     {256, 128, 64, 2, 2, 3},   // 8: 144 KiB, 4 waves of 128x64 (1 wave / SIMD)
+    {128, 128, 64, 2, 2, 2, 2},   // 9: wgrad only, 2 k-groups of 4 waves: 128 KiB, 1 block/CU
 };
 // (4 waves of 128x128 per 256x256 / 192x256 tile, accumulators in AGPRs: 20-40 %
 // slower than the 8-wave tiles on every ViT shape -- profiles/gemm_vs_hipblaslt_r2.txt)
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 constexpr bool cfg_ok(const Cfg& c, bool at, bool bt) {
-  return (!at || c.bm % 128 == 0) && (!bt || c.bn % 128 == 0);
+  return (!at || c.bm % 128 == 0) && (!bt || c.bn % 128 == 0) && (c.kg == 1 || (at && bt));
 }
 
 template <int C, bool AT, bool BT, int EPI>
@@ -725,8 +764,12 @@ void launch_cfg(const GemmArgs& a, int splits, hipStream_t s) {
     GemmArgs g = a;
     g.tiles_n = (g.N + c.bn - 1) / c.bn;
     const int tiles = ((g.M + c.bm - 1) / c.bm) * g.tiles_n;
-    hipLaunchKernelGGL((gemm_kernel<c.bm, c.bn, c.bk, c.wm, c.wn, c.ns, AT, BT, EPI>),
-                       dim3((unsigned)tiles, (unsigned)splits), dim3(64 * c.wm * c.wn), 0, s, g);
+    if constexpr (c.kg == 1 || EPI == EPI_ACC32)
+      hipLaunchKernelGGL((gemm_kernel<c.bm, c.bn, c.bk, c.wm, c.wn, c.ns, AT, BT, EPI, c.kg>),
+                         dim3((unsigned)tiles, (unsigned)splits), dim3(64 * c.wm * c.wn * c.kg), 0,
+                         s, g);
+    else
+      throw std::runtime_error("gemm: k-group configs are weight-gradient only");
   }
 }
 
@@ -742,7 +785,8 @@ void launch_mode(int cfg, const GemmArgs& a, int splits, hipStream_t s) {
     case 5: launch_cfg<5, AT, BT, EPI>(a, splits, s); break;
     case 6: launch_cfg<6, AT, BT, EPI>(a, splits, s); break;
     case 7: launch_cfg<7, AT, BT, EPI>(a, splits, s); break;
-    default: launch_cfg<8, AT, BT, EPI>(a, splits, s); break;
+    case 8: launch_cfg<8, AT, BT, EPI>(a, splits, s); break;
+    default: launch_cfg<9, AT, BT, EPI>(a, splits, s); break;
   }
 }
 
@@ -761,7 +805,7 @@ void gemm_config_info(int cfg, int* info) {
   const Cfg& c = kCfgs[cfg];
   info[0] = c.bm;
   info[1] = c.bn;
-  info[2] = 64 * c.wm * c.wn;
+  info[2] = 64 * c.wm * c.wn * c.kg;
   info[3] = c.ns;
   info[4] = c.bk;
 }

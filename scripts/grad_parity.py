@@ -32,11 +32,28 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--zero-init-residual", action="store_true",
+                    help="zero the last BatchNorm gamma of every residual block (both models): "
+                         "the well-conditioned start where stock bf16 is itself close to fp32")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     mk = lambda lr: Worker(TrainConfig(model=a.model, batch_size=a.batch, mode="single", lr=lr,  # noqa: E731
                                        evaluate=False, verbose=False), DistInfo(device=dev))
+    def zero_res(worker):
+        if not a.zero_init_residual:
+            return
+        from distributed_ml_pytorch_amd.models.resnet import BasicBlock, Bottleneck
+
+        with torch.no_grad():
+            for m in worker.model.modules():
+                if isinstance(m, Bottleneck):
+                    m.bn3.weight.zero_()
+                elif isinstance(m, BasicBlock):
+                    m.bn2.weight.zero_()
+        worker.arena.refresh_shadow()
+
     w = mk(0.0)
+    zero_res(w)
     ctor, shape, nc = sb.MODELS[a.model]
     ref = ctor().to(dev).to(memory_format=torch.channels_last)
     P, Q = list(w.model.parameters()), list(ref.parameters())
@@ -75,6 +92,7 @@ def main():
 
     # trajectory: plain SGD, same init, same batches
     w2 = mk(a.lr)
+    zero_res(w2)
     with torch.no_grad():
         for p, q in zip(w2.model.parameters(), ref.parameters()):
             q.copy_(p.float())

@@ -158,3 +158,27 @@ def test_skinny_wgrad_kernel(M, N, K, ldb):
     ref = a.float().t() @ b.float() + 0.25
     torch.testing.assert_close(c, ref, rtol=2e-3, atol=2e-3 * float(ref.abs().max()))
     torch.testing.assert_close(db, a.float().sum(0) - 1.0, rtol=2e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(768, 256, 1000), (256, 384, 12608)])
+def test_gemm_wgrad_every_config_split_slab(M, N, K):
+    """Weight-gradient GEMM (dW[M][N] += dY^T X over K rows, + dbias) for every
+    tile config of mode 2 -- including the 2-k-group 8-wave tile (cfg 9) --
+    with and without split-K, atomics and slab reductions, vs fp32."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    torch.manual_seed(0)
+    a = torch.randn(K, M, device="cuda").to(torch.bfloat16)
+    b = torch.randn(K, N, device="cuda").to(torch.bfloat16)
+    ref = a.float().t() @ b.float()
+    refb = a.float().sum(0)
+    cfgs = [c[0] for c in native().gemm_configs() if native().gemm_config_ok(2, c[0])]
+    assert 9 in cfgs
+    for cfg in cfgs:
+        for splits, slab in ((1, False), (3, False), (3, True)):
+            c = torch.full((M, N), 0.5, device="cuda")
+            db = torch.zeros(M, device="cuda")
+            native().gemm(2, 3, cfg, a, b, c, None, None, None, db, splits, False, None, slab)
+            err = float((c - 0.5 - ref).norm() / ref.norm())
+            assert err < 1e-2, (cfg, splits, slab, err)
+            assert float((db - refb).norm() / refb.norm()) < 1e-2, (cfg, splits, slab)
