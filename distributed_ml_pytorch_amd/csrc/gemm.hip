@@ -634,61 +634,47 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
 // thread and pass), each tile staged once into LDS as fp32 by all 256 threads,
 // and the block's partial sums leave through one fp32 atomic per output (and
 // per dbias row).  Blocks = enough chunks to cover every CU a few times.
-constexpr int kSkinnyMaxOut = 4096, kSkinnyTR = 32;
+constexpr int kSkinnyMaxOut = 4096;
 
+// One tile of `chunk` rows per block: every load of the tile is in flight at
+// once (one memory latency per block instead of one per 32-row stage).
 __global__ void __launch_bounds__(256) gemm_skinny_wgrad_kernel(GemmArgs g, int chunk) {
   constexpr int OPT = kSkinnyMaxOut / 256;                // outputs per thread (max)
-  extern __shared__ float sk_lds[];                       // [TR][M] A, then [TR][N] B
+  extern __shared__ float sk_lds[];                       // [chunk][M] A, then [chunk][N] B
   const int M = g.M, N = g.N;
   float* As = sk_lds;
-  float* Bs = sk_lds + kSkinnyTR * M;
+  float* Bs = sk_lds + chunk * M;
   const int tid = threadIdx.x;
   const int k0 = blockIdx.x * chunk;
-  const int k1 = min(g.K, k0 + chunk);
-  if (k0 >= k1) return;
-  const int MN = M * N;
-  float acc[OPT];
-  float bsum = 0.f;                                       // dbias row sums (tid < M)
-#pragma unroll
-  for (int q = 0; q < OPT; ++q) acc[q] = 0.f;
-  for (int kt = k0; kt < k1; kt += kSkinnyTR) {
-    const int rows = min(kSkinnyTR, k1 - kt);
-    __syncthreads();                                      // previous tile consumed
-    for (int e = tid; e < kSkinnyTR * M; e += 256) {
-      const int r = e / M, m = e - r * M;
-      As[e] = r < rows ? bf2f(g.a[(long long)(kt + r) * g.lda + m]) : 0.f;
-    }
-    for (int e = tid; e < kSkinnyTR * N; e += 256) {
-      const int r = e / N, n = e - r * N;
-      Bs[e] = r < rows ? bf2f(g.b[(long long)(kt + r) * g.ldb + n]) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < OPT; ++q) {
-      const int o = tid + 256 * q;
-      if (o < MN) {
-        const int m = o / N, n = o - m * N;
-        float t = acc[q];
-#pragma unroll 8
-        for (int r = 0; r < kSkinnyTR; ++r) t = fmaf(As[r * M + m], Bs[r * N + n], t);
-        acc[q] = t;
-      }
-    }
-    if (g.dbias != nullptr && tid < M) {
-#pragma unroll 8
-      for (int r = 0; r < kSkinnyTR; ++r) bsum += As[r * M + tid];
-    }
+  const int rows = min(g.K - k0, chunk);
+  if (rows <= 0) return;
+  for (int e = tid; e < rows * M; e += 256) {
+    const int r = e / M, m = e - r * M;
+    As[e] = bf2f(g.a[(long long)(k0 + r) * g.lda + m]);
   }
+  for (int e = tid; e < rows * N; e += 256) {
+    const int r = e / N, n = e - r * N;
+    Bs[e] = bf2f(g.b[(long long)(k0 + r) * g.ldb + n]);
+  }
+  __syncthreads();
+  const int MN = M * N;
   float* C = reinterpret_cast<float*>(g.c);
 #pragma unroll
   for (int q = 0; q < OPT; ++q) {
     const int o = tid + 256 * q;
     if (o < MN) {
       const int m = o / N, n = o - m * N;
-      atomicAdd(C + (long long)m * g.ldc + n, acc[q]);
+      float t = 0.f;
+#pragma unroll 4
+      for (int r = 0; r < rows; ++r) t = fmaf(As[r * M + m], Bs[r * N + n], t);
+      atomicAdd(C + (long long)m * g.ldc + n, t);
     }
   }
-  if (g.dbias != nullptr && tid < M) atomicAdd(g.dbias + tid, bsum);
+  if (g.dbias != nullptr && tid < M) {
+    float t = 0.f;
+    for (int r = 0; r < rows; ++r) t += As[r * M + tid];
+    atomicAdd(g.dbias + tid, t);
+  }
 }
 
 // C[m][n] (ldc) += sum over the splits of slab[s][m][n]; 4 columns per thread
@@ -833,11 +819,13 @@ void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const u
   } else if (cfg == -2) {
     if ((long long)M * N > kSkinnyMaxOut || M > 256 || N > 1024)
       throw std::runtime_error("gemm: skinny wgrad needs M*N <= 4096 (M <= 256, N <= 1024)");
-    // ~1024 blocks over the reduction, whole TR-row tiles per chunk
-    int chunk = (K + 1023) / 1024;
-    chunk = std::max(kSkinnyTR, (chunk + kSkinnyTR - 1) / kSkinnyTR * kSkinnyTR);
+    // ~one block per CU (two when the reduction is short), one tile each, the
+    // tile capped at 64 KiB of fp32 LDS (two resident blocks per CU)
+    const int cap = std::max(8, (int)(65536 / (4 * (M + N))));
+    int chunk = std::max(8, (K + 255) / 256);
+    chunk = std::min(cap, (chunk + 7) / 8 * 8);
     const int blocks = (K + chunk - 1) / chunk;
-    const size_t lds = (size_t)kSkinnyTR * (M + N) * sizeof(float);
+    const size_t lds = (size_t)chunk * (M + N) * sizeof(float);
     hipLaunchKernelGGL(gemm_skinny_wgrad_kernel, dim3((unsigned)blocks), dim3(256), lds, s, g,
                        chunk);
   } else {

@@ -233,7 +233,7 @@ class Worker:
         self._graph_key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
         return loss.clone(), hits.clone()
 
-    def _graph_step(self, x, y):
+    def _graph_step(self, x, y, keep: bool = True):
         key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
         if self.graph is None or key != self._graph_key:
             return self._capture(x, y)
@@ -243,13 +243,18 @@ class Worker:
             self.graph.replay()
         self.opt.comm_step()
         self.step_idx += 1
-        # the captured outputs are overwritten by the next replay
+        # the captured outputs are overwritten by the next replay: copies unless
+        # the caller reads them before the next step (``keep=False``)
+        if not keep:
+            return self._gloss, self._ghits
         return self._gloss.clone(), self._ghits.clone()
 
-    def train_step(self, x, y):
-        """One fwd+bwd+update. Returns (loss, hits) as device tensors (no sync)."""
+    def train_step(self, x, y, keep: bool = True):
+        """One fwd+bwd+update. Returns (loss, hits) as device tensors (no sync).
+        ``keep=False``: with hipGraph replay the returned tensors are the graph's
+        own outputs, valid until the next step (no per-step copy kernels)."""
         if getattr(self, "use_graph", False):
-            return self._graph_step(x, y)
+            return self._graph_step(x, y, keep)
         with self.timer.time("compute_launch"):
             self.opt.zero_grad()
             logits = self.model(x)
