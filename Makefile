@@ -6,7 +6,7 @@ NPROC ?= 8
 MASTER_PORT ?= 29500
 
 .PHONY: build install setup graph first second server single gpu launch launch-gpu bench \
-	bench-scale test test-gpu profile dist clean
+	bench-scale bench-scale-central test test-gpu profile dist clean
 
 # compile every gfx950 HIP kernel + bindings into distributed_ml_pytorch_amd/_native*.so
 build:
@@ -52,6 +52,14 @@ bench-scale:
 	for n in 1 2 4 8; do \
 	  $(PY) -m torch.distributed.run --nnodes=1 --nproc-per-node $$n --master-addr 127.0.0.1 \
 	    --master-port $(MASTER_PORT) bench.py --gpus $$n || exit $$?; \
+	done
+
+# the reference topology at every N: rank 0 = parameter server, ranks 1..N-1 = workers
+# (BASELINE config #3 "1 PS + 7 workers"), payloads over one RCCL communicator per pair
+bench-scale-central:
+	for n in 2 4 8; do \
+	  $(PY) -m torch.distributed.run --nnodes=1 --nproc-per-node $$n --master-addr 127.0.0.1 \
+	    --master-port $(MASTER_PORT) bench.py --gpus $$n --ps central || exit $$?; \
 	done
 
 test:
