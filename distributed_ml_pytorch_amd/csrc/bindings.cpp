@@ -328,7 +328,8 @@ Tensor gap_bwd(Tensor dy, int64_t H, int64_t W) {
   return dx;
 }
 
-std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K, int64_t S, int64_t P, bool nchw_out) {
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K, int64_t S, int64_t P, bool nchw_out,
+                                bool relu_in) {
   if (S < 0) S = K;
   check_nhwc_bf16(x, "x");
   TORCH_CHECK(x.dim() == 4, "maxpool expects 4-D input");
@@ -345,7 +346,7 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t K, int64_t S, int64_t P, bool 
   auto idx = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(mf));
   dmp::launch_maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                           reinterpret_cast<uint16_t*>(y.data_ptr()), idx.data_ptr<uint8_t>(), N, H,
-                          W, C, (int)K, (int)S, (int)P, cur_stream(), nchw);
+                          W, C, (int)K, (int)S, (int)P, cur_stream(), nchw, relu_in);
   if (nchw_out && !nchw) y = y.contiguous();
   return {y, idx};
 }
@@ -942,8 +943,8 @@ void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
   TORCH_CHECK(!relu || epi == 0, "gemm: relu only with the store epilogue");
   TORCH_CHECK(mode >= 0 && mode <= 2, "gemm: mode must be 0 (fwd), 1 (dgrad) or 2 (wgrad)");
   TORCH_CHECK(c.dim() == 2 && a.dim() == 2 && b.dim() == 2, "gemm: 2-D operands expected");
-  TORCH_CHECK((mode == 0 && (epi == 0 || epi == 1)) || (mode == 1 && (epi == 0 || epi == 2)) ||
-                  (mode == 2 && epi == 3),
+  TORCH_CHECK((mode == 0 && (epi == 0 || epi == 1)) ||
+                  (mode == 1 && (epi == 0 || epi == 2 || epi == 4)) || (mode == 2 && epi == 3),
               "gemm: epilogue ", epi, " not available in mode ", mode);
   TORCH_CHECK(dmp::gemm_config_ok((int)mode, (int)cfg), "gemm: config ", cfg,
               " is not available in mode ", mode);
@@ -967,11 +968,12 @@ void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
   }
   const uint16_t* auxp = nullptr;
   if (aux.has_value() && aux->defined()) {
-    TORCH_CHECK(epi == 0 || epi == 2, "gemm: aux only with epilogues 0 / 2");
+    TORCH_CHECK(epi == 0 || epi == 2 || epi == 4, "gemm: aux only with epilogues 0 / 2 / 4");
     same_as_c(*aux, "aux");
     auxp = reinterpret_cast<const uint16_t*>(aux->data_ptr());
   }
   TORCH_CHECK(epi != 2 || auxp != nullptr, "gemm: GELU-backward epilogue needs aux = h");
+  TORCH_CHECK(epi != 4 || auxp != nullptr, "gemm: ReLU-backward epilogue needs aux = the input");
   const uint16_t* biasp = nullptr;
   if (bias.has_value() && bias->defined()) {
     TORCH_CHECK(epi == 0 || epi == 1, "gemm: bias only in the forward epilogues");
@@ -1566,7 +1568,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC KxK / stride S / pad P max pool forward",
         py::arg("x"), py::arg("K"), py::arg("S") = -1, py::arg("P") = 0,
-        py::arg("nchw_out") = false);
+        py::arg("nchw_out") = false, py::arg("relu_in") = false);
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC KxK / stride S / pad P max pool backward",
         py::arg("dy"), py::arg("idx"), py::arg("H"), py::arg("W"), py::arg("K"),
         py::arg("S") = -1, py::arg("P") = 0);

@@ -44,10 +44,16 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr unsigned kOOBg = 0x80000000u;
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_ACC32 = 3 };
+// EPI_DRELU (data gradient): out = aux > 0 ? acc : 0 with aux = the layer's own
+// forward INPUT -- the output of a ReLU (or of a dropout after one), so the
+// data gradient leaves already multiplied by that ReLU's derivative and the
+// producing layer skips its separate mask pass (ops/linear.py)
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_ACC32 = 3, EPI_DRELU = 4 };
 
 // epilogues that may read an aux [M][N] operand (register slots reserved)
-constexpr bool has_aux_slots(int epi) { return epi == EPI_STORE || epi == EPI_DGELU; }
+constexpr bool has_aux_slots(int epi) {
+  return epi == EPI_STORE || epi == EPI_DGELU || epi == EPI_DRELU;
+}
 
 struct GemmArgs {
   const u16* a;
@@ -281,7 +287,7 @@ __global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + rb + j * 16 + 4 * (lane >> 4);
         f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-        if (EPI != EPI_DGELU && g.bias != nullptr && n < g.N) {
+        if (EPI != EPI_DGELU && EPI != EPI_DRELU && g.bias != nullptr && n < g.N) {
           const uint2 raw = *reinterpret_cast<const uint2*>(g.bias + n);
           bv = f32x4{__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
                      __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
@@ -373,7 +379,7 @@ __global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
       // the aux row segments (GELU' pre-activation / addend) are fetched first,
       // so their latency overlaps the LDS staging below
       u32x4_t xa[has_aux_slots(EPI) ? NR : 1];
-      if (!narrow && (EPI == EPI_DGELU || (EPI == EPI_STORE && has_aux))) {
+      if (!narrow && (EPI == EPI_DGELU || EPI == EPI_DRELU || (EPI == EPI_STORE && has_aux))) {
 #pragma unroll
         for (int q = 0; q < (has_aux_slots(EPI) ? NR : 1); ++q)
           xa[q] = __builtin_amdgcn_raw_buffer_load_b128(rsX, o[q], 0, 0);
@@ -419,6 +425,8 @@ __global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
           } else if constexpr (EPI == EPI_GELU) {
             out.v[e] = v.v[e];                                 // h (pre-activation)
             out2.v[e] = f2bf(gelu_tanh(a, nullptr));           // gelu of the stored h
+          } else if constexpr (EPI == EPI_DRELU) {   // xv = the layer's ReLU'd input
+            out.v[e] = bf2f(xv.v[e]) > 0.f ? v.v[e] : (u16)0;
           } else {   // EPI_DGELU: xv = pre-activation h
             float d;
             gelu_tanh(bf2f(xv.v[e]), &d);
@@ -605,7 +613,8 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
         else C[o] += v;
       } else {
         u16* C = reinterpret_cast<u16*>(g.c);
-        const float b = (EPI != EPI_DGELU && g.bias != nullptr) ? bf2f(g.bias[n]) : 0.f;
+        const float b = (EPI != EPI_DGELU && EPI != EPI_DRELU && g.bias != nullptr)
+                            ? bf2f(g.bias[n]) : 0.f;
         if constexpr (EPI == EPI_STORE) {
           const float t = v + b + (g.aux != nullptr ? bf2f(g.aux[o]) : 0.f);
           C[o] = f2bf(g.relu ? fmaxf(t, 0.f) : t);
@@ -613,6 +622,8 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
           const u16 h = f2bf(v + b);
           C[o] = h;
           g.c2[o] = f2bf(gelu_tanh(bf2f(h), nullptr));
+        } else if constexpr (EPI == EPI_DRELU) {
+          C[o] = bf2f(g.aux[o]) > 0.f ? f2bf(v) : (u16)0;
         } else {
           float d;
           gelu_tanh(bf2f(g.aux[o]), &d);
@@ -648,14 +659,20 @@ __global__ void __launch_bounds__(256) gemm_skinny_wgrad_kernel(GemmArgs g, int 
   const int k0 = blockIdx.x * chunk;
   const int rows = min(g.K - k0, chunk);
   if (rows <= 0) return;
-  for (int e = tid; e < rows * M; e += 256) {
-    const int r = e / M, m = e - r * M;
-    As[e] = bf2f(g.a[(long long)(k0 + r) * g.lda + m]);
-  }
-  for (int e = tid; e < rows * N; e += 256) {
-    const int r = e / N, n = e - r * N;
-    Bs[e] = bf2f(g.b[(long long)(k0 + r) * g.ldb + n]);
-  }
+  // (row, column) of element e walked incrementally: one division per thread,
+  // not one per staged element (the loads are independent: all in flight)
+  auto stage = [&](float* dst, const u16* src, int ld, int cols) {
+    const int dr = 256 / cols, dc = 256 - dr * cols;
+    int r = tid / cols, c = tid - r * cols;
+    for (int e = tid; e < rows * cols; e += 256) {
+      dst[e] = bf2f(src[(long long)(k0 + r) * ld + c]);
+      r += dr;
+      c += dc;
+      if (c >= cols) { c -= cols; ++r; }
+    }
+  };
+  stage(As, g.a, g.lda, M);
+  stage(Bs, g.b, g.ldb, N);
   __syncthreads();
   const int MN = M * N;
   float* C = reinterpret_cast<float*>(g.c);
@@ -815,6 +832,7 @@ void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const u
     else launch_mode<false, false, EPI_STORE>(cfg, g, 1, s);
   } else if (mode == 1) {
     if (epi == EPI_DGELU) launch_mode<false, true, EPI_DGELU>(cfg, g, 1, s);
+    else if (epi == EPI_DRELU) launch_mode<false, true, EPI_DRELU>(cfg, g, 1, s);
     else launch_mode<false, true, EPI_STORE>(cfg, g, 1, s);
   } else if (cfg == -2) {
     if ((long long)M * N > kSkinnyMaxOut || M > 256 || N > 1024)

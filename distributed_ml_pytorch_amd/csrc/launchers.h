@@ -61,7 +61,8 @@ void launch_gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStr
 void launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s);
 int maxpool_out(int H, int K, int S, int P);
 void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C,
-                        int K, int S, int P, hipStream_t s, bool nchw_out = false);
+                        int K, int S, int P, hipStream_t s, bool nchw_out = false,
+                        bool relu_in = false);
 void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H,
                         int W, int C, int K, int S, int P, hipStream_t s, bool nchw_dy = false);
 

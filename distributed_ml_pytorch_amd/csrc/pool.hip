@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const u16* __restrict_
                                                           u16* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H,
                                                           int W, int C, int K, int S, int P,
-                                                          int Ho, int Wo) {
+                                                          int Ho, int Wo, int relu_in) {
   const int tpr = C >> 3;
   const long long total = (long long)N * Ho * Wo * tpr;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -89,7 +89,11 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const u16* __restrict_
     }
     bf16x8 o;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o.v[k] = f2bf(best[k]);
+    for (int k = 0; k < 8; ++k) {
+      o.v[k] = f2bf(best[k]);
+      // a ReLU'd input whose window max is 0: relu' = 0 everywhere in it -> no tap
+      if (relu_in && !(best[k] > 0.f)) bi[k] = 255;
+    }
     if constexpr (NCHW_OUT) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) y[((n * C + cg * 8 + k) * Ho + ho) * Wo + wo] = o.v[k];
@@ -157,7 +161,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_c1_kernel(const u16* __restri
                                                              u16* __restrict__ y,
                                                              uint8_t* __restrict__ idx, int N,
                                                              int H, int W, int C, int K, int S,
-                                                             int P, int Ho, int Wo) {
+                                                             int P, int Ho, int Wo, int relu_in) {
   const long long total = (long long)N * Ho * Wo * C;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
@@ -180,7 +184,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_c1_kernel(const u16* __restri
       }
     }
     y[t] = f2bf(best);
-    idx[t] = bi;
+    idx[t] = (relu_in && !(best > 0.f)) ? (uint8_t)255 : bi;
   }
 }
 
@@ -223,21 +227,22 @@ void launch_gap_bwd(const u16* dy, u16* dx, int N, int HW, int C, hipStream_t s)
 int maxpool_out(int H, int K, int S, int P) { return (H + 2 * P - K) / S + 1; }
 
 void launch_maxpool_fwd(const u16* x, u16* y, uint8_t* idx, int N, int H, int W, int C, int K,
-                        int S, int P, hipStream_t s, bool nchw_out) {
+                        int S, int P, hipStream_t s, bool nchw_out, bool relu_in) {
   const int Ho = maxpool_out(H, K, S, P), Wo = maxpool_out(W, K, S, P);
+  const int ri = relu_in ? 1 : 0;
   if (C % 8) {
     const long long n1 = (long long)N * Ho * Wo * C;
     hipLaunchKernelGGL(maxpool_fwd_c1_kernel, dim3(stream_grid(n1, 256)), dim3(256), 0, s, x, y,
-                       idx, N, H, W, C, K, S, P, Ho, Wo);
+                       idx, N, H, W, C, K, S, P, Ho, Wo, ri);
     return;
   }
   const long long total = (long long)N * Ho * Wo * (C / 8);
   if (nchw_out)
     hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(stream_grid(total, 256)), dim3(256), 0, s, x,
-                       y, idx, N, H, W, C, K, S, P, Ho, Wo);
+                       y, idx, N, H, W, C, K, S, P, Ho, Wo, ri);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(stream_grid(total, 256)), dim3(256), 0, s,
-                       x, y, idx, N, H, W, C, K, S, P, Ho, Wo);
+                       x, y, idx, N, H, W, C, K, S, P, Ho, Wo, ri);
 }
 
 void launch_maxpool_bwd(const u16* dy, const uint8_t* idx, u16* dx, int N, int H, int W, int C,

@@ -31,6 +31,7 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from ._ext import native
+from .functional import is_relu_masked, set_nonneg
 from .tuner import TUNER
 
 _NATIVE_ENABLED = True
@@ -298,8 +299,9 @@ class _NativeConv(Function):
             return None, None, None, None, None, None, None, None, dxa, None
         x, w16, y = ctx.saved_tensors
         H, W, stride, pad = ctx.geom
+        masked = is_relu_masked(dy)           # the consumer applied relu'(y) already
         dy = dy.contiguous(memory_format=torch.channels_last)
-        if y is not None:
+        if y is not None and not masked:
             dy = native().relu_bwd(dy, y)
         dx = None
         master = ctx.master
@@ -460,8 +462,9 @@ class _Im2colConv(Function):
         master, bias = ctx.params
         B, CI, H, W, R, S, K, stride, pad = ctx.geom
         CO = master.shape[0]
+        masked = is_relu_masked(dy)
         dy2 = dy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, CO)
-        if y2 is not None:
+        if y2 is not None and not masked:
             dy2 = native().relu_bwd(dy2, y2)
         gw = gb = None
         wants_w = master is not None and master.requires_grad
@@ -669,6 +672,7 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
                                             bool(relu))
             if part is not None:
                 y._dmp_bn_part = part
+            set_nonneg(y, relu)
             return (y, xa) if alias else y
         if master is not None and b is None and not relu and _STEM != "im2col" and \
                 small_conv_supported(x, master, stride, padding, dilation, groups):
@@ -705,6 +709,7 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
                     b16 = b.detach().to(torch.bfloat16).contiguous()
             y = _Im2colConv.apply(x, w16, master, b16, b, _pair(stride)[0], _pair(padding)[0],
                                   bool(relu))
+            set_nonneg(y, relu)
             return (y, x) if alias else y
         if w is None:
             w = master.to(x.dtype)

@@ -38,6 +38,42 @@ def _notify(*ps):
             cb(p)
 
 
+# ----------------------------------------------------- ReLU-mask hand-offs
+# A layer with a fused ReLU (conv / linear epilogue) masks its incoming gradient
+# by relu'(y) in its backward.  When the gradient's producer already applied
+# that mask -- a max-pool over the non-negative ReLU output (a window whose max
+# is <= 0 passes no gradient), or a Linear whose data-gradient epilogue masks
+# by its own ReLU'd input (EPI_DRELU) -- it registers the gradient tensor
+# here, dropout's backward forwards the registration, and the layer skips its
+# mask pass.  The check is by OBJECT identity on a live tensor (weak values):
+# a gradient that autograd accumulated or copied is a different object and is
+# masked as usual, and masking twice would be a no-op anyway.
+import weakref  # noqa: E402
+
+_RELU_MASKED: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDictionary()
+
+
+def mark_relu_masked(t):
+    if t is not None:
+        _RELU_MASKED[id(t)] = t
+    return t
+
+
+def is_relu_masked(t) -> bool:
+    return t is not None and _RELU_MASKED.get(id(t)) is t
+
+
+def nonneg(t) -> bool:
+    """``t`` is known >= 0 (the output of a fused ReLU, or a dropout of one)."""
+    return bool(getattr(t, "_dmp_nonneg", False))
+
+
+def set_nonneg(t, flag: bool = True):
+    if flag and t is not None:
+        t._dmp_nonneg = True
+    return t
+
+
 # --------------------------------------------------------------- shadow weight
 class _ShadowWeight(Function):
     """Use the arena's bf16 shadow of an fp32 master parameter in compute.
@@ -363,18 +399,24 @@ def global_avg_pool(x):
 
 class _MaxPool(Function):
     @staticmethod
-    def forward(ctx, x, k, s, p, nchw_out=False):
+    def forward(ctx, x, k, s, p, nchw_out=False, relu_in=False):
         x = x.contiguous(memory_format=CL)
-        y, idx = native().maxpool_fwd(x, k, s, p, nchw_out)
+        # relu_in: x >= 0 (a fused-ReLU output): a window whose max is <= 0 (all
+        # zeros) records "no tap", so the backward is relu'-masked already
+        y, idx = native().maxpool_fwd(x, k, s, p, nchw_out, relu_in)
         ctx.save_for_backward(idx)
         ctx.meta = (x.shape[2], x.shape[3], k, s, p)
+        ctx.relu_in = relu_in
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
         H, W, k, s, p = ctx.meta
-        return native().maxpool_bwd(dy, idx, H, W, k, s, p), None, None, None, None
+        dx = native().maxpool_bwd(dy, idx, H, W, k, s, p)
+        if ctx.relu_in:
+            mark_relu_masked(dx)
+        return dx, None, None, None, None, None
 
 
 def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0,
@@ -388,7 +430,9 @@ def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0,
             and 1 <= kernel_size <= 15 and stride >= 1 and 0 <= 2 * padding <= kernel_size
             and x.shape[2] + 2 * padding >= kernel_size
             and x.shape[3] + 2 * padding >= kernel_size):
-        return _MaxPool.apply(x, int(kernel_size), int(stride), int(padding), bool(nchw_out))
+        y = _MaxPool.apply(x, int(kernel_size), int(stride), int(padding), bool(nchw_out),
+                           nonneg(x))
+        return set_nonneg(y, nonneg(x))
     return F.max_pool2d(x, kernel_size, stride, padding)
 
 
@@ -429,7 +473,10 @@ class _Dropout(Function):
     @staticmethod
     def backward(ctx, dy):
         (mask,) = ctx.saved_tensors
-        return native().dropout_bwd(dy, mask, float(ctx.p), int(ctx.mode)), None, None, None, None
+        dx = native().dropout_bwd(dy, mask, float(ctx.p), int(ctx.mode))
+        if is_relu_masked(dy):
+            mark_relu_masked(dx)       # a positive scaling keeps the mask valid
+        return dx, None, None, None, None
 
 
 def dropout(x, p: float, training: bool, channelwise: bool = False, state=None, seed: int = 0):
@@ -450,7 +497,7 @@ def dropout(x, p: float, training: bool, channelwise: bool = False, state=None, 
             else:
                 x = x.contiguous()
                 mode = 1
-        return _Dropout.apply(x, p, seed, state, mode)
+        return set_nonneg(_Dropout.apply(x, p, seed, state, mode), nonneg(x))
     if channelwise:
         return F.dropout2d(x, p, True)
     return F.dropout(x, p, True)

@@ -31,7 +31,7 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from ._ext import native
-from .functional import _notify
+from .functional import _notify, is_relu_masked, mark_relu_masked, nonneg, set_nonneg
 from .tuner import TUNER
 
 _GEMM_MODE = os.environ.get("DMP_GEMM", "native")
@@ -297,6 +297,9 @@ class _ArenaLinear(Function):
         ctx.save_for_backward(x2, w16, y if relu else None)
         ctx.params = (w, b)
         ctx.xshape = x.shape
+        # the input is a ReLU output (or a dropout of one): the data gradient's
+        # epilogue applies that ReLU's derivative (EPI_DRELU, mask = input > 0)
+        ctx.x_nonneg = nonneg(x)
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
@@ -304,14 +307,20 @@ class _ArenaLinear(Function):
         x2, w16, y = ctx.saved_tensors
         w, b = ctx.params
         N, K = w16.shape
+        masked = is_relu_masked(dy)
         dy2 = _rows(dy, N)
-        if y is not None:
+        if y is not None and not masked:
             dy2 = native().relu_bwd(dy2, y)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(dy2.shape[0], K, dtype=dy.dtype, device=dy.device)
-            gemm(1, 0, dy2, w16, dx)
+            if ctx.x_nonneg:
+                gemm(1, 4, dy2, w16, dx, aux=x2)
+            else:
+                gemm(1, 0, dy2, w16, dx)
             dx = dx.view(ctx.xshape)
+            if ctx.x_nonneg:
+                mark_relu_masked(dx)
         gw, gb = _weight_grads(dy2, x2, w, b)
         return dx, None, None, gw, gb, None
 
@@ -349,8 +358,8 @@ def linear(x, w, b, relu: bool = False):
     w16 = w._dmp_w16
     b16 = b._dmp_w16 if b is not None else None
     if not _needs_graph(x, w, b):
-        return _infer_linear(x, w16, b16, bool(relu))
-    return _ArenaLinear.apply(x, w16, b16, w, b, bool(relu))
+        return set_nonneg(_infer_linear(x, w16, b16, bool(relu)), relu)
+    return set_nonneg(_ArenaLinear.apply(x, w16, b16, w, b, bool(relu)), relu)
 
 
 # ------------------------------------------------------------ fused ViT MLP

@@ -159,3 +159,49 @@ def test_reference_models_step_matches_fp32(name):
     for (n, p), q, r in zip(model.named_parameters(), ref.parameters(), stock.parameters()):
         ours, theirs = _rel(p.grad, q.grad), _rel(r.grad, q.grad)
         assert ours <= 2 * theirs + 1e-2, (n, ours, theirs)
+
+
+@pytest.mark.parametrize("name,expect", [("lenet", 0), ("alexnet", 2), ("mlp", 0)])
+def test_relu_masks_folded_into_consumers(name, expect):
+    """ReLU derivative hand-offs: a max-pool over a fused-ReLU output (zero
+    windows record no tap) and a Linear whose data-gradient epilogue masks by its
+    ReLU'd input (EPI_DRELU) deliver already-masked gradients, so the producing
+    layer skips its relu_bwd pass.  LeNet: all 4 folded; AlexNet: the two
+    conv -> ReLU -> conv edges (conv3, conv4) still run it; the step still
+    matches PyTorch (test_reference_models_step_matches_fp32)."""
+    from distributed_ml_pytorch_amd.models import build_model
+    from distributed_ml_pytorch_amd.ops._ext import native
+    from distributed_ml_pytorch_amd.parallel.arena import FlatArena
+
+    torch.manual_seed(0)
+    m, shape, nc = build_model(name)
+    m = m.cuda().train()
+    FlatArena(m, device="cuda")
+    x = torch.randn(32, *shape, device="cuda").to(torch.bfloat16)
+    if x.dim() == 4:
+        x = x.contiguous(memory_format=torch.channels_last)
+    nat = native()
+    orig = nat.relu_bwd
+    calls = []
+    nat.relu_bwd = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        m(x).float().square().mean().backward()
+    finally:
+        nat.relu_bwd = orig
+    assert len(calls) == expect, (name, len(calls))
+
+
+def test_gemm_dgrad_relu_epilogue():
+    """EPI_DRELU: dX = (dY W) * (aux > 0), MFMA tiles and the any-shape kernel."""
+    from distributed_ml_pytorch_amd.ops.linear import gemm
+
+    torch.manual_seed(0)
+    for M, N, K in ((256, 384, 512), (64, 84, 120), (64, 10, 84)):
+        dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+        w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+        aux = torch.relu(torch.randn(M, K, device="cuda")).to(torch.bfloat16)
+        dx = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+        gemm(1, 4, dy, w, dx, aux=aux)
+        ref = (dy.float() @ w.float()) * (aux.float() > 0)
+        assert _rel(dx, ref) < 1e-2, (M, N, K)
+        assert bool(((dx == 0) | (aux > 0)).all())
