@@ -59,6 +59,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--max-steps", type=int, default=None)
     p.add_argument("--bucket-mb", type=float, default=32.0)
     p.add_argument("--label-smoothing", type=float, default=0.0)
+    p.add_argument("--no-divergence-check", action="store_true", default=False,
+                   help="keep training when the parameters go non-finite (the reference's "
+                        "behaviour); default: halt with an error at the next log interval")
     p.add_argument("--checkpoint", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--resume", default=None,
@@ -89,7 +92,7 @@ def config_from_args(a) -> TrainConfig:
         log_dir=a.log_dir, checkpoint=a.checkpoint, checkpoint_every=a.checkpoint_every,
         resume=a.resume, ps_resume=a.ps_resume, delta_scale=a.delta_scale,
         ps_worker_timeout=a.ps_worker_timeout, bucket_mb=a.bucket_mb,
-        label_smoothing=a.label_smoothing)
+        label_smoothing=a.label_smoothing, divergence_check=not a.no_divergence_check)
 
 
 def main(argv=None):

@@ -634,66 +634,6 @@ __global__ void __launch_bounds__(256) gemm_small_kernel(GemmArgs g) {
   }
 }
 
-// ------------------------------------------------- skinny weight gradient
-// C[M][N] (fp32, ldc) += sum_k A(k, m) B(k, n), A = [K][lda], B = [K][ldb] (both
-// k-strided), for a SMALL output (M*N <= kSkinnyMaxOut: the LeNet / CIFAR-stem
-// convs' weight gradients over B*OH*OW patch rows, 6 x 75 over 50,176 rows) and
-// a LONG reduction.  The 64x64-tile fallback above spends 89 % of its MACs on
-// padding there and walks 32-row stages with one scalar load per element per
-// stage (~27 us per LeNet conv1 wgrad); here every block reduces TR-row tiles
-// of ITS chunk of k into all M*N outputs held in registers (an output per
-// thread and pass), each tile staged once into LDS as fp32 by all 256 threads,
-// and the block's partial sums leave through one fp32 atomic per output (and
-// per dbias row).  Blocks = enough chunks to cover every CU a few times.
-constexpr int kSkinnyMaxOut = 4096;
-
-// One tile of `chunk` rows per block: every load of the tile is in flight at
-// once (one memory latency per block instead of one per 32-row stage).
-__global__ void __launch_bounds__(256) gemm_skinny_wgrad_kernel(GemmArgs g, int chunk) {
-  constexpr int OPT = kSkinnyMaxOut / 256;                // outputs per thread (max)
-  extern __shared__ float sk_lds[];                       // [chunk][M] A, then [chunk][N] B
-  const int M = g.M, N = g.N;
-  float* As = sk_lds;
-  float* Bs = sk_lds + chunk * M;
-  const int tid = threadIdx.x;
-  const int k0 = blockIdx.x * chunk;
-  const int rows = min(g.K - k0, chunk);
-  if (rows <= 0) return;
-  // (row, column) of element e walked incrementally: one division per thread,
-  // not one per staged element (the loads are independent: all in flight)
-  auto stage = [&](float* dst, const u16* src, int ld, int cols) {
-    const int dr = 256 / cols, dc = 256 - dr * cols;
-    int r = tid / cols, c = tid - r * cols;
-    for (int e = tid; e < rows * cols; e += 256) {
-      dst[e] = bf2f(src[(long long)(k0 + r) * ld + c]);
-      r += dr;
-      c += dc;
-      if (c >= cols) { c -= cols; ++r; }
-    }
-  };
-  stage(As, g.a, g.lda, M);
-  stage(Bs, g.b, g.ldb, N);
-  __syncthreads();
-  const int MN = M * N;
-  float* C = reinterpret_cast<float*>(g.c);
-#pragma unroll
-  for (int q = 0; q < OPT; ++q) {
-    const int o = tid + 256 * q;
-    if (o < MN) {
-      const int m = o / N, n = o - m * N;
-      float t = 0.f;
-#pragma unroll 4
-      for (int r = 0; r < rows; ++r) t = fmaf(As[r * M + m], Bs[r * N + n], t);
-      atomicAdd(C + (long long)m * g.ldc + n, t);
-    }
-  }
-  if (g.dbias != nullptr && tid < M) {
-    float t = 0.f;
-    for (int r = 0; r < rows; ++r) t += As[r * M + tid];
-    atomicAdd(g.dbias + tid, t);
-  }
-}
-
 // C[m][n] (ldc) += sum over the splits of slab[s][m][n]; 4 columns per thread
 // when rows are whole float4s
 __global__ void __launch_bounds__(256) gemm_slab_reduce_kernel(const float* __restrict__ slab,
@@ -799,7 +739,6 @@ int gemm_num_configs() { return kNumCfgs; }
 
 bool gemm_config_ok(int mode, int cfg) {
   if (cfg == -1) return true;
-  if (cfg == -2) return mode == 2;   // skinny weight gradient
   if (cfg < 0 || cfg >= kNumCfgs) return false;
   return cfg_ok(kCfgs[cfg], mode == 2, mode >= 1);
 }
@@ -834,18 +773,6 @@ void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const u
     if (epi == EPI_DGELU) launch_mode<false, true, EPI_DGELU>(cfg, g, 1, s);
     else if (epi == EPI_DRELU) launch_mode<false, true, EPI_DRELU>(cfg, g, 1, s);
     else launch_mode<false, true, EPI_STORE>(cfg, g, 1, s);
-  } else if (cfg == -2) {
-    if ((long long)M * N > kSkinnyMaxOut || M > 256 || N > 1024)
-      throw std::runtime_error("gemm: skinny wgrad needs M*N <= 4096 (M <= 256, N <= 1024)");
-    // ~one block per CU (two when the reduction is short), one tile each, the
-    // tile capped at 64 KiB of fp32 LDS (two resident blocks per CU)
-    const int cap = std::max(8, (int)(65536 / (4 * (M + N))));
-    int chunk = std::max(8, (K + 255) / 256);
-    chunk = std::min(cap, (chunk + 7) / 8 * 8);
-    const int blocks = (K + chunk - 1) / chunk;
-    const size_t lds = (size_t)chunk * (M + N) * sizeof(float);
-    hipLaunchKernelGGL(gemm_skinny_wgrad_kernel, dim3((unsigned)blocks), dim3(256), lds, s, g,
-                       chunk);
   } else {
     // slab split-K only for the MFMA tiles with more than one split
     if (slab != nullptr && splits > 1 && cfg >= 0) g.slab = slab;

@@ -597,8 +597,8 @@ def small_conv_supported(x, weight, stride, padding, dilation, groups) -> bool:
     if st[0] != st[1] or pd[0] != pd[1] or not isinstance(pd[0], int):
         return False
     co, ci, r, s = weight.shape
-    # VALU kernels: a win over MIOpen only while K = R*S*CI is tiny (CIFAR-style
-    # 3x3x3 stems); 7x7 / 11x11 stems stay on MIOpen's MFMA path
+    # VALU kernels: the pick only while K = R*S*CI is tiny (CIFAR-style 3x3x3
+    # stems); the 7x7 stem runs on csrc/stem.hip, 11x11 / 5x5 on im2col + GEMM
     return co % 64 == 0 and r * s * ci <= _SMALL_MAX_K
 
 

@@ -37,13 +37,8 @@ from .tuner import TUNER
 _GEMM_MODE = os.environ.get("DMP_GEMM", "native")
 _BLAS = -1000          # candidate id of the library GEMM (DMP_GEMM=auto only)
 _SMALL = -1            # any-shape fallback kernel
-_SKINNY = -2000        # candidate id of the skinny weight-gradient kernel (cfg -2)
 
 
-def _skinny_ok(mode: int, M: int, N: int, K: int) -> bool:
-    """csrc/gemm.hip gemm_skinny_wgrad_kernel: small output, long reduction
-    (the LeNet convs' / CIFAR-stem weight gradients over B*OH*OW rows)."""
-    return mode == 2 and M * N <= 4096 and M <= 256 and N <= 1024 and K >= 512
 _COLSUM_SCRATCH: dict = {}
 
 
@@ -141,10 +136,9 @@ def _small_split_options(mode: int, K: int):
 
 
 def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bool):
-    skinny = [_SKINNY] if _skinny_ok(mode, M, N, K) else []
     if not ok:
-        return [_enc(_SMALL, s) for s in _small_split_options(mode, K)] + skinny
-    cands = list(skinny)
+        return [_enc(_SMALL, s) for s in _small_split_options(mode, K)]
+    cands = []
     for c in native().gemm_configs():
         cid, bm, bn = c[0], c[1], c[2]
         if not native().gemm_config_ok(mode, cid):
@@ -195,8 +189,7 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
     ok = _mfma_ok(mode, M, N, K, a, b)
     plain = epi == 0 and aux is None and not relu and part is None
     key = ("gemm", mode, epi, M, N, K, bias is not None, aux is not None, dbias is not None,
-           bool(relu)) + (("stats",) if part is not None else ()) + (
-               ("skinny",) if _skinny_ok(mode, M, N, K) else ())   # new candidate: re-tune
+           bool(relu)) + (("stats",) if part is not None else ())
     pick = TUNER.cache.get(key)
     if pick is None:
         cands = _candidates(mode, epi, M, N, K, plain, ok)
@@ -216,9 +209,6 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
             def run(e):
                 if e == _BLAS:
                     _blas(mode, a, b, cs, bias)
-                elif e == _SKINNY:
-                    native().gemm(mode, epi, -2, a, b, cs, c2, bias, aux, ds, 1, relu, None,
-                                  False)
                 else:
                     cfg_e, split_e = _dec(e)
                     ps = torch.zeros_like(part) if part is not None else None
@@ -229,9 +219,6 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
                 pick = _default(mode, M, N, K, ok)
     if pick == _BLAS:
         _blas(mode, a, b, c, bias)
-        return
-    if pick == _SKINNY:
-        native().gemm(mode, epi, -2, a, b, c, c2, bias, aux, dbias, 1, relu, None, False)
         return
     cfg, splits = _dec(pick)
     native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits, relu, part,

@@ -42,6 +42,7 @@ class KernelTuner:
         self.path = os.environ.get("DMP_CONV_TUNE_CACHE")
         self.reps = int(os.environ.get("DMP_CONV_TUNE_REPS", "5"))
         self.rounds = int(os.environ.get("DMP_CONV_TUNE_ROUNDS", "2"))
+        self.spin = int(os.environ.get("DMP_CONV_TUNE_SPIN", "2000000"))   # GPU cycles
         self.new: dict[tuple, int] = {}     # picks made by this process
         for seed in filter(None, os.environ.get("DMP_CONV_TUNE_SEED", "").split(os.pathsep)):
             self.cache.update(self._read(seed))
@@ -75,6 +76,10 @@ class KernelTuner:
                 for c in candidates:
                     a = torch.cuda.Event(enable_timing=True)
                     b = torch.cuda.Event(enable_timing=True)
+                    # the GPU spins while the host enqueues the reps, so they run
+                    # back-to-back: a ~10 us kernel is otherwise timed at the
+                    # host's launch rate and every candidate looks the same
+                    torch.cuda._sleep(self.spin)
                     a.record()
                     for _ in range(self.reps):
                         runner(c)

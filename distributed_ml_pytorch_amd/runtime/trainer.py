@@ -45,6 +45,10 @@ from .dist import DistInfo, preflight
 _LOG = logging.getLogger(__name__)
 
 
+class DivergenceError(RuntimeError):
+    """Training produced non-finite parameters (the log-interval watchdog)."""
+
+
 @dataclass
 class TrainConfig:
     model: str = "alexnet"
@@ -83,6 +87,7 @@ class TrainConfig:
     ps_worker_timeout: float = 0.0    # central PS: drop a worker silent this long (0 = never)
     bucket_mb: float = 32.0
     label_smoothing: float = 0.0
+    divergence_check: bool = True     # halt on non-finite parameters at each log interval
     verbose: bool = True
     extra: dict = field(default_factory=dict)
 
@@ -249,6 +254,17 @@ class Worker:
             return self._gloss, self._ghits
         return self._gloss.clone(), self._ghits.clone()
 
+    def param_norm(self) -> float:
+        """L2 norm of the flat fp32 master parameters: one native reduction over
+        the arena on GPU (csrc/optim.hip sumsq_partial_kernel), the divergence
+        watchdog's probe -- a NaN / inf anywhere in the model shows up here."""
+        flat = self.arena.p32
+        if flat.is_cuda:
+            from ..ops._ext import native
+
+            return math.sqrt(float(native().sumsq(flat)))
+        return float(flat.double().norm())
+
     def train_step(self, x, y, keep: bool = True):
         """One fwd+bwd+update. Returns (loss, hits) as device tensors (no sync).
         ``keep=False``: with hipGraph replay the returned tensors are the graph's
@@ -393,6 +409,11 @@ def run_training(cfg: TrainConfig, info: DistInfo):
             row = log.append(epoch, i, loss)
             if cfg.log_interval and i % cfg.log_interval == 0 and i > 0:
                 row["samples_per_sec"] = meter.rate()
+                row["param_norm"] = w.param_norm()
+                if cfg.divergence_check and not math.isfinite(row["param_norm"]):
+                    raise DivergenceError(
+                        f"rank {info.rank}: non-finite parameters at epoch {epoch} iteration {i} "
+                        f"(loss {float(loss):.4g}); lower --lr or pass --no-divergence-check")
                 if cfg.evaluate:
                     row["test_loss"], row["test_accuracy"] = w.evaluate(test_loader)
                 log.flush_pending()

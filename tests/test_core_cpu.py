@@ -1,4 +1,5 @@
 """CPU tests of the framework core: arena, serialization, ASGD math, models, checkpoint, CLI."""
+import math
 import os
 
 import pytest
@@ -193,6 +194,32 @@ def test_cli_single_process(tmp_path):
     assert res["steps"] == 8
     assert os.path.exists(tmp_path / "log" / "single.csv")
     assert res["test_accuracy"] > 0.3     # learnable synthetic data
+
+
+def test_divergence_watchdog_halts_and_can_be_disabled(tmp_path):
+    """A blown-up learning rate makes the parameters non-finite: the log-interval
+    watchdog (arena norm) halts with DivergenceError; --no-divergence-check keeps
+    the reference's keep-going behaviour and logs the norm column."""
+    import csv
+
+    from distributed_ml_pytorch_amd.cli import main
+    from distributed_ml_pytorch_amd.runtime.trainer import DivergenceError
+
+    def argv(lr, log):
+        return ["--no-distributed", "--model", "mlp", "--epochs", "1", "--n-train", "512",
+                "--n-test", "128", "--log-interval", "4", "--lr", lr,
+                "--log-dir", str(tmp_path / log), "--no-eval"]
+
+    with pytest.raises(DivergenceError):
+        main(argv("1e30", "log"))
+    res = main(argv("1e30", "log") + ["--no-divergence-check"])
+    assert res["steps"] == 8
+    rows = list(csv.DictReader(open(tmp_path / "log" / "single.csv")))
+    norms = [r["param_norm"] for r in rows if r.get("param_norm")]
+    assert norms and not math.isfinite(float(norms[-1]))
+    main(argv("0.05", "ok"))
+    rows = list(csv.DictReader(open(tmp_path / "ok" / "single.csv")))
+    assert all(math.isfinite(float(r["param_norm"])) for r in rows if r.get("param_norm"))
 
 
 def test_synthetic_data_is_learnable():

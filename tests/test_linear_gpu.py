@@ -142,19 +142,22 @@ def test_linear_odd_head_native():
 
 
 @pytest.mark.parametrize("M,N,K,ldb", [(6, 75, 50176, 80), (16, 150, 6400, 152), (64, 27, 9000, 32),
-                                       (10, 84, 4096, 84)])
-def test_skinny_wgrad_kernel(M, N, K, ldb):
-    """Small-output / long-reduction weight gradient (cfg -2, LeNet's convs over
-    B*OH*OW patch rows): dW += dY^T X and dbias += colsum(dY) vs fp32."""
+                                       (10, 84, 4096, 88)])
+@pytest.mark.parametrize("cfg,splits", [(4, 96), (9, 24), (-1, 196)])
+def test_small_output_long_reduction_wgrad(M, N, K, ldb, cfg, splits):
+    """Small-output / long-reduction weight gradient (LeNet's convs over
+    B*OH*OW patch rows; the picks scripts/gemm_shape_sweep.py measures fastest:
+    an MFMA tile split 24-128 ways over k with fp32 atomics, or the any-shape
+    kernel): dW += dY^T X and dbias += colsum(dY) vs fp32, accumulating."""
     from distributed_ml_pytorch_amd.ops._ext import native
 
     torch.manual_seed(0)
-    a = torch.randn(K, M, device="cuda").to(torch.bfloat16)
+    a = torch.randn(K, (M + 7) // 8 * 8, device="cuda").to(torch.bfloat16)[:, :M]
     bfull = torch.randn(K, ldb, device="cuda").to(torch.bfloat16)
     b = bfull[:, :N]
     c = torch.full((M, N), 0.25, device="cuda")
     db = torch.full((M,), -1.0, device="cuda")
-    native().gemm(2, 3, -2, a, b, c, None, None, None, db, 1, False, None, False)
+    native().gemm(2, 3, cfg, a, b, c, None, None, None, db, splits, False, None, False)
     ref = a.float().t() @ b.float() + 0.25
     torch.testing.assert_close(c, ref, rtol=2e-3, atol=2e-3 * float(ref.abs().max()))
     torch.testing.assert_close(db, a.float().sum(0) - 1.0, rtol=2e-3, atol=1e-2)
