@@ -99,6 +99,14 @@ def parse(argv=None):
                     help="class-template amplitude of the time-to-target images (0.05: ~1000 "
                          "steps to loss 0.5 at N=1, profiles/ttl_calibration_r2.txt)")
     ap.add_argument("--ttl-batches", type=int, default=128, help="distinct TTL batches (one dataset, all ranks)")
+    ap.add_argument("--central-check", type=int, default=-1,
+                    help="after the JSON line, at N>1: STEPS of the reference topology (rank 0 "
+                         "= PS, pushes / pulls over the per-pair payload communicators, RCCL on "
+                         "GPUs) with a one-line report on stderr; -1 = 12 when the timed run "
+                         "is not already central, 0 = off")
+    ap.add_argument("--central-check-timeout", type=float, default=150.0,
+                    help="seconds before a stuck central check ends every rank (exit 0: the "
+                         "benchmark line is already out)")
     ap.add_argument("--ttl-compare-sync", type=int, default=1,
                     help="also measure time-to-target of sync all-reduce DP at the same N")
     return ap.parse_args(argv)
@@ -276,6 +284,70 @@ def time_to_target(a, cfg, ctx, mode=None):
     return {"time_to_target_s": round(t, 3), "ttl_steps": steps, "ttl_reached": reached}
 
 
+def _central_check(a, cfg, ctx, steps: int):
+    """The reference's own topology (/root/reference/example/main.py:135-165: one
+    PS process, every other rank a Downpour worker) run for ``steps`` worker steps
+    AFTER the benchmark line: the (PS, worker) payload communicators -- RCCL
+    pairs on GPUs -- carry real pushes and pulls, and rank 0 reports what moved.
+    A watchdog ends a stuck check (every rank exits 0: the measured line is
+    already printed), so it can never cost the benchmark its result."""
+    import threading
+    from dataclasses import replace
+
+    from distributed_ml_pytorch_amd.parallel.server import make_ps_groups
+    from distributed_ml_pytorch_amd.runtime.dist import preflight
+    from distributed_ml_pytorch_amd.runtime.trainer import Worker, run_server
+    from distributed_ml_pytorch_amd.utils.data import DeviceBatchPool
+
+    info = ctx.info
+
+    def _expire():
+        print(f"[central-check] rank {info.rank}: no result after "
+              f"{a.central_check_timeout:.0f} s, exiting", file=sys.stderr, flush=True)
+        os._exit(0)
+
+    dog = threading.Timer(a.central_check_timeout, _expire)
+    dog.daemon = True
+    dog.start()
+    t0 = time.perf_counter()
+    payload = "rccl" if info.backend == "nccl" else "gloo"
+    groups = make_ps_groups(0, payload)
+    pf = preflight(info, ctx.cpu_group, groups[1], 0)
+    ccfg = replace(cfg, ps="central", delta_scale="sum", n_push=2, n_pull=2, seed=2000)
+    mine = None
+    if info.rank == 0:
+        st = run_server(ccfg, info, groups)
+        mine = {k: st[k] for k in ("version", "counts", "bytes_in", "bytes_out",
+                                   "staleness_max") if k in st}
+    else:
+        w = Worker(ccfg, info, groups)
+        w.enable_graph(bool(a.graph))
+        pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device, n_batches=2,
+                               dtype=w.compute_dtype, seed=info.rank + 50)
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            x, y = pool.next()
+            loss, _ = w.train_step(x, y)
+        lv = float(loss.float().item())
+        ms = 1e3 * (time.perf_counter() - t1) / steps
+        st = w.opt.client.stats() if hasattr(w.opt, "client") else {}
+        mine = {"rank": info.rank, "ms_per_step": round(ms, 3), "loss": round(lv, 4),
+                "hip_graph": bool(getattr(w, "use_graph", False) and w.graph is not None),
+                "pushes": st.get("pushes"), "pulls": st.get("pulls")}
+        w.finish()
+        del w
+    got = ctx.gather(mine)
+    dog.cancel()
+    if info.rank == 0:
+        ps, workers = got[0], got[1:]
+        ok = all(r is not None and r["loss"] == r["loss"] for r in workers) and \
+            int(ps.get("version", 0)) > 0
+        rep = {"ok": ok, "payload": payload, "steps": steps, "pairs_pinged": pf["pairs_pinged"],
+               "rccl_ranks": pf["rccl_ranks"], "seconds": round(time.perf_counter() - t0, 2),
+               "ps": ps, "workers": workers}
+        print("[central-check] " + json.dumps(rep), file=sys.stderr, flush=True)
+
+
 def run(a):
     import torch
 
@@ -439,6 +511,9 @@ def run(a):
         if ttl_sync is not None:
             out["ttl_sync_dp"] = ttl_sync
         print(json.dumps(out), flush=True)
+    steps = a.central_check if a.central_check >= 0 else (12 if not ctx.central else 0)
+    if steps > 0 and world > 1 and a.mode == "asgd":
+        _central_check(a, cfg, ctx, steps)
     shutdown()
 
 

@@ -48,6 +48,14 @@ def test_bench_self_spawns_n_ranks():
     assert out["config"]["global_batch"] == 32
     assert out["backend"] == "gloo" and out["dtype"].startswith("fp32")
     assert "sharded" in out["config"]["parallelism"]
+    # after the line: the reference topology (1 PS + 3 workers) over the pair
+    # payload communicators, reported on stderr
+    chk = [ln for ln in r.stderr.splitlines() if ln.startswith("[central-check] ")]
+    assert len(chk) == 1, r.stderr[-3000:]
+    rep = json.loads(chk[0].split(" ", 1)[1])
+    assert rep["ok"] and rep["payload"] == "gloo" and len(rep["workers"]) == 3
+    assert rep["ps"]["counts"]["GradientUpdate"] == 3 * 6     # 12 steps / n_push 2, 3 workers
+    assert all(wk["pushes"] == 6 and wk["pulls"] == 6 for wk in rep["workers"])
 
 
 def test_bench_central_ps_three_ranks():
