@@ -216,18 +216,27 @@ def _serve(a, cfg, ctx, sessions: int):
 
 
 def _timed_steps(w, pool, steps, warmup, ctx):
+    trace = os.environ.get("DMP_BENCH_LOSSES") == "1"
+    seen = []
     for _ in range(warmup):
         x, y = pool.next()
         loss, _ = w.train_step(x, y)
+        if trace:
+            seen.append(loss)
     ctx.worker_barrier()
     _sync()
     w.timer.reset()
     t0 = time.perf_counter()
     for _ in range(steps):
         x, y = pool.next()
-        loss, _ = w.train_step(x, y, keep=False)   # only the last loss is read
+        loss, _ = w.train_step(x, y, keep=not trace)   # only the last loss is read
+        if trace:
+            seen.append(loss)
     _sync()
     ctx.worker_barrier()
+    if trace:
+        print("[trace] losses " + " ".join(f"{float(v.float()):.3g}" for v in seen)
+              + f" |p| {w.param_norm():.4f}", file=sys.stderr, flush=True)
     return time.perf_counter() - t0, loss
 
 

@@ -530,12 +530,15 @@ void pad_rows_batched(Tensor src, Tensor dst, Tensor table, int64_t max_elems) {
                                (int)table.size(0), (long long)max_elems, cur_stream());
 }
 
-// hipMemsetAsync zero of a dense tensor (graph-capturable memset node; the grad
-// arena zeroing every step: no ATen fill kernel)
+// Native zero fill of a dense tensor (the grad arena at every step start: no
+// ATen fill kernel).  Deliberately a kernel and not hipMemsetAsync: a captured
+// memset node raced with the previous graph replay (csrc/optim.hip zero_fill).
 void zero_(Tensor t) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_: a contiguous GPU tensor");
-  TORCH_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream()) ==
-                  hipSuccess, "zero_: hipMemsetAsync failed");
+  const long long bytes = (long long)t.numel() * t.element_size();
+  TORCH_CHECK(bytes % 4 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "zero_: a 16-B aligned tensor of whole dwords");
+  dmp::launch_zero_fill(t.data_ptr(), bytes, cur_stream());
 }
 
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,

@@ -22,6 +22,7 @@ void launch_pull_land_bf16(float* p, const uint16_t* src, const float* acc, uint
 void launch_push_handoff(float* acc, float* out32, uint16_t* out16, long long n, hipStream_t s);
 void launch_cast_f32_bf16(const float* src, uint16_t* dst, long long n, hipStream_t s);
 int launch_sumsq_partial(const float* x, float* partial, long long n, hipStream_t s);
+void launch_zero_fill(void* p, long long bytes, hipStream_t s);
 
 // xent.hip
 void launch_softmax_xent_bf16(const uint16_t* logits, const int64_t* labels, uint16_t* dlogits,

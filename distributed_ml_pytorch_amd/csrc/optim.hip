@@ -192,7 +192,31 @@ __global__ void __launch_bounds__(256) sumsq_partial_kernel(
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// Zero fill of a dense buffer, 16 B per lane (the grad arena at every step
+// start).  A kernel, not hipMemsetAsync: a memset node captured into the step's
+// hipGraph was NOT ordered behind the previous replay's kernels on this stack
+// (ROCm 7.x): back-to-back replays without a host sync zeroed the arena while
+// the previous step's weight-gradient atomics / fused update still used it, and
+// training went non-finite within tens of steps (scripts/nan_hunt.py A/B:
+// 3 of 3 memset runs diverged at least once, 0 of 6 with a kernel).
+__global__ void __launch_bounds__(256) zero_fill_kernel(float4* __restrict__ x, long long n4,
+                                                         float* __restrict__ tail, int ntail) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float4 z = {0.f, 0.f, 0.f, 0.f};
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) x[i] = z;
+  if (blockIdx.x == 0 && (int)threadIdx.x < ntail) tail[threadIdx.x] = 0.f;
+}
+
 // ---------------------------------------------------------------- launchers
+void launch_zero_fill(void* p, long long bytes, hipStream_t s) {
+  // bytes % 4 == 0 and 16-B aligned base (torch allocations); the < 16-B tail
+  // is handled by block 0
+  const long long n4 = bytes / 16;
+  const int ntail = (int)((bytes - n4 * 16) / 4);
+  hipLaunchKernelGGL(zero_fill_kernel, dim3(stream_grid(n4 > 0 ? n4 : 1, 256)), dim3(256), 0, s,
+                     (float4*)p, n4, (float*)p + n4 * 4, ntail);
+}
+
 void launch_asgd_fused_step(const float* g, float* p, float* acc, float* mom, u16* w16,
                             long long n, float lr, float wd, float momentum, float dampening,
                             bool nesterov, hipStream_t s) {

@@ -202,7 +202,7 @@ class FlatArena:
             if self.g32.is_cuda:
                 from ..ops._ext import native
 
-                native().zero_(self.g32)      # a memset node, not an ATen fill kernel
+                native().zero_(self.g32)      # native fill kernel (not a graph memset node)
             else:
                 self.g32.zero_()
 

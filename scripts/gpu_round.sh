@@ -11,7 +11,7 @@ STAGE=${1:-all}
 BENCH_ARGS=${BENCH_ARGS:-"--steps 30 --warmup 10"}
 
 if [[ "$STAGE" == all || "$STAGE" == tests ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; tail -25 gpurun_out/pytest_gpu.log; echo "pytest rc=$rc"
   ok_rc $rc || exit $rc
 fi
