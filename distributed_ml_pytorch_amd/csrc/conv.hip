@@ -506,6 +506,152 @@ struct HaloGeom {
 
 constexpr int kHaloAPW = 8;   // max halo DMA instructions per wave per stage
 
+// Epilogue of the halo tiles (forward layout: output row m = pixel m): bias
+// (fwd), residual gradient addend (FLIP), BN partial sums (STATS) -- as
+// conv_igemm_kernel.  Wave (wm, wn) holds TM x TN 16x16 D^T fragments; the
+// LDS at lds_h is free (the caller synchronised after its last stage read).
+template <int BM, int BN, int WM, int WN, bool FLIP, bool STATS, int TM, int TN>
+__device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM][TN], long long m0,
+                                              int n0, int wm, int wn, int tid, int lane,
+                                              u16* lds_h) {
+  constexpr int NW = WM * WN;
+  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+  const long long Mtot = (long long)a.B * a.OH * a.OW;
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.y, 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  const bool add_in = FLIP && a.addend != nullptr;
+  const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  constexpr bool BNB = FLIP && STATS;   // fused BN(+ReLU) backward
+  const __amdgpu_buffer_rsrc_t rsBx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNB ? a.bnx : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsBm = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNB && (a.bnrelu == 1 || a.bnrelu == 3) ? a.bnmask : a.y), 0,
+      (int)((a.bnrelu == 3 ? 1LL : 16LL) * Mtot * a.CO / 8), 0x00020000);
+  float bj[TN][4];
+  bool nok[TN];
+  // BNB: per-channel mean | scale | shift of the BN (channels n..n+3 of tile j)
+  float bmu[BNB ? TN : 1][4], bsc[BNB ? TN : 1][4], bsh[BNB ? TN : 1][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+    nok[j] = n < a.CO;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bj[j][r] = (!FLIP && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
+      if constexpr (BNB) {
+        const int ch = nok[j] ? n + r : 0;
+        bmu[j][r] = a.bnstat[ch];
+        bsc[j][r] = a.bnrelu == 2 ? a.bnstat[2 * a.CO + ch] : 0.f;
+        bsh[j][r] = a.bnrelu == 2 ? a.bnstat[3 * a.CO + ch] : 0.f;
+      }
+    }
+  }
+  float s_sum[TN][4], s_sq[TN][4];
+  if (STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s_sum[j][r] = 0.f; s_sq[j][r] = 0.f; }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const long long m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+    const bool mok = m < Mtot;
+    const unsigned rowoff = 2u * (unsigned)(m * a.CO);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+      const bool ok = mok && nok[j];
+      float ad[4] = {0.f, 0.f, 0.f, 0.f};
+      if (add_in) {
+        const unsigned aoff = a.addend_sub ? 2u * (unsigned)(m * a.CO) : rowoff;
+        const u32x2_t av =
+            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? aoff + 2u * n : kOOB, 0, 0);
+        ad[0] = __uint_as_float(av.x << 16);
+        ad[1] = __uint_as_float(av.x & 0xffff0000u);
+        ad[2] = __uint_as_float(av.y << 16);
+        ad[3] = __uint_as_float(av.y & 0xffff0000u);
+      }
+      float xb[4] = {0.f, 0.f, 0.f, 0.f}, mk[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BNB) {
+        const u32x2_t xv = __builtin_amdgcn_raw_buffer_load_b64(rsBx, ok ? rowoff + 2u * n : kOOB, 0, 0);
+        xb[0] = bnb_lo(xv.x); xb[1] = bnb_hi(xv.x); xb[2] = bnb_lo(xv.y); xb[3] = bnb_hi(xv.y);
+        if (a.bnrelu == 1) {
+          const u32x2_t mv =
+              __builtin_amdgcn_raw_buffer_load_b64(rsBm, ok ? rowoff + 2u * n : kOOB, 0, 0);
+          mk[0] = bnb_lo(mv.x); mk[1] = bnb_hi(mv.x); mk[2] = bnb_lo(mv.y); mk[3] = bnb_hi(mv.y);
+        } else if (a.bnrelu == 3) {
+          // byte (pixel, n / 8) of the bit mask; bits (n & 4) .. +3 are channels n .. n+3
+          const unsigned bits = __builtin_amdgcn_raw_buffer_load_b8(
+              rsBm, ok ? (rowoff >> 4) + (unsigned)(n >> 3) : kOOB, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mk[r] = (bits >> ((n & 4) + r)) & 1u ? 1.f : 0.f;
+        }
+      }
+      u16 hv[4];
+      float v[4], t[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        t[r] = acc[i][j][r] + bj[j][r] + ad[r];
+        if (!FLIP && a.relu) t[r] = fmaxf(t[r], 0.f);
+        if constexpr (BNB)
+          t[r] = bnb_on(a.bnrelu, xb[r], mk[r], bsc[j][r], bsh[j][r]) ? t[r] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hv[r] = f2bf(t[r]);
+        v[r] = bf2f(hv[r]);
+      }
+      const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
+      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
+      if (STATS) {
+        const float keep = ok ? 1.f : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = v[r] * keep;
+          s_sum[j][r] += x;
+          if constexpr (BNB) s_sq[j][r] += x * (xb[r] - bmu[j][r]);
+          else s_sq[j][r] += x * x;
+        }
+      }
+    }
+  }
+  if (STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s_sum[j][r] = row_sum16(s_sum[j][r]);
+        s_sq[j][r] = row_sum16(s_sq[j][r]);
+      }
+    float* red = reinterpret_cast<float*>(lds_h);   // [WM][BN] sums, then [WM][BN] squares
+    if ((lane & 15) == 15) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = wn * (BN / WN) + j * 16 + 4 * (lane >> 4) + r;
+          red[wm * BN + nl] = s_sum[j][r];
+          red[WM * BN + wm * BN + nl] = s_sq[j][r];
+        }
+    }
+    __syncthreads();
+    for (int nl = tid; nl < BN; nl += 64 * NW) {
+      const int n = n0 + nl;
+      if (n < a.CO) {
+        float ss = 0.f, qq = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) { ss += red[w * BN + nl]; qq += red[WM * BN + w * BN + nl]; }
+        if (BNB) qq *= a.bnstat[a.CO + n];   // sum dz * (x - mean) -> sum dz * xhat
+        const int slot = (blockIdx.x + blockIdx.z * gridDim.x) % kBnSlots;
+        atomicAdd(a.part + (long long)slot * a.CO + n, ss);
+        atomicAdd(a.part + (long long)(kBnSlots + slot) * a.CO + n, qq);
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int BK, int WM, int WN, int NS, bool FLIP, bool STATS>
 __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, HaloGeom hg) {
   constexpr int NW = WM * WN;
@@ -666,144 +812,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
     }
   }
   __syncthreads();   // all stage reads done before the epilogue reuses LDS
-
-  // epilogue (forward layout: output row m = pixel m): bias (fwd), residual
-  // gradient addend (FLIP), BN partial sums (STATS) -- as conv_igemm_kernel
-  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-  const long long Mtot = (long long)a.B * a.OH * a.OW;
-  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.y, 0, (int)(2LL * Mtot * a.CO), 0x00020000);
-  const bool add_in = FLIP && a.addend != nullptr;
-  const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
-  constexpr bool BNB = FLIP && STATS;   // fused BN(+ReLU) backward
-  const __amdgpu_buffer_rsrc_t rsBx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(BNB ? a.bnx : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsBm = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(BNB && (a.bnrelu == 1 || a.bnrelu == 3) ? a.bnmask : a.y), 0,
-      (int)((a.bnrelu == 3 ? 1LL : 16LL) * Mtot * a.CO / 8), 0x00020000);
-  float bj[TN][4];
-  bool nok[TN];
-  // BNB: per-channel mean | scale | shift of the BN (channels n..n+3 of tile j)
-  float bmu[BNB ? TN : 1][4], bsc[BNB ? TN : 1][4], bsh[BNB ? TN : 1][4];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
-    nok[j] = n < a.CO;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      bj[j][r] = (!FLIP && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
-      if constexpr (BNB) {
-        const int ch = nok[j] ? n + r : 0;
-        bmu[j][r] = a.bnstat[ch];
-        bsc[j][r] = a.bnrelu == 2 ? a.bnstat[2 * a.CO + ch] : 0.f;
-        bsh[j][r] = a.bnrelu == 2 ? a.bnstat[3 * a.CO + ch] : 0.f;
-      }
-    }
-  }
-  float s_sum[TN][4], s_sq[TN][4];
-  if (STATS) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { s_sum[j][r] = 0.f; s_sq[j][r] = 0.f; }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const long long m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
-    const bool mok = m < Mtot;
-    const unsigned rowoff = 2u * (unsigned)(m * a.CO);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
-      const bool ok = mok && nok[j];
-      float ad[4] = {0.f, 0.f, 0.f, 0.f};
-      if (add_in) {
-        const unsigned aoff = a.addend_sub ? 2u * (unsigned)(m * a.CO) : rowoff;
-        const u32x2_t av =
-            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? aoff + 2u * n : kOOB, 0, 0);
-        ad[0] = __uint_as_float(av.x << 16);
-        ad[1] = __uint_as_float(av.x & 0xffff0000u);
-        ad[2] = __uint_as_float(av.y << 16);
-        ad[3] = __uint_as_float(av.y & 0xffff0000u);
-      }
-      float xb[4] = {0.f, 0.f, 0.f, 0.f}, mk[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (BNB) {
-        const u32x2_t xv = __builtin_amdgcn_raw_buffer_load_b64(rsBx, ok ? rowoff + 2u * n : kOOB, 0, 0);
-        xb[0] = bnb_lo(xv.x); xb[1] = bnb_hi(xv.x); xb[2] = bnb_lo(xv.y); xb[3] = bnb_hi(xv.y);
-        if (a.bnrelu == 1) {
-          const u32x2_t mv =
-              __builtin_amdgcn_raw_buffer_load_b64(rsBm, ok ? rowoff + 2u * n : kOOB, 0, 0);
-          mk[0] = bnb_lo(mv.x); mk[1] = bnb_hi(mv.x); mk[2] = bnb_lo(mv.y); mk[3] = bnb_hi(mv.y);
-        } else if (a.bnrelu == 3) {
-          // byte (pixel, n / 8) of the bit mask; bits (n & 4) .. +3 are channels n .. n+3
-          const unsigned bits = __builtin_amdgcn_raw_buffer_load_b8(
-              rsBm, ok ? (rowoff >> 4) + (unsigned)(n >> 3) : kOOB, 0, 0);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) mk[r] = (bits >> ((n & 4) + r)) & 1u ? 1.f : 0.f;
-        }
-      }
-      u16 hv[4];
-      float v[4], t[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        t[r] = acc[i][j][r] + bj[j][r] + ad[r];
-        if (!FLIP && a.relu) t[r] = fmaxf(t[r], 0.f);
-        if constexpr (BNB)
-          t[r] = bnb_on(a.bnrelu, xb[r], mk[r], bsc[j][r], bsh[j][r]) ? t[r] : 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        hv[r] = f2bf(t[r]);
-        v[r] = bf2f(hv[r]);
-      }
-      const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
-      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
-      if (STATS) {
-        const float keep = ok ? 1.f : 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x = v[r] * keep;
-          s_sum[j][r] += x;
-          if constexpr (BNB) s_sq[j][r] += x * (xb[r] - bmu[j][r]);
-          else s_sq[j][r] += x * x;
-        }
-      }
-    }
-  }
-  if (STATS) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s_sum[j][r] = row_sum16(s_sum[j][r]);
-        s_sq[j][r] = row_sum16(s_sq[j][r]);
-      }
-    float* red = reinterpret_cast<float*>(lds_h);   // [WM][BN] sums, then [WM][BN] squares
-    if ((lane & 15) == 15) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int nl = wn * (BN / WN) + j * 16 + 4 * (lane >> 4) + r;
-          red[wm * BN + nl] = s_sum[j][r];
-          red[WM * BN + wm * BN + nl] = s_sq[j][r];
-        }
-    }
-    __syncthreads();
-    for (int nl = tid; nl < BN; nl += 64 * NW) {
-      const int n = n0 + nl;
-      if (n < a.CO) {
-        float ss = 0.f, qq = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) { ss += red[w * BN + nl]; qq += red[WM * BN + w * BN + nl]; }
-        if (BNB) qq *= a.bnstat[a.CO + n];   // sum dz * (x - mean) -> sum dz * xhat
-        const int slot = (blockIdx.x + blockIdx.z * gridDim.x) % kBnSlots;
-        atomicAdd(a.part + (long long)slot * a.CO + n, ss);
-        atomicAdd(a.part + (long long)(kBnSlots + slot) * a.CO + n, qq);
-      }
-    }
-  }
+  halo_epilogue<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h);
 }
 
 // ------------------------------------ persistent 3x3 halo tiles, 64 channels
