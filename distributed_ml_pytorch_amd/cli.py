@@ -62,6 +62,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-divergence-check", action="store_true", default=False,
                    help="keep training when the parameters go non-finite (the reference's "
                         "behaviour); default: halt with an error at the next log interval")
+    p.add_argument("--deterministic", action="store_true", default=False,
+                   help="bitwise-reproducible debugging mode (e.g. for asgd-vs-sync "
+                        "differences): fp32 compute on PyTorch's deterministic kernels, no "
+                        "atomics-based split reductions (see runtime/determinism.py)")
     p.add_argument("--checkpoint", default=None)
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--resume", default=None,
@@ -92,7 +96,8 @@ def config_from_args(a) -> TrainConfig:
         log_dir=a.log_dir, checkpoint=a.checkpoint, checkpoint_every=a.checkpoint_every,
         resume=a.resume, ps_resume=a.ps_resume, delta_scale=a.delta_scale,
         ps_worker_timeout=a.ps_worker_timeout, bucket_mb=a.bucket_mb,
-        label_smoothing=a.label_smoothing, divergence_check=not a.no_divergence_check)
+        label_smoothing=a.label_smoothing, divergence_check=not a.no_divergence_check,
+        deterministic=a.deterministic)
 
 
 def main(argv=None):

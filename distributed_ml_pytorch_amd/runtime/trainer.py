@@ -40,6 +40,7 @@ from ..parallel.server import ParameterServer, make_ps_groups
 from ..utils import checkpoint as ckpt
 from ..utils.data import get_datasets, make_loaders
 from ..utils.metrics import IterationLog, StepTimer, Throughput, classification_report
+from .determinism import enable_determinism
 from .dist import DistInfo, preflight
 
 _LOG = logging.getLogger(__name__)
@@ -88,6 +89,7 @@ class TrainConfig:
     bucket_mb: float = 32.0
     label_smoothing: float = 0.0
     divergence_check: bool = True     # halt on non-finite parameters at each log interval
+    deterministic: bool = False       # bitwise-reproducible debug mode (runtime/determinism.py)
     verbose: bool = True
     extra: dict = field(default_factory=dict)
 
@@ -105,6 +107,8 @@ class Worker:
         :class:`~..parallel.clients.SharedPSClient` of the virtual-worker runner)."""
         self.cfg = cfg
         self.info = info
+        if cfg.deterministic:
+            cfg = self.cfg = enable_determinism(cfg)
         torch.manual_seed(cfg.seed + info.rank)
         self.device = info.device if (cfg.cuda and info.device.type == "cuda") else \
             torch.device("cpu")

@@ -275,3 +275,21 @@ def test_fused_sgd_dampening_matches_torch_sgd():
             o.step()
     for p, q in zip(m.parameters(), ref.parameters()):
         torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_deterministic_flag_plumbing():
+    """--deterministic reaches the worker: PyTorch deterministic kernels on, fp32 compute."""
+    from distributed_ml_pytorch_amd.cli import build_parser, config_from_args
+    from distributed_ml_pytorch_amd.runtime.dist import DistInfo
+    from distributed_ml_pytorch_amd.runtime.trainer import Worker
+
+    a = build_parser().parse_args(["--model", "mlp", "--no-distributed", "--deterministic"])
+    cfg = config_from_args(a)
+    assert cfg.deterministic
+    try:
+        w = Worker(cfg, DistInfo())
+        assert torch.are_deterministic_algorithms_enabled()
+        assert w.cfg.dtype == "fp32" and w.compute_dtype == torch.float32
+    finally:
+        torch.use_deterministic_algorithms(False)
+        torch.backends.cudnn.deterministic = False

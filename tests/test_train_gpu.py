@@ -297,3 +297,35 @@ def test_rccl_world1_device_async_shards_and_bf16_wire():
         assert st["payload"] == "rccl"
     finally:
         dist.destroy_process_group()
+
+
+def _det_run(model, steps=6, mode="asgd", graph=False):
+    w = _worker(model, mode=mode, batch=16, n_push=2, n_pull=3, deterministic=True)
+    if graph:
+        w.enable_graph(True)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(16, *w.input_shape, generator=g)
+    y = torch.randint(0, w.num_classes, (16,), generator=g)
+    x, y = w.prepare(x, y)
+    losses = [float(w.train_step(x, y)[0].float()) for _ in range(steps)]
+    w.finish()
+    torch.cuda.synchronize()
+    return losses, w.arena.p32.clone(), w.compute_dtype
+
+
+@pytest.mark.parametrize("model,mode", [("resnet18", "asgd"), ("vit_tiny", "sync")])
+def test_deterministic_mode_is_bitwise_reproducible(model, mode):
+    """--deterministic: two runs of the same steps give bitwise-equal losses and
+    parameters (runtime/determinism.py; the bf16 native path sums split reductions
+    with fp32 atomics and is only reproducible to rounding)."""
+    try:
+        l1, p1, dt = _det_run(model, mode=mode)
+        l2, p2, _ = _det_run(model, mode=mode)
+        assert torch.are_deterministic_algorithms_enabled()
+    finally:
+        torch.use_deterministic_algorithms(False)
+        torch.backends.cudnn.deterministic = False
+    assert dt == torch.float32
+    assert all(l == l for l in l1), l1
+    assert l1 == l2, (l1, l2)
+    assert torch.equal(p1, p2)
