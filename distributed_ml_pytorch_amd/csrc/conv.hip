@@ -670,8 +670,13 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   const int n0 = blockIdx.y * BN;
   const int H = a.GH, W = a.GW, C = a.CI, TH = hg.TH, HW2 = W + 2;
   const int img = H * W;
-  const int b0 = (int)(m0 / img), h0 = (int)(m0 - (long long)b0 * img) / W;
+  // (32-bit: M * C < 2^31 by the host checks; a 64-bit division is ~100 instructions)
+  const int b0 = (int)m0 / img, h0 = ((int)m0 - b0 * img) / W;
   const int per_img = (TH + 2) * HW2;
+  // in-tile index math by float reciprocal (small_divmod): the integer
+  // division sequences were ~2/3 of the ~500-VALU per-block prologue
+  const float rcp_pi = 1.f / (float)per_img, rcp_w2 = 1.f / (float)HW2;
+  const float rcp_tw = 1.f / (float)(TH * W), rcp_w = 1.f / (float)W;
 
   // halo DMA slots: lane's row of each 1-KiB piece -> (image, h, w) of the
   // source pixel; positions outside the image (or past the batch) read zeros
@@ -680,8 +685,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   for (int j = 0; j < kHaloAPW; ++j) {
     const int ins = wid + j * NW;
     const int row = ins * RPI + lane / CPR;
-    const int tb = row / per_img, rem = row - tb * per_img;
-    const int hh = rem / HW2, ww = rem - hh * HW2;
+    int tb, rem, hh, ww;
+    small_divmod(row, per_img, rcp_pi, tb, rem);
+    small_divmod(rem, HW2, rcp_w2, hh, ww);
     const int b = b0 + tb, h = h0 - 1 + hh, w = ww - 1;
     const bool ok = ins < hg.A_INS && row < hg.HROWS && b < a.B && (unsigned)h < (unsigned)H &&
                     (unsigned)w < (unsigned)W;
@@ -732,8 +738,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
-    const int tb = ml / (TH * W), r2 = ml - tb * TH * W;
-    const int th = r2 / W, tw = r2 - th * W;
+    int tb, r2, th, tw;
+    small_divmod(ml, TH * W, rcp_tw, tb, r2);
+    small_divmod(r2, W, rcp_w, th, tw);
     hrow[i] = (tb * (TH + 2) + th) * HW2 + tw;
   }
   int offB[BK / 32];

@@ -354,37 +354,58 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
   const int img = H * W;
   const int P = (int)a.P;
 
-  // dY DMA slots (fixed per lane): row of the tile, swizzled source column
-  int d_row[D_PW], d_off[D_PW];
+  // DMA slots, fixed per lane: byte offsets RELATIVE to the tile's first pixel.
+  // dY: row of the tile + swizzled source column.  X: staged row -> (image in
+  // tile tb, source row dh relative to the tile's first row h0, column w); a
+  // row that is outside the image for every tile (column halo, rows past the
+  // staged image, and with whole-image tiles the row halo) holds kOOBw, and
+  // the halo row above the tile wraps below 0 (correct modulo 2^32 once the
+  // tile's base offset is added).  Interior tiles then issue every piece with
+  // ONE v_add (kOOBw + base stays >= 2^31, past the descriptor's bound); only
+  // tiles touching an image edge or the end of P test rows per lane.  (Per-tile
+  // integer divisions and the per-piece decode/compare chain were ~2/3 of the
+  // kernel's VALU: 4.1 VALU per MFMA, issue-bound, profiles/conv_kernels_r2.txt.)
+  int d_row[D_PW];
+  unsigned d_rel[D_PW];
 #pragma unroll
   for (int j = 0; j < D_PW; ++j) {
     const int row = (wid + j * NW) * 8 + lane / 8, pch = lane % 8;
     d_row[j] = row;
-    d_off[j] = row * CO + co0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8;
+    d_rel[j] = 2u * (unsigned)(row * CO + co0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8);
   }
-  // X DMA slots: staged row -> element offset relative to the tile's first
-  // pixel (x_off) + {valid, image in tile, source row - h0} (x_inf)
-  int x_off[kWhXPW];
-  unsigned x_inf[kWhXPW];
+  const bool whole_img = TH == H;   // tiles of whole images: h0 == 0 for every tile
+  unsigned x_rel[kWhXPW];
+  int x_dh[kWhXPW], x_tb[kWhXPW];
 #pragma unroll
   for (int j = 0; j < kWhXPW; ++j) {
-    x_off[j] = 0;
-    x_inf[j] = 0;
+    x_rel[j] = kOOBw;
+    x_dh[j] = 0;
+    x_tb[j] = 0;
     if (j < XPW) {
       const int row = (wid + j * NW) * 8 + lane / 8, pch = lane % 8;
       const int tb = row / (THX * W2), rem = row - tb * THX * W2;
       const int th = rem / W2, w = rem - th * W2 - 1;
       const int dh = th - 1 + r0;
-      const bool ok = row < hg.XROWS && tb < hg.TB && (unsigned)w < (unsigned)W;
-      x_off[j] = (tb * img + dh * W + w) * C + ci0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) +
-                 (pch & 1) * 8;
-      x_inf[j] = (ok ? 0x80000000u : 0u) | ((unsigned)tb << 16) | ((unsigned)(dh + 64) << 8);
+      const bool ok = row < hg.XROWS && tb < hg.TB && (unsigned)w < (unsigned)W &&
+                      (!whole_img || (unsigned)dh < (unsigned)H);
+      if (ok)
+        x_rel[j] = 2u * (unsigned)((tb * img + dh * W + w) * C + ci0 +
+                                   (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8);
+      x_dh[j] = dh;
+      x_tb[j] = tb;
     }
   }
   const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.dy, 0, (int)(2LL * P * CO), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.x, 0, (int)(2LL * a.B * img * C), 0x00020000);
+
+  // tile cursor (image b0, first row h0 of the tile stage() issues next): the
+  // stages are issued for consecutive tiles, so it advances by one tile per
+  // call instead of dividing per tile
+  int cb0 = (t_begin * BM) / img;
+  int ch0 = (t_begin * BM - cb0 * img) / W;
+  const int lo_dh = r0 - 1, hi_dh = THX - 2 + r0;   // staged rows relative to h0
 
   // issue stage `t` into ring slot `buf`; a tile past the run loads zeros so
   // every wave's DMA count per stage stays D_PW + XPW
@@ -393,19 +414,35 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
     u16* Xs = Ds + D_EL;
     const bool live = t < t_end;
     const int m0 = t * BM;
-    const int b0 = m0 / img, h0 = (m0 - b0 * img) / W;
-#pragma unroll
-    for (int j = 0; j < D_PW; ++j) {
-      const bool ok = live && m0 + d_row[j] < P;
-      bdma16w(rsD, ok ? 2u * (unsigned)(m0 * CO + d_off[j]) : kOOBw, Ds + (wid + j * NW) * 512);
+    const int b0 = cb0, h0 = ch0;
+    if (whole_img) {
+      cb0 += hg.TB;
+    } else {
+      ch0 += TH;
+      if (ch0 >= H) { ch0 = 0; cb0 += 1; }
     }
+    const unsigned dbase = 2u * (unsigned)(m0 * CO), xbase = 2u * (unsigned)(m0 * C);
+    const bool interior = live && m0 + BM <= P && b0 + hg.TB <= a.B &&
+                          (whole_img || (h0 + lo_dh >= 0 && h0 + hi_dh < H));
+    if (interior) {
 #pragma unroll
-    for (int j = 0; j < kWhXPW; ++j) {
-      if (j < XPW) {
-        const unsigned inf = x_inf[j];
-        const int tb = (int)((inf >> 16) & 0x7fff), dh = (int)((inf >> 8) & 255) - 64;
-        const bool ok = live && (inf >> 31) && b0 + tb < a.B && (unsigned)(h0 + dh) < (unsigned)H;
-        bdma16w(rsX, ok ? 2u * (unsigned)(m0 * C + x_off[j]) : kOOBw, Xs + (wid + j * NW) * 512);
+      for (int j = 0; j < D_PW; ++j) bdma16w(rsD, d_rel[j] + dbase, Ds + (wid + j * NW) * 512);
+#pragma unroll
+      for (int j = 0; j < kWhXPW; ++j)
+        if (j < XPW) bdma16w(rsX, x_rel[j] + xbase, Xs + (wid + j * NW) * 512);
+    } else {
+#pragma unroll
+      for (int j = 0; j < D_PW; ++j) {
+        const bool ok = live && m0 + d_row[j] < P;
+        bdma16w(rsD, ok ? d_rel[j] + dbase : kOOBw, Ds + (wid + j * NW) * 512);
+      }
+#pragma unroll
+      for (int j = 0; j < kWhXPW; ++j) {
+        if (j < XPW) {
+          const bool ok = live && x_rel[j] != kOOBw && b0 + x_tb[j] < a.B &&
+                          (whole_img || (unsigned)(h0 + x_dh[j]) < (unsigned)H);
+          bdma16w(rsX, ok ? x_rel[j] + xbase : kOOBw, Xs + (wid + j * NW) * 512);
+        }
       }
     }
   };

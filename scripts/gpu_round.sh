@@ -21,7 +21,7 @@ if [[ "$STAGE" == all || "$STAGE" == bench ]]; then
   [[ $rc == 0 ]] || exit $rc
 fi
 if [[ "$STAGE" == all || "$STAGE" == prof ]]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 10 --warmup 3 > gpurun_out/prof.log 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 10 --warmup 3 --ttl-target 0 --ref-batch 0 > gpurun_out/prof.log 2>&1
   rc=$?; tail -3 gpurun_out/prof.log; echo "prof rc=$rc"
   [[ $rc == 0 ]] || exit $rc
 fi
