@@ -39,6 +39,10 @@ class LayerNorm(nn.LayerNorm):
             self.__dict__["_dmp_slots"] = slots
         return slots
 
+    def stream_forward(self, x):
+        """(x, LayerNorm(x)) with x's later gradient formed in the LN backward."""
+        return DF.stream_layer_norm(x, self.weight, self.bias, self.eps, self._slots(x))
+
     def add_forward(self, x, r):
         """(h, LayerNorm(h)) with h = x + r, fused (pre-norm residual add)."""
         return DF.add_layer_norm(x, r, self.weight, self.bias, self.eps, self._slots(x))
@@ -93,7 +97,7 @@ class Block(nn.Module):
         its result (add + norm1, add + norm2).  Returns ``(h, mlp_out)`` with
         ``mlp_out`` still to be added by the caller (next block / final norm)."""
         if pending is None:
-            y = self.norm1(h)
+            h, y = self.norm1.stream_forward(h)
         else:
             h, y = self.norm1.add_forward(h, pending)
         h, y = self.norm2.add_forward(h, self.attn(y))

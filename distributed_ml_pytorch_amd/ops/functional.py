@@ -575,6 +575,60 @@ class _AddLayerNorm(Function):
         return dx, dx, ret_g, ret_b, None, None
 
 
+class _LayerNormStream(Function):
+    """``(h, LayerNorm(h))`` for a residual stream ``h`` that is also read by the
+    next residual add: ``h`` comes back as a view, so autograd sees ONE consumer
+    and the LayerNorm-backward kernel forms ``dh_total = dh + LN_bwd(dy)``
+    itself (two consumers would have autograd sum the gradients with an ATen add
+    over the whole stream -- the first ViT block's 19 MB add)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, slots=None):
+        ctx.set_materialize_grads(False)
+        x = x.contiguous()
+        g32 = gamma.detach() if gamma is not None else None
+        b32 = beta.detach() if beta is not None else None
+        y, mean, rstd = native().layernorm_fwd(x, g32, b32, float(eps))
+        ctx.save_for_backward(x, mean, rstd)
+        ctx.gamma, ctx.beta, ctx.slots = gamma, beta, slots
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        if dy is None:
+            return dh, None, None, None, None
+        x, mean, rstd = ctx.saved_tensors
+        gamma, beta = ctx.gamma, ctx.beta
+        dg_arena, db_arena = _arena_grad(gamma), _arena_grad(beta)
+        need_g = gamma is not None and ctx.needs_input_grad[1]
+        need_b = beta is not None and ctx.needs_input_grad[2]
+        dg = dg_arena if dg_arena is not None else (
+            torch.zeros_like(gamma, dtype=torch.float32) if need_g else None)
+        db = db_arena if db_arena is not None else (
+            torch.zeros_like(beta, dtype=torch.float32) if need_b else None)
+        g32 = gamma.detach() if gamma is not None else None
+        if dh is not None and dh.dtype != x.dtype:
+            dh = dh.to(x.dtype)
+        dx = native().layernorm_bwd(x, dy.to(x.dtype), g32, mean, rstd, dg, db, ctx.slots, dh)
+        if dg_arena is not None or db_arena is not None:
+            _notify(gamma, beta)
+        ret_g = None if (dg_arena is not None or not need_g) else dg.to(gamma.dtype)
+        ret_b = None if (db_arena is not None or not need_b) else db.to(beta.dtype)
+        return dx, ret_g, ret_b, None, None
+
+
+def stream_layer_norm(x, weight, bias, eps: float, slots=None):
+    """``(x, LayerNorm(x))`` where the caller keeps using ``x`` (pre-norm
+    residual stream): the returned ``x`` carries the stream's gradient into the
+    LayerNorm backward kernel (native bf16 path); plain ``(x, layer_norm(x))``
+    elsewhere."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and layernorm_supported(x.shape[-1])
+            and (weight is None or weight.dtype == torch.float32)
+            and (bias is None or bias.dtype == torch.float32)):
+        return _LayerNormStream.apply(x, weight, bias, eps, slots)
+    return x, layer_norm(x, weight, bias, eps, slots)
+
+
 LN_SLOTS = 32   # csrc/transformer.hip kLnSlots
 
 
