@@ -1309,6 +1309,20 @@ std::vector<int64_t> conv_halo_configs(int64_t H, int64_t W, int64_t C, int64_t 
   return out;
 }
 
+// stride-2 halo dgrad cfg ids applicable to dX [*, CI, H, W] from dY [*, CO, OH, OW]
+std::vector<int64_t> conv_dgrad_s2_configs(int64_t H, int64_t W, int64_t OH, int64_t OW,
+                                           int64_t CO, int64_t CI, int64_t R, int64_t S,
+                                           int64_t stride, int64_t pad) {
+  std::vector<int64_t> out;
+  for (int i = 0; i < dmp::conv_dgrad_s2_num_configs(); ++i) {
+    const int c = dmp::conv_dgrad_s2_base() + i;
+    if (dmp::conv_dgrad_s2_ok(c, (int)H, (int)W, (int)OH, (int)OW, (int)CO, (int)CI, (int)R,
+                              (int)S, (int)stride, (int)pad))
+      out.push_back(c);
+  }
+  return out;
+}
+
 // halo wgrad cfg ids applicable to dW of a conv over [B, CI, H, W] -> CO channels
 std::vector<int64_t> conv_wgrad_halo_configs(int64_t B, int64_t H, int64_t W, int64_t CI,
                                              int64_t CO, int64_t R, int64_t S, int64_t stride,
@@ -1488,6 +1502,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("conv_configs", &conv_configs, "[(id, BM, BN, BK, threads)] of the compiled conv tiles");
   m.def("conv_wgrad_halo_configs", &conv_wgrad_halo_configs,
         "3x3/stride-1 halo wgrad cfg ids applicable to (B, H, W, CI, CO, R, S, stride, pad)");
+  m.def("conv_dgrad_s2_configs", &conv_dgrad_s2_configs,
+        "3x3/stride-2 halo data-gradient cfg ids for (H, W, OH, OW, CO, CI, R, S, stride, pad)");
   m.def("conv_halo_configs", &conv_halo_configs,
         "3x3/stride-1 halo-tile cfg ids applicable to (H, W, C, R, S, stride, pad)");
   m.def("bn_fwd_from_partials", &bn_fwd_from_partials, "BN forward from conv-epilogue partials",

@@ -510,16 +510,21 @@ constexpr int kHaloAPW = 8;   // max halo DMA instructions per wave per stage
 // (fwd), residual gradient addend (FLIP), BN partial sums (STATS) -- as
 // conv_igemm_kernel.  Wave (wm, wn) holds TM x TN 16x16 D^T fragments; the
 // LDS at lds_h is free (the caller synchronised after its last stage read).
-template <int BM, int BN, int WM, int WN, bool FLIP, bool STATS, int TM, int TN>
+// S2: the stride-2 data gradient's parity class `cls` (conv_dgrad_s2_kernel): row
+// m of the class grid (dY geometry GH x GW) is dX pixel (2i + ph, 2j + pw); a
+// subsampled addend (addend_sub) lands on class 0 only, indexed by m.
+template <int BM, int BN, int WM, int WN, bool FLIP, bool STATS, int TM, int TN, bool S2 = false>
 __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM][TN], long long m0,
                                               int n0, int wm, int wn, int tid, int lane,
-                                              u16* lds_h) {
+                                              u16* lds_h, int cls = 0) {
   constexpr int NW = WM * WN;
   typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
   const long long Mtot = (long long)a.B * a.OH * a.OW;
+  const long long Mrows = S2 ? (long long)a.B * a.GH * a.GW : Mtot;
   const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.y, 0, (int)(2LL * Mtot * a.CO), 0x00020000);
-  const bool add_in = FLIP && a.addend != nullptr;
+  const bool add_in = S2 ? (a.addend != nullptr && (!a.addend_sub || cls == 0))
+                         : (FLIP && a.addend != nullptr);
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
   constexpr bool BNB = FLIP && STATS;   // fused BN(+ReLU) backward
@@ -557,8 +562,14 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const long long m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
-    const bool mok = m < Mtot;
-    const unsigned rowoff = 2u * (unsigned)(m * a.CO);
+    const bool mok = m < Mrows;
+    long long pix = m;
+    if constexpr (S2) {
+      const int mi = (int)m, gi = a.GH * a.GW;
+      const int b = mi / gi, rem = mi - b * gi, ii = rem / a.GW, jj = rem - ii * a.GW;
+      pix = ((long long)b * a.OH + 2 * ii + (cls >> 1)) * a.OW + 2 * jj + (cls & 1);
+    }
+    const unsigned rowoff = 2u * (unsigned)(pix * a.CO);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
@@ -820,6 +831,181 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   }
   __syncthreads();   // all stage reads done before the epilogue reuses LDS
   halo_epilogue<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h);
+}
+
+// ------------------------------- 3x3 stride-2 data gradient, halo tiles
+// dX of a 3x3 / stride-2 / pad-1 conv splits into the parity classes (h % 2,
+// w % 2) of dX (top of this file).  Class (ph, pw) is a small STRIDE-1 conv over
+// dY: dX[2i+ph][2j+pw] = sum dY[i+u][j+v] Wt[r][s] with r = 1 (ph = 0) or r in
+// {2 at u = 0, 0 at u = 1} (ph = 1), s likewise: every tap (r, s) belongs to
+// exactly one class.  conv_igemm_kernel runs the classes as implicit GEMMs that
+// gather dY once per tap (330-460 TF/s, profiles/conv_layers_bs512_r2.txt).
+// Here a block stages its dY tile ONCE per 32-channel chunk with a one-row /
+// one-column halo below / right (zeros past the image) plus all nine weight
+// taps, and runs the nine taps out of LDS into FOUR accumulator sets, one per
+// class -- the fill per MFMA of the stride-1 halo kernel.  (A tile per class
+// measured no faster than the implicit GEMM: classes of 1 and 2 taps re-stage
+// the same dY tile for a few MFMAs.)  A block's BM pixels are whole rows (or
+// whole images) of the class grid = the dY grid for even H, W; halo_epilogue<S2>
+// scatters each class's tile to its dX pixels.  Wave tile TM x 16 pixels x
+// TN x 16 channels per class (4 x TM x TN accumulators).
+template <int BM, int BN, int WM, int WN, int NS>
+__global__ void __launch_bounds__(64 * WM * WN) conv_dgrad_s2_kernel(ConvArgs a, HaloGeom hg) {
+  constexpr int NW = WM * WN, BK = 32, CPR = BK / 8, RPI = 64 / CPR;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int B_ROWS = 9 * BN, B_INS = B_ROWS / RPI, B_PW = (B_INS + NW - 1) / NW;
+  static_assert(B_ROWS % RPI == 0, "weight tile rows");
+  extern __shared__ __attribute__((aligned(16))) u16 lds_h[];
+  const int A_EL = hg.A_INS * RPI * BK;
+  const int STAGE = A_EL + B_ROWS * BK;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int H = a.GH, W = a.GW, C = a.CI, TH = hg.TH, W1 = W + 1;
+  const int img = H * W;
+  const int b0 = (int)m0 / img, h0 = ((int)m0 - b0 * img) / W;
+  const int per_img = (TH + 1) * W1;
+  const float rcp_pi = 1.f / (float)per_img, rcp_w1 = 1.f / (float)W1;
+  const float rcp_tw = 1.f / (float)(TH * W), rcp_w = 1.f / (float)W;
+
+  // dY tile + halo: staged row (tb, hh, jj) = dY[b0 + tb][h0 + hh][jj], hh <= TH,
+  // jj <= W; the bottom / right halo past the image reads zeros
+  unsigned a_base[kHaloAPW];
+#pragma unroll
+  for (int j = 0; j < kHaloAPW; ++j) {
+    const int ins = wid + j * NW;
+    const int row = ins * RPI + lane / CPR;
+    int tb, rem, hh, jj;
+    small_divmod(row, per_img, rcp_pi, tb, rem);
+    small_divmod(rem, W1, rcp_w1, hh, jj);
+    const int b = b0 + tb, h = h0 + hh;
+    const bool ok = ins < hg.A_INS && row < hg.HROWS && b < a.B && h < H && jj < W;
+    a_base[j] = ok ? 2u * (unsigned)(((b * H + h) * W + jj) * C + swz<BK>(row, lane % CPR) * 8)
+                   : kOOB;
+  }
+  // weight rows: t * BN + n <- Wt[n0 + n][t][chunk]   (t = r * 3 + s)
+  unsigned b_base[B_PW];
+#pragma unroll
+  for (int j = 0; j < B_PW; ++j) {
+    const int ins = wid + j * NW;
+    const int row = ins * RPI + lane / CPR;
+    const int t = row / BN, n = row - t * BN;
+    const bool ok = ins < B_INS && n0 + n < a.CO;
+    b_base[j] = ok ? 2u * (unsigned)(((n0 + n) * 9 + t) * C + swz<BK>(row, lane % CPR) * 8) : kOOB;
+  }
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, 0, (int)(2LL * a.B * H * W * C), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.w, 0, (int)(2LL * a.CO * 9 * C), 0x00020000);
+  auto stage = [&](int buf, int c) {
+    u16* As = lds_h + buf * STAGE;
+    u16* Bs = As + A_EL;
+    const unsigned cd = 2u * (unsigned)(c * BK);
+#pragma unroll
+    for (int j = 0; j < kHaloAPW; ++j) {
+      const int ins = wid + j * NW;
+      if (ins < hg.A_INS) bdma16(rsA, a_base[j] == kOOB ? kOOB : a_base[j] + cd, As + ins * (RPI * BK));
+    }
+#pragma unroll
+    for (int j = 0; j < B_PW; ++j) {
+      const int ins = wid + j * NW;
+      if (B_INS % NW == 0 || ins < B_INS)
+        bdma16(rsB, b_base[j] == kOOB ? kOOB : b_base[j] + cd, Bs + ins * (RPI * BK));
+    }
+  };
+
+  f32x4 acc[4][TM][TN];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int hrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
+    int tb, r2, th, tw;
+    small_divmod(ml, TH * W, rcp_tw, tb, r2);
+    small_divmod(r2, W, rcp_w, th, tw);
+    hrow[i] = (tb * (TH + 1) + th) * W1 + tw;
+  }
+  int offB;
+  {
+    const int rb = wn * (BN / WN) + (lane & 15);
+    offB = rb * BK + swz<BK>(rb, lane >> 4) * 8;
+  }
+  // tap t = (r, s): class (r != 1, s != 1), dY offset (r == 0, s == 0)
+  auto compute = [&](int buf) {
+    const u16* As = lds_h + buf * STAGE;
+    const u16* Bs = As + A_EL;
+    bf16x8 af[2][TM], bw[2][TN];
+    auto load = [&](int t, int slot) {
+      const int r = t / 3, sc = t % 3;
+      const int rowoff = (r == 0 ? W1 : 0) + (sc == 0 ? 1 : 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = hrow[i] + rowoff;
+        af[slot][i] = *reinterpret_cast<const bf16x8*>(As + row * BK + swz<BK>(row, lane >> 4) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bw[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + t * BN * BK + offB + j * 16 * BK);
+    };
+    load(0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int q = (t / 3 != 1 ? 2 : 0) + (t % 3 != 1 ? 1 : 0);
+      if (t + 1 < 9) load(t + 1, (t + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[q][i][j] = mfma16(bw[t & 1][j], af[t & 1][i], acc[q][i][j]);
+      if (t + 1 < 9) {
+#pragma unroll
+        for (int k = 0; k < TM + TN && k < TM * TN; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if (TM * TN > TM + TN) __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
+        if (TM * TN < TM + TN) __builtin_amdgcn_sched_group_barrier(0x100, TM + TN - TM * TN, 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
+      }
+    }
+  };
+  const int KC = C / BK;
+  if constexpr (NS == 2) {
+    // two stages: chunk c+1's DMA in flight under chunk c's MFMAs (an 8-wave
+    // block holds the CU's register file alone, so no second block hides the fill)
+    stage(0, 0);
+    for (int c = 0; c < KC; ++c) {
+      wait_vm<0>();                       // chunk c landed (this wave's DMAs) ...
+      __builtin_amdgcn_s_barrier();       // ... for every wave; chunk c-1's slot is free
+      asm volatile("" ::: "memory");
+      if (c + 1 < KC) stage((c + 1) & 1, c + 1);
+      compute(c & 1);
+    }
+  } else {
+    // one stage (several blocks per CU overlap each other's fill and MFMAs)
+    for (int c = 0; c < KC; ++c) {
+      if (c > 0) __syncthreads();         // everyone done reading chunk c-1
+      stage(0, c);
+      wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      compute(0);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    halo_epilogue<BM, BN, WM, WN, true, false, TM, TN, true>(a, acc[q], m0, n0, wm, wn, tid, lane,
+                                                             lds_h, q);
 }
 
 // ------------------------------------ persistent 3x3 halo tiles, 64 channels
@@ -1427,6 +1613,81 @@ static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
   return false;
 }
 
+// stride-2 halo data-gradient tiles (conv_dgrad_s2_kernel): id, BM, BN, WM, WN
+constexpr int kS2Base = 200;
+// (wave tiles of 32 pixels x 64 channels or 64 x 32 per class: 4 classes x 8
+// accumulator tiles = 128 registers)
+#define DMP_S2_CONFIGS(X)      \
+  X(0, 128, 64, 4, 1, 1)       \
+  X(1, 256, 64, 8, 1, 1)       \
+  X(2, 128, 128, 4, 2, 1)      \
+  X(3, 256, 32, 4, 1, 1)       \
+  X(4, 64, 64, 2, 1, 1)        \
+  X(5, 112, 64, 7, 1, 1)       \
+  X(6, 256, 64, 8, 1, 2)       \
+  X(7, 128, 128, 4, 2, 2)      \
+  X(8, 128, 64, 8, 1, 2)       \
+  X(9, 112, 64, 7, 1, 2)
+constexpr int kNumS2Configs = 10;
+static bool s2_cfg(int cfg, int* bm, int* bn, int* nw, int* ns) {
+  switch (cfg - kS2Base) {
+#define X(i, BM, BN, WM, WN, NS) \
+  case i: *bm = BM; *bn = BN; *nw = WM * WN; *ns = NS; return true;
+    DMP_S2_CONFIGS(X)
+#undef X
+  }
+  return false;
+}
+// geometry of a stride-2 halo dgrad config: dY (OH x OW, K channels) -> dX (H x W, N channels)
+static bool s2_geom(int cfg, int H, int W, int OH, int OW, int K, int N, int R, int S, int stride,
+                    int pad, HaloGeom* g, size_t* lds) {
+  int bm, bn, nw, ns;
+  if (!s2_cfg(cfg, &bm, &bn, &nw, &ns)) return false;
+  if (R != 3 || S != 3 || stride != 2 || pad != 1 || H != 2 * OH || W != 2 * OW) return false;
+  if (K % 32 != 0 || N % bn != 0) return false;
+  const int img = OH * OW;
+  HaloGeom h{};
+  if (bm <= img) {
+    if (bm % OW != 0 || img % bm != 0) return false;
+    h.TH = bm / OW;
+    h.TB = 1;
+  } else {
+    if (bm % img != 0) return false;
+    h.TH = OH;
+    h.TB = bm / img;
+  }
+  h.HROWS = h.TB * (h.TH + 1) * (OW + 1);
+  h.A_INS = (h.HROWS + 15) / 16;
+  if (h.A_INS > kHaloAPW * nw) return false;
+  const size_t bytes = (size_t)ns * 2 * ((size_t)h.A_INS * 512 + (size_t)9 * bn * 32);
+  if (bytes > 160 * 1024) return false;
+  *g = h;
+  *lds = bytes;
+  return true;
+}
+bool conv_dgrad_s2_ok(int cfg, int H, int W, int OH, int OW, int K, int N, int R, int S, int stride,
+                      int pad) {
+  HaloGeom g;
+  size_t lds;
+  return s2_geom(cfg, H, W, OH, OW, K, N, R, S, stride, pad, &g, &lds);
+}
+int conv_dgrad_s2_base() { return kS2Base; }
+int conv_dgrad_s2_num_configs() { return kNumS2Configs; }
+
+template <int BM, int BN, int WM, int WN, int NS>
+static void launch_s2_t(const ConvArgs& a, const HaloGeom& g, size_t lds, hipStream_t s) {
+  auto kern = conv_dgrad_s2_kernel<BM, BN, WM, WN, NS>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const long long M = (long long)a.B * a.GH * a.GW;   // class-grid pixels (= dY pixels)
+  const dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)(a.CO / BN));
+  hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, a, g);
+}
+
 int conv_fwd_num_mblocks(long long M, int CO, int cfg) {
   {
     int bm, bn, bk, nw, ns;
@@ -1466,6 +1727,19 @@ void launch_conv_dgrad(const u16* dy, const u16* wt, u16* dx, int B, int H, int 
     a.bnmask = bnf->mask;
     a.bnstat = bnf->stats;
     a.bnrelu = bnf->relu;
+  }
+  if (cfg >= kS2Base && cfg < kS2Base + kNumS2Configs) {
+    HaloGeom g;
+    size_t lds;
+    if (!bnf && s2_geom(cfg, H, W, OH, OW, CO, CI, R, S, stride, pad, &g, &lds)) {
+      switch (cfg - kS2Base) {
+#define X(i, BM, BN, WM, WN, NS) \
+  case i: launch_s2_t<BM, BN, WM, WN, NS>(a, g, lds, s); return;
+        DMP_S2_CONFIGS(X)
+#undef X
+      }
+    }
+    cfg = -1;   // not applicable: heuristic implicit-GEMM tile
   }
   if (cfg >= kHaloBase) {
     // stride 1, 3x3, pad 1: dX = the same conv over dY with Wt and mirrored taps

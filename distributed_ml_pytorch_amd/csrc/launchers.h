@@ -111,6 +111,11 @@ int conv_default_config(long long M, int CO);
 int conv_fwd_num_mblocks(long long M, int CO, int cfg);
 // 3x3 / stride-1 halo-tile kernels: cfg ids conv_halo_base() + [0, conv_num_halo_configs())
 int conv_num_halo_configs();
+// 3x3 / stride-2 halo data-gradient tiles: cfg ids conv_dgrad_s2_base() + [0, num)
+bool conv_dgrad_s2_ok(int cfg, int H, int W, int OH, int OW, int K, int N, int R, int S, int stride,
+                      int pad);
+int conv_dgrad_s2_base();
+int conv_dgrad_s2_num_configs();
 int conv_halo_base();
 bool conv_halo_ok(int cfg, int H, int W, int C, int R, int S, int stride, int pad);
 // 3x3 / stride-1 halo wgrad: cfg ids conv_wgrad_halo_base() + [0, conv_wgrad_num_halo_configs())

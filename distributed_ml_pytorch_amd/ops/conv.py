@@ -208,6 +208,11 @@ def _dgrad_cfg(dy, w16, H, W, stride, pad):
     cands = _igemm_candidates(w16.shape[1])
     if (H, W) == tuple(dy.shape[2:]):
         cands += _halo_candidates(H, W, dy.shape[1], w16.shape[2], w16.shape[3], stride, pad)
+    elif _HALO_ENABLED and stride == 2:
+        # 3x3 / stride-2: parity classes run as halo tiles over dY (conv_dgrad_s2_kernel)
+        cands += list(native().conv_dgrad_s2_configs(H, W, dy.shape[2], dy.shape[3], dy.shape[1],
+                                                     w16.shape[1], w16.shape[2], w16.shape[3],
+                                                     stride, pad))
     if _gemm1x1_ok(w16.shape, stride, pad, w16.shape[1], w16.shape[0]):
         cands.append(_GEMM_ROUTE)
 

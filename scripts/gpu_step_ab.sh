@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out && export TMPDIR=/tmp
 MODEL_ARGS=${MODEL_ARGS:-""}
 rm -rf /tmp/old && mkdir -p /tmp/old && cp -r distributed_ml_pytorch_amd bench.py tuning /tmp/old/ && \
-  cp abtmp/_native_old.so /tmp/old/distributed_ml_pytorch_amd/_native.cpython-310-x86_64-linux-gnu.so || exit 1
+  cp abtmp/_native_old.so /tmp/old/distributed_ml_pytorch_amd/_native.cpython-310-x86_64-linux-gnu.so && { [ ! -f abtmp/tune_cache_old.json ] || cp abtmp/tune_cache_old.json /tmp/old/tuning/mi355x_tune_cache.json; } && { [ ! -d abtmp/overlay ] || cp -r abtmp/overlay/. /tmp/old/; } || exit 1
 for r in 1 2 3; do
   (cd /tmp/old && timeout -k 10 300 python bench.py --steps 40 --warmup 10 --ttl-target 0 $MODEL_ARGS 2>/dev/null | tail -1 | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('old', d['ms_per_step'], d['value'])") || exit 1
   timeout -k 10 300 python bench.py --steps 40 --warmup 10 --ttl-target 0 $MODEL_ARGS 2>/dev/null | tail -1 | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('new', d['ms_per_step'], d['value'])" || exit 1

@@ -557,3 +557,33 @@ def test_bn_backward_fusion_falls_back_on_shared_output(monkeypatch):
     assert Fn.BN_BWD_FUSE_STATS["fallback"] > before["fallback"]
     for a, b in zip(ref, got):
         assert _rel(b, a) < 5e-3
+
+
+@pytest.mark.parametrize("B,CI,H,CO", [(4, 64, 32, 128), (2, 128, 16, 256), (8, 256, 8, 512),
+                                       (2, 64, 56, 128)])
+def test_stride2_halo_dgrad_configs(B, CI, H, CO):
+    """3x3/stride-2 data gradient as parity-class halo tiles (conv_dgrad_s2_kernel):
+    every applicable config vs fp32, plain, with a full-resolution addend, and with
+    the subsampled shortcut addend (class (0, 0) only)."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    torch.manual_seed(0)
+    OH = H // 2
+    w = (torch.randn(CO, CI, 3, 3, device="cuda") / (CI * 9) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    dy = torch.randn(B, CO, OH, OH, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    ref = torch.nn.grad.conv2d_input((B, CI, H, H), w.float(), dy.float(), stride=2, padding=1)
+    add = torch.randn(B, CI, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    sub = torch.randn(B, CI, OH, OH, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    ref_sub = ref.clone()
+    ref_sub[:, :, ::2, ::2] += sub.float()
+    cfgs = list(nat.conv_dgrad_s2_configs(H, H, OH, OH, CO, CI, 3, 3, 2, 1))
+    assert cfgs, "no stride-2 halo config applies"
+    for cfg in cfgs:
+        dx = nat.conv_dgrad(dy, w, H, H, 2, 1, cfg)
+        assert _rel(dx, ref) < 1e-2, cfg
+        dxa = nat.conv_dgrad(dy, w, H, H, 2, 1, cfg, None, add)
+        assert _rel(dxa, ref + add.float()) < 1e-2, cfg
+        dxs = nat.conv_dgrad(dy, w, H, H, 2, 1, cfg, addend=sub, addend_sub=True)
+        assert _rel(dxs, ref_sub) < 1e-2, cfg
