@@ -1201,8 +1201,43 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   for (int j = 0; j < TN; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s_sum[j][r] = 0.f; s_sq[j][r] = 0.f; }
-  auto epilogue = [&](int k) {
+  // residual-gradient addend of the data gradient (FLIP): its rows of tile k are
+  // loaded (inline asm, counted by hand) BEFORE the next tile's DMA is issued,
+  // so the deferred epilogue waits only for them, never for that DMA
+  typedef unsigned int u32x2_a __attribute__((ext_vector_type(2)));
+  const bool add_in = FLIP && a.addend != nullptr;
+  const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * P * a.CO), 0x00020000);
+  u32x2_a ad[TM][TN];
+  auto aload = [&](int k) {
     const int m0 = tile_of(k) * BM;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wid * (BM / NW) + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + j * 16 + 4 * (lane >> 4);
+        const unsigned off = (m < P && n < a.CO) ? 2u * (unsigned)(m * a.CO + n) : kOOB;
+        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(ad[i][j]) : "v"(off), "s"(rsAdd)
+                     : "memory");
+      }
+    }
+  };
+  // this wave's DMA pieces per stage (issued after the addend loads)
+  int dma_pw = 0;
+#pragma unroll
+  for (int j = 0; j < kHpAPW; ++j)
+    if (j < APW && (NS != 2 || wid + j * NW < hg.AINS)) ++dma_pw;
+  auto epilogue = [&](int k, bool last) {
+    const int m0 = tile_of(k) * BM;
+    if (add_in) {
+      if (last) wait_vm<0>();
+      else wait_vm_n(dma_pw);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(ad[i][j]));
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wid * (BM / NW) + i * 16 + (lane & 15);
@@ -1212,10 +1247,17 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + j * 16 + 4 * (lane >> 4);
         const bool ok = mok && n < a.CO;
+        float av[4] = {0.f, 0.f, 0.f, 0.f};
+        if (add_in) {
+          av[0] = __uint_as_float(ad[i][j].x << 16);
+          av[1] = __uint_as_float(ad[i][j].x & 0xffff0000u);
+          av[2] = __uint_as_float(ad[i][j].y << 16);
+          av[3] = __uint_as_float(ad[i][j].y & 0xffff0000u);
+        }
         u16 hv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float t = acc[i][j][r] + bj[j][r];
+          float t = acc[i][j][r] + bj[j][r] + av[r];
           if (!FLIP && a.relu) t = fmaxf(t, 0.f);
           hv[r] = f2bf(t);
           if (STATS) {
@@ -1262,15 +1304,17 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     if (!FLIP && hg.xform) xform_tile(k);
     __builtin_amdgcn_s_barrier();       // ... for every wave; slot (k-1) % NS is free
     asm volatile("" ::: "memory");
+    if (k > 0 && add_in) aload(k - 1);
     stage((k + NS - 1) % NS, k + NS - 1);
-    if (k > 0) epilogue(k - 1);
+    if (k > 0) epilogue(k - 1, false);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     compute(k % NS);
   }
-  epilogue(nt - 1);
+  if (add_in) aload(nt - 1);
+  epilogue(nt - 1, true);
   if (STATS) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -1579,10 +1623,11 @@ static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
     HaloPGeom pg;
     int bm, ns, nw;
     size_t plds;
-    // a residual-gradient addend and the BN-backward epilogue are not fused in
-    // the persistent kernel (its deferred epilogue runs with the next tile's DMA
-    // in flight): take the 4-wave halo tile for those dgrads instead
-    if (FLIP && (a.addend != nullptr || STATS))
+    // the BN-backward epilogue is not fused in the persistent kernel (its
+    // deferred epilogue runs with the next tile's DMA in flight): take the 4-wave
+    // halo tile for those dgrads instead (a residual addend is fused: loaded ahead
+    // of the DMA, see conv_halo64p_kernel)
+    if (FLIP && (STATS || (a.addend != nullptr && a.addend_sub)))
       return launch_halo<FLIP, STATS>(a, kHaloBase + 9, s) ||
              launch_halo<FLIP, STATS>(a, kHaloBase + 5, s);
     if (!halop_geom(cfg, a.B, a.GH, a.GW, a.CI, a.R, a.S, a.stride, a.pad, &pg, &bm, &ns, &nw,
