@@ -22,6 +22,8 @@
 //            summed through LDS, then fp32 atomics into the arena gradient.
 // The input image is read with explicit element strides (any dense layout of
 // the bf16 activations).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dmp {
@@ -484,14 +486,16 @@ __global__ void __launch_bounds__(256) stem3_fwd_kernel(Stem3Args a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s[j][r] = 0.f; q[j][r] = 0.f; }
   const long long base = ((long long)blockIdx.x * 4 + wid) * a.groups * 16;
-  for (int gi = 0; gi < a.groups; ++gi) {
+  // the 8-tap gather of group gi+1 is issued before group gi's MFMAs and stores:
+  // one dependent L2 round trip per group otherwise set the kernel time (a wave
+  // walks its groups in sequence at 2 waves / SIMD)
+  auto gather = [&](int gi, bf16x8& xf) {
     const long long px = base + gi * 16 + col;
     const bool pv = px < a.P;
     const int p32 = pv ? (int)px : 0;
     const int ow = p32 % a.W, t = p32 / a.W;
     const int oh = t % a.H, b = t / a.H;
     const int boff = b * a.sb;
-    bf16x8 xf;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int ih = oh + dr[i], iw = ow + ds[i];
@@ -499,6 +503,14 @@ __global__ void __launch_bounds__(256) stem3_fwd_kernel(Stem3Args a) {
       const int off = ok ? 2 * (boff + ih * a.sh + iw * a.sw + ci[i] * a.sc) : 0x7ffffff0;
       xf.v[i] = __builtin_bit_cast(u16, __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
     }
+  };
+  bf16x8 xnext;
+  gather(0, xnext);
+  for (int gi = 0; gi < a.groups; ++gi) {
+    const long long px = base + gi * 16 + col;
+    const bool pv = px < a.P;
+    const bf16x8 xf = xnext;
+    if (gi + 1 < a.groups) gather(gi + 1, xnext);
     f32x4 acc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = s3_mfma(wf[j], xf, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -666,7 +678,11 @@ void launch_stem3_fwd(const u16* x, int xbytes, int sb, int sh, int sw, int sc, 
   a.P = (long long)B * H * W;
   // 16 groups of 16 pixels per wave (1024 pixels per block) unless that leaves
   // fewer than ~2 blocks per CU
-  int groups = 16;
+  static const int gmax = [] {
+    const char* e = getenv("DMP_STEM3_GROUPS");   // A/B knob: max groups per wave
+    return e ? atoi(e) : 16;
+  }();
+  int groups = gmax > 0 ? gmax : 16;
   while (groups > 1 && (a.P + 64LL * groups - 1) / (64LL * groups) < 512) groups >>= 1;
   a.groups = groups;
   const long long nb = (a.P + 64LL * groups - 1) / (64LL * groups);
@@ -681,8 +697,13 @@ void launch_stem3_wgrad(const u16* dy, const u16* x, int xbytes, int sb, int sh,
   a.H = H; a.W = W; a.CI = CI; a.K = 9 * CI;
   a.P = (long long)B * H * W;
   // ~512 blocks: 128-pixel steps per block
+  static const long long target = [] {
+    const char* e = getenv("DMP_STEM3_WG_BLOCKS");   // A/B knob: target block count
+    const long long v = e ? atoll(e) : 512;
+    return v > 0 ? v : 512;
+  }();
   const long long steps = (a.P + 127) / 128;
-  long long per = (steps + 511) / 512;
+  long long per = (steps + target - 1) / target;
   if (per < 1) per = 1;
   a.groups = (int)per;
   const long long nb = (steps + per - 1) / per;
