@@ -586,24 +586,23 @@ __global__ void __launch_bounds__(256) stem3_wgrad_kernel(Stem3Args a) {
   for (int j = 0; j < 4; ++j) { acc[j][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[j][1] = acc[j][0]; }
   u16* im = img[wid];
   const long long blk0 = (long long)blockIdx.x * a.groups * 128;
-  for (int st = 0; st < a.groups; ++st) {
+  // step st+1's dY chunks and X taps are loaded into registers before step st's
+  // LDS image write and MFMAs (each step was one dependent round trip)
+  auto load_step = [&](int st, bf16x8 (&dv)[4], bf16x8 (&xf)[2]) {
     const long long p0 = blk0 + (long long)st * 128 + wid * 32;   // this wave's 32 pixels
-    // stage dY[p0 .. p0+32)[0..64) : 256 real 16-B chunks per wave image, 4 per lane
+    // dY[p0 .. p0+32)[0..64) : 256 real 16-B chunks per wave image, 4 per lane
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = u * 64 + lane;              // logical chunk: row e >> 3, cols (e & 7) * 8
       const int row = e >> 3, c0 = (e & 7) * 8;
       const long long p = p0 + row;
-      bf16x8 v;
-      if (p < a.P) v = *reinterpret_cast<const bf16x8*>(a.dy + p * 64 + c0);
+      if (p < a.P) dv[u] = *reinterpret_cast<const bf16x8*>(a.dy + p * 64 + c0);
       else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v.v[i] = 0;
+        for (int i = 0; i < 8; ++i) dv[u].v[i] = 0;
       }
-      *reinterpret_cast<bf16x8*>(im + s3_toff(row, c0)) = v;   // 8 cols stay in one granule
     }
     // X fragments: pixels p0 + 8kg + i (one image row when W % 8 == 0), taps 16t + col
-    bf16x8 xf[2];
     {
       const long long pb = p0 + 8 * kg;
       const bool pv = pb < a.P;
@@ -623,6 +622,21 @@ __global__ void __launch_bounds__(256) stem3_wgrad_kernel(Stem3Args a) {
           xf[t].v[i] = __builtin_bit_cast(u16, __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
         }
       }
+    }
+  };
+  bf16x8 dnext[4], xnext[2];
+  load_step(0, dnext, xnext);
+  for (int st = 0; st < a.groups; ++st) {
+    bf16x8 dcur[4], xf[2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dcur[u] = dnext[u];
+    xf[0] = xnext[0];
+    xf[1] = xnext[1];
+    if (st + 1 < a.groups) load_step(st + 1, dnext, xnext);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = u * 64 + lane;
+      *reinterpret_cast<bf16x8*>(im + s3_toff(e >> 3, (e & 7) * 8)) = dcur[u];   // 8 cols stay in one granule
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS image writes landed
     __builtin_amdgcn_wave_barrier();
