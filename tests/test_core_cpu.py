@@ -293,3 +293,22 @@ def test_deterministic_flag_plumbing():
     finally:
         torch.use_deterministic_algorithms(False)
         torch.backends.cudnn.deterministic = False
+
+
+def test_stream_layer_norm_cpu_matches_two_consumers():
+    """ops.functional.stream_layer_norm on CPU: (x, LayerNorm(x)) whose two outputs'
+    gradients both reach x (the GPU path forms the sum inside the LN backward)."""
+    import torch.nn.functional as F
+
+    from distributed_ml_pytorch_amd.ops.functional import stream_layer_norm
+
+    torch.manual_seed(0)
+    x = torch.randn(3, 5, 16, requires_grad=True)
+    w = torch.randn(16, requires_grad=True)
+    b = torch.randn(16, requires_grad=True)
+    h, y = stream_layer_norm(x, w, b, 1e-6)
+    (h * 2.0 + y * 3.0).sum().backward()
+    x2 = x.detach().clone().requires_grad_(True)
+    ref = x2 * 2.0 + F.layer_norm(x2, (16,), w.detach(), b.detach(), 1e-6) * 3.0
+    ref.sum().backward()
+    torch.testing.assert_close(x.grad, x2.grad)
