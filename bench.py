@@ -99,6 +99,14 @@ def parse(argv=None):
                     help="class-template amplitude of the time-to-target images (0.05: ~1000 "
                          "steps to loss 0.5 at N=1, profiles/ttl_calibration_r2.txt)")
     ap.add_argument("--ttl-batches", type=int, default=128, help="distinct TTL batches (one dataset, all ranks)")
+    ap.add_argument("--ttl-heldout-batches", type=int, default=8,
+                    help="held-out split of the TTL data: same class templates, disjoint samples "
+                         "(its own noise seed), evaluated through the no-grad native path every "
+                         "--ttl-eval-every steps as the reference evaluates on its test set "
+                         "(/root/reference/example/main.py:83-89,110-131); 0 skips")
+    ap.add_argument("--ttl-eval-every", type=int, default=50)
+    ap.add_argument("--ttl-heldout-acc", type=float, default=0.8,
+                    help="held-out accuracy target: ttl_heldout_steps = first evaluation at or above it")
     ap.add_argument("--central-check", type=int, default=-1,
                     help="after the JSON line, at N>1: STEPS of the reference topology (rank 0 "
                          "= PS, pushes / pulls over the per-pair payload communicators, RCCL on "
@@ -250,7 +258,7 @@ def time_to_target(a, cfg, ctx, mode=None):
     import torch
 
     from distributed_ml_pytorch_amd.runtime.trainer import Worker
-    from distributed_ml_pytorch_amd.utils.data import DeviceBatchPool
+    from distributed_ml_pytorch_amd.utils.data import ttl_pools
 
     info = ctx.info
     cfg = replace(cfg, mode=mode or cfg.mode, seed=1000)
@@ -261,16 +269,19 @@ def time_to_target(a, cfg, ctx, mode=None):
     # ranks), each worker starting at its own offset into it: with per-rank
     # datasets, N workers saw N x the distinct samples and the training loss fell
     # later simply because there was less to memorise (sync DP at N = 8 took
-    # 2200 steps against 970 at N = 1 in the 8-rank rehearsal)
-    pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device,
-                           n_batches=a.ttl_batches, dtype=w.compute_dtype,
-                           seed=100, learnable=True, signal=a.ttl_signal)
+    # 2200 steps against 970 at N = 1 in the 8-rank rehearsal).  The held-out
+    # split (same templates, disjoint samples) is what generalisation is scored on.
+    pool, held = ttl_pools(a.batch, w.input_shape, w.num_classes, w.device, a.ttl_batches,
+                           a.ttl_heldout_batches, dtype=w.compute_dtype, signal=a.ttl_signal)
     widx = info.rank - 1 if ctx.central else info.rank
     pool.i = (widx * a.ttl_batches // max(1, ctx.n_workers)) % a.ttl_batches
     ctx.worker_barrier()
     _sync()
     t0 = time.perf_counter()
     steps, reached, window = 0, False, []
+    t_train, train_steps = None, 0
+    h_reached, h_steps, h_time, h_last = held is None, None, None, (None, None)
+    eval_s = 0.0
     while steps < a.ttl_max_steps:
         x, y = pool.next()
         loss, _ = w.train_step(x, y)
@@ -282,24 +293,47 @@ def time_to_target(a, cfg, ctx, mode=None):
             m = ctx.worker_mean(torch.stack(window).mean().reshape(1))
             window.clear()
             if steps % 200 == 0 and info.rank == 0:   # progress for long (multi-rank) runs
-                print(f"[ttl] {mode or cfg.mode} step {steps} mean loss {float(m.item()):.4f}",
-                      file=sys.stderr, flush=True)
-            if float(m.item()) <= a.ttl_target:
+                print(f"[ttl] {mode or cfg.mode} step {steps} mean loss {float(m.item()):.4f}"
+                      + (f" held-out loss {h_last[0]:.4f} acc {h_last[1]:.4f}"
+                         if h_last[0] is not None else ""), file=sys.stderr, flush=True)
+            if not reached and float(m.item()) <= a.ttl_target:
                 reached = True
-                break
+                _sync()
+                t_train, train_steps = time.perf_counter() - t0, steps
+        if held is not None and steps % a.ttl_eval_every == 0:
+            # the reference's periodic test-set evaluation (main.py:83-89): the
+            # native no-grad forward over the whole held-out split, BN in eval mode
+            te = time.perf_counter()
+            hl, ha = w.evaluate(zip(held.x, held.y))
+            hv = ctx.worker_mean(torch.tensor([hl, ha], dtype=torch.float64,
+                                              device=w.device)).tolist()
+            h_last = (hv[0], hv[1])
+            eval_s += time.perf_counter() - te
+            if not h_reached and h_last[1] >= a.ttl_heldout_acc:
+                h_reached, h_steps, h_time = True, steps, time.perf_counter() - t0
+        if reached and h_reached:
+            break
     _sync()
     t = time.perf_counter() - t0
     w.finish()
-    return {"time_to_target_s": round(t, 3), "ttl_steps": steps, "ttl_reached": reached}
+    out = {"time_to_target_s": round(t_train if reached else t, 3),
+           "ttl_steps": train_steps if reached else steps, "ttl_reached": reached}
+    if held is not None:
+        out.update({"ttl_heldout_loss": None if h_last[0] is None else round(h_last[0], 4),
+                    "ttl_heldout_acc": None if h_last[1] is None else round(h_last[1], 4),
+                    "ttl_heldout_steps": h_steps, "ttl_heldout_reached": bool(h_reached),
+                    "ttl_heldout_s": None if h_time is None else round(h_time, 3),
+                    "ttl_eval_s": round(eval_s, 3)})
+    return out
 
 
-def _central_check(a, cfg, ctx, steps: int):
+def _central_check(a, cfg, ctx, steps: int, line=None):
     """The reference's own topology (/root/reference/example/main.py:135-165: one
     PS process, every other rank a Downpour worker) run for ``steps`` worker steps
-    AFTER the benchmark line: the (PS, worker) payload communicators -- RCCL
-    pairs on GPUs -- carry real pushes and pulls, and rank 0 reports what moved.
-    A watchdog ends a stuck check (every rank exits 0: the measured line is
-    already printed), so it can never cost the benchmark its result."""
+    after the timed runs: the (PS, worker) payload communicators -- RCCL pairs on
+    GPUs -- carry real pushes and pulls, and rank 0 reports what moved.  Runs BEFORE rank 0 prints its line and returns the report that goes into
+    it (``central_check``); a watchdog ends a stuck check: rank 0 prints the
+    measured line with ``central_check.ok = false`` and every rank exits 3."""
     import threading
     from dataclasses import replace
 
@@ -311,9 +345,15 @@ def _central_check(a, cfg, ctx, steps: int):
     info = ctx.info
 
     def _expire():
+        # a hang in the pair communicators or the PS loop is a FAILURE: rank 0
+        # still prints the measured line (with the failed check in it), and every
+        # rank exits non-zero
         print(f"[central-check] rank {info.rank}: no result after "
               f"{a.central_check_timeout:.0f} s, exiting", file=sys.stderr, flush=True)
-        os._exit(0)
+        if info.rank == 0 and line is not None:
+            line["central_check"] = {"ok": False, "timeout_s": a.central_check_timeout}
+            print(json.dumps(line), flush=True)
+        os._exit(3)
 
     dog = threading.Timer(a.central_check_timeout, _expire)
     dog.daemon = True
@@ -355,6 +395,8 @@ def _central_check(a, cfg, ctx, steps: int):
                "rccl_ranks": pf["rccl_ranks"], "seconds": round(time.perf_counter() - t0, 2),
                "ps": ps, "workers": workers}
         print("[central-check] " + json.dumps(rep), file=sys.stderr, flush=True)
+        return rep
+    return None
 
 
 def run(a):
@@ -431,12 +473,27 @@ def run(a):
     # -------- reduce over ranks (host side; the PS contributes zeros) --------
     ttl_vals = [ttl["time_to_target_s"], ttl["ttl_steps"], float(ttl["ttl_reached"])] \
         if ttl else [0.0, 0.0, 0.0]
+    # held-out fields are already worker means (identical on every worker); the
+    # MAX brings them to rank 0 (the PS contributes -1 = "not a worker")
+    held_keys = ("ttl_heldout_loss", "ttl_heldout_acc", "ttl_heldout_steps",
+                 "ttl_heldout_reached", "ttl_heldout_s", "ttl_eval_s")
+    held_vals = [-1.0 if not ttl or ttl.get(k) is None else float(ttl[k]) for k in held_keys]
     red = ctx.host_reduce([elapsed, -elapsed if elapsed else -1e30, ref_elapsed, final_loss,
-                           *ttl_vals])
+                           *ttl_vals, *held_vals])
     elapsed, min_elapsed, ref_elapsed, final_loss = red[0], -red[1], red[2], red[3]
     if ttl is not None or ctx.is_ps:
         ttl = {"time_to_target_s": round(red[4], 3), "ttl_steps": int(red[5]),
                "ttl_reached": bool(red[6])} if a.ttl_target > 0 else None
+        if ttl is not None and a.ttl_heldout_batches > 0:
+            hv = dict(zip(held_keys, red[7:7 + len(held_keys)]))
+            ttl.update({
+                "ttl_heldout_loss": None if hv["ttl_heldout_loss"] < 0 else round(hv["ttl_heldout_loss"], 4),
+                "ttl_heldout_acc": None if hv["ttl_heldout_acc"] < 0 else round(hv["ttl_heldout_acc"], 4),
+                "ttl_heldout_steps": None if hv["ttl_heldout_steps"] < 0 else int(hv["ttl_heldout_steps"]),
+                "ttl_heldout_reached": hv["ttl_heldout_reached"] > 0,
+                "ttl_heldout_s": None if hv["ttl_heldout_s"] < 0 else round(hv["ttl_heldout_s"], 3),
+                "ttl_eval_s": max(0.0, round(hv["ttl_eval_s"], 3)),
+                "ttl_heldout_target_acc": a.ttl_heldout_acc})
     if ctx.is_ps:
         shape_src = ctx.host_reduce([0.0, 0.0, 0.0])      # matched by workers below
     else:
@@ -448,6 +505,7 @@ def run(a):
                                    "phases_host_ms": res.get("phases_host_ms"),
                                    "comm": res.get("comm")}
     ranks = ctx.gather(mine)
+    out = None
     if info.rank == 0:
         nw = ctx.n_workers
         global_batch = a.batch * nw
@@ -516,13 +574,24 @@ def run(a):
             out.update({"ttl_target_loss": a.ttl_target,
                         "ttl_data": f"synthetic class-template images (signal {a.ttl_signal} "
                                     f"+ N(0,1) noise), one dataset of {a.ttl_batches} "
-                                    "batches shared by all workers (per-worker offsets)"})
+                                    "batches shared by all workers (per-worker offsets); "
+                                    f"held-out split of {a.ttl_heldout_batches} batches from the "
+                                    "same templates with disjoint samples, evaluated every "
+                                    f"{a.ttl_eval_every} steps"})
         if ttl_sync is not None:
             out["ttl_sync_dp"] = ttl_sync
-        print(json.dumps(out), flush=True)
     steps = a.central_check if a.central_check >= 0 else (12 if not ctx.central else 0)
+    check_ok = True
     if steps > 0 and world > 1 and a.mode == "asgd":
-        _central_check(a, cfg, ctx, steps)
+        rep = _central_check(a, cfg, ctx, steps, out)
+        if info.rank == 0:
+            out["central_check"] = rep
+            check_ok = bool(rep and rep["ok"])
+    if info.rank == 0:
+        print(json.dumps(out), flush=True)
+    shutdown()
+    if not check_ok:
+        sys.exit(3)          # the line is out, but the reference-topology check failed
     shutdown()
 
 

@@ -45,22 +45,19 @@ def _notify(*ps):
 # is <= 0 passes no gradient), or a Linear whose data-gradient epilogue masks
 # by its own ReLU'd input (EPI_DRELU) -- it registers the gradient tensor
 # here, dropout's backward forwards the registration, and the layer skips its
-# mask pass.  The check is by OBJECT identity on a live tensor (weak values):
-# a gradient that autograd accumulated or copied is a different object and is
-# masked as usual, and masking twice would be a no-op anyway.
-import weakref  # noqa: E402
-
-_RELU_MASKED: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDictionary()
-
-
+# mask pass.  The mark is an attribute of the tensor OBJECT holding its version
+# counter at marking time: a gradient that autograd accumulated or copied is a
+# different object, and one that autograd's InputBuffer accumulated a second
+# consumer's gradient into IN PLACE has a bumped version -- both are masked as
+# usual (masking twice is a no-op anyway, skipping a needed mask is not).
 def mark_relu_masked(t):
     if t is not None:
-        _RELU_MASKED[id(t)] = t
+        t._dmp_relu_masked_ver = t._version
     return t
 
 
 def is_relu_masked(t) -> bool:
-    return t is not None and _RELU_MASKED.get(id(t)) is t
+    return t is not None and getattr(t, "_dmp_relu_masked_ver", None) == t._version
 
 
 def nonneg(t) -> bool:

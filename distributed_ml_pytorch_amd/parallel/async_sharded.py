@@ -50,7 +50,8 @@ import torch
 import torch.distributed as dist
 
 from . import messaging as M
-from .clients import PSClient, _Pending
+from .clients import PSClient, _EventWork, _Pending
+from .links import PairGroupTransport, PairLinks, wait_on
 
 _LOG = logging.getLogger(__name__)
 
@@ -96,7 +97,7 @@ class ShardServer:
     groups this server receives pushes on / sends replies on."""
 
     def __init__(self, rank: int, world: int, init_shard: torch.Tensor, req_group,
-                 push_groups: dict, reply_groups: dict, scale: float = 1.0):
+                 push_groups: dict, reply_groups: dict, scale: float = 1.0, transport=None):
         self.rank, self.world = rank, world
         self.device = init_shard.device
         self.cuda = self.device.type == "cuda"
@@ -111,6 +112,14 @@ class ShardServer:
                 self.master = init_shard.detach().to(torch.float32).clone()
         else:
             self.master = init_shard.detach().to(torch.float32).clone()
+        # link-concurrent payloads (:mod:`.links`): one stream + buffer ring per
+        # (peer, direction), so pushes from different ranks land concurrently and
+        # only the applies serialise, on self.stream.  The same code path runs on
+        # CPU (gloo groups, host waits) -- the multi-process tests exercise it.
+        self.rx = PairLinks(self.device, transport or PairGroupTransport(
+            {s: g for (s, _o), g in push_groups.items()}))
+        self.tx = PairLinks(self.device, transport or PairGroupTransport(
+            {d: g for (_o, d), g in reply_groups.items()}))
         self.req = req_group
         self.push_g = push_groups
         self.reply_g = reply_groups
@@ -121,10 +130,6 @@ class ShardServer:
         self.staleness: list[int] = []
         self.error: BaseException | None = None
         self.n = self.master.numel()
-        self._rbuf: dict = {}          # (sender, dtype) -> receive buffer
-        self._sbuf: dict = {}          # dst -> reply buffer [n + 1] fp32 (GPU)
-        self._swork: dict = {}         # dst -> in-flight reply send (GPU)
-        self.tracker = M.SendTracker()
         self.thread = threading.Thread(target=self._run, daemon=True, name=f"shard-ps-{rank}")
 
     def start(self):
@@ -147,15 +152,20 @@ class ShardServer:
     def apply(self, delta: torch.Tensor, base_version: int | None = None):
         """Apply a delta from the calling thread (the co-located worker's own
         slice): on GPU ordered after the caller's current stream, run on the PS
-        stream."""
+        stream.  Returns the event marking the apply done (GPU; ``None`` on CPU):
+        ``delta`` may be overwritten only after it -- ``record_stream`` guards
+        the allocation, not a reuse of the same buffer."""
         with self.lock:
             if self.cuda:
                 self.stream.wait_stream(torch.cuda.current_stream(self.device))
                 with self._ctx():
                     self._apply_locked(delta, base_version)
+                    done = torch.cuda.Event()
+                    done.record()
                 delta.record_stream(self.stream)
-            else:
-                self._apply_locked(delta, base_version)
+                return done
+            self._apply_locked(delta, base_version)
+            return None
 
     def snapshot(self, out: torch.Tensor | None = None):
         """``(copy of the shard, version, event)``: on GPU the copy is taken on the
@@ -176,44 +186,27 @@ class ShardServer:
         if nelem != self.n:
             raise RuntimeError(f"shard {self.rank}: rank {sender} pushed {nelem} elements, "
                                f"the shard has {self.n}")
-        key = (sender, dtype)
-        buf = self._rbuf.get(key)
-        if buf is None:
-            buf = torch.empty(nelem, dtype=dtype, device=self.device)
-            self._rbuf[key] = buf
-        g = self.push_g[(sender, self.rank)]
-        if self.cuda:
-            with self.lock, self._ctx():
-                # the receive is ordered after the previous apply out of this
-                # buffer (torch makes the RCCL stream wait on the current = PS
-                # stream) and the apply after the receive (work.wait = a stream wait)
-                work = dist.irecv(buf, sender, group=g)
-                work.wait()
-                self._apply_locked(buf, version)
-        else:
-            dist.recv(buf, sender, group=g)
-            with self.lock:
-                self._apply_locked(buf, version)
+        # posted on the sender's own link stream, behind nothing but the apply
+        # that last read its ring slot; no lock: only the apply needs one
+        slot, ready = self.rx.recv(sender, nelem, dtype)
+        with self.lock, self._ctx():
+            wait_on(self.stream, ready)
+            self._apply_locked(slot.buf, version)
+            self.rx.release(slot, self.stream)
 
     def _reply(self, dst: int):
-        g = self.reply_g[(self.rank, dst)]
         n = self.n
-        if self.cuda:
-            with self.lock, self._ctx():
-                prev = self._swork.pop(dst, None)
-                if prev is not None:
-                    prev.wait()           # the previous reply has left this buffer
-                buf = self._sbuf.get(dst)
-                if buf is None:
-                    buf = torch.empty(n + 1, dtype=torch.float32, device=self.device)
-                    self._sbuf[dst] = buf
+        with self.lock:
+            version = float(self.version)
+
+            def fill(buf):
                 buf[:n].copy_(self.master)
-                buf[n:].fill_(float(self.version))
-                self._swork[dst] = dist.isend(buf, dst, group=g)
-        else:
-            with self.lock:
-                out = torch.cat([self.master, torch.tensor([float(self.version)])])
-            self.tracker.add(dist.isend(out, dst, group=g), out)
+                buf[n:].fill_(version)
+
+            # snapshot on the PS stream (after every apply enqueued so far), sent on
+            # dst's own reply-link stream; the ring slot is reused only after its
+            # previous send completed
+            self.tx.send(dst, n + 1, torch.float32, fill, self.stream)
 
     def _run(self):
         remaining = set(range(self.world)) - {self.rank}
@@ -232,12 +225,9 @@ class ShardServer:
 
     def join(self):
         self.thread.join()
-        self.tracker.drain()
+        self.rx.synchronize()
+        self.tx.synchronize()
         if self.cuda:
-            with self._ctx():
-                for w in self._swork.values():
-                    w.wait()
-            self._swork.clear()
             self.stream.synchronize()
         if self.error is not None:
             raise RuntimeError(f"shard server {self.rank} failed: {self.error!r}")
@@ -245,6 +235,8 @@ class ShardServer:
     def stats(self) -> dict:
         st = self.staleness
         return {"shard_version": self.version, "shard_counts": dict(self.counts),
+                "shard_links": dict(self.rx.counts, sends=self.tx.counts["send"],
+                                    send_reused=self.tx.counts["reused"]),
                 "shard_staleness_mean": (sum(st) / len(st)) if st else 0.0,
                 "shard_staleness_max": max(st) if st else 0}
 
@@ -252,9 +244,10 @@ class ShardServer:
 class _ShardedPull:
     """The per-shard replies of one pull (plus the local shard's snapshot)."""
 
-    def __init__(self, parts, own):
+    def __init__(self, parts, own, own_version: int = 0):
         self.parts = parts         # [(lo, hi, rbuf [hi - lo + 1], work)]
         self.own = own             # (lo, hi, buf, event)
+        self.own_version = own_version
         self.done = False
 
     def wait(self):
@@ -328,7 +321,12 @@ class AsyncShardedPSClient(PSClient):
         for o in range(self.world):
             lo, hi = self._bounds(o)
             if o == self.rank:
-                self.server.apply(buf[lo:hi], self.version)
+                done = self.server.apply(buf[lo:hi], self.version)
+                if done is not None:
+                    # the PS stream reads this slot asynchronously (and may be
+                    # parked in a slow peer's receive): the next hand-off into
+                    # the slot, two pushes later, must wait for the apply
+                    self._push_work[slot].append(_EventWork(done))
                 continue
             header = M.make_header(M.MessageCode.GradientUpdate, self.rank, step, self.version,
                                    hi - lo, buf.dtype)
@@ -363,9 +361,9 @@ class AsyncShardedPSClient(PSClient):
         lo, hi = self._bounds(self.rank)
         if self.cuda and free_ev is not None:
             self.server.stream.wait_event(free_ev)
-        _, _, ev = self.server.snapshot(bufs[self.rank])
-        self.pending.append(_Pending(step, bufs, work=_ShardedPull(parts,
-                                                                   (lo, hi, bufs[self.rank], ev))))
+        _, own_v, ev = self.server.snapshot(bufs[self.rank])
+        self.pending.append(_Pending(step, bufs, work=_ShardedPull(
+            parts, (lo, hi, bufs[self.rank], ev), own_v)))
         self.bytes_recv += self.arena.numel * 4 * (self.world - 1) // self.world
 
     def _land(self, pend):
@@ -392,17 +390,16 @@ class AsyncShardedPSClient(PSClient):
                         arena.p32[lo:hi].add_(acc[lo:hi])
             if not self.cuda and arena.w16 is not None:
                 arena.w16.copy_(arena.p32)
-        vsrcs = [rbuf[hi - lo:] for lo, hi, rbuf, _ in pull.parts]
+        # per-shard versions in shard order (the own shard's is known on the host);
+        # the landed base version is their MIN on every backend -- on GPU resolved
+        # without a host sync once the copies' event has completed
+        vsrcs = {lo // self.shard_n: rbuf[hi - lo:] for lo, hi, rbuf, _ in pull.parts}
+        vsrcs[self.rank] = torch.tensor([float(pull.own_version)])
+        self._note_versions([vsrcs[o] for o in range(self.world)])
+        ev = None
         if self.cuda:
-            for v in vsrcs:
-                self._note_version(v)
             ev = torch.cuda.Event()
             ev.record()            # the staging set is free once the land kernels ran
-        else:
-            self.shard_versions = [int(v.item()) for v in vsrcs]
-            if self.shard_versions:
-                self.version = max(self.version, min(self.shard_versions))
-            ev = None
         self.pulls += 1
         arena.bump()
         self._pull_free.append((pend.buf, ev))
@@ -421,7 +418,9 @@ class AsyncShardedPSClient(PSClient):
             torch.cuda.current_stream().wait_stream(self.server.stream)
 
     def stats(self) -> dict:
+        self._resolve_versions()
         st = super().stats()
+        st["shard_versions"] = list(self.shard_versions)
         st.update(self.server.stats())
         st["payload"] = self.payload_backend
         return st

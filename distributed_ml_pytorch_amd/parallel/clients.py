@@ -166,13 +166,38 @@ class PSClient:
         host.copy_(vsrc.reshape(1), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self._vq.append((host, ev))
+        self._vq.append((host, ev, False))
+
+    def _note_versions(self, vsrcs: list):
+        """Versions of the shards of ONE landed pull (shard order): recorded as
+        :attr:`shard_versions`, and the landed base version is their minimum.
+        Device sources are copied to pinned memory and resolved once their
+        event has completed (no host sync); host sources resolve at once."""
+        if all(v.device.type == "cpu" for v in vsrcs):
+            self._set_shard_versions([int(v.reshape(-1)[0].item()) for v in vsrcs])
+            return
+        if not hasattr(self, "_vq"):
+            self._vq = deque()
+        host = torch.empty(len(vsrcs), dtype=torch.float32, pin_memory=True)
+        for i, v in enumerate(vsrcs):
+            host[i:i + 1].copy_(v.reshape(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._vq.append((host, ev, True))
+
+    def _set_shard_versions(self, vals: list):
+        self.shard_versions = vals
+        if vals:
+            self.version = max(self.version, min(vals))
 
     def _resolve_versions(self):
         vq = getattr(self, "_vq", None)
         while vq and vq[0][1].query():
-            host, _ = vq.popleft()
-            self.version = max(self.version, int(host.item()))
+            host, _, group = vq.popleft()
+            if group:
+                self._set_shard_versions([int(x) for x in host.tolist()])
+            else:
+                self.version = max(self.version, int(host.item()))
 
     def land_due(self, step: int, force: bool = False):
         while self.pending and (force or self.pending[0].step <= step - self.staleness):

@@ -1,0 +1,218 @@
+"""Link-concurrent payload path for parameter servers.
+
+A PS GPU in the reference topology (1 PS + 7 workers on 8 GPUs) has one xGMI
+link to every worker.  The reference's PS served all workers from one receive
+loop (/root/reference/example/main.py:135-138; the worker side
+/root/reference/asgd/optim/Asynchronous.py:34,49,59), and a straight port puts
+every transfer on ONE stream: torch's RCCL p2p makes each operation's RCCL
+stream wait on the current stream, so worker B's receive cannot start before
+worker A's receive and apply have finished -- one link busy at a time.
+
+:class:`PairLinks` gives every peer its own HIP stream and its own ring of
+payload buffers:
+
+* a receive from peer ``p`` is posted on ``stream[p]`` behind nothing but the
+  apply that last read the ring slot it lands in, so receives from different
+  peers are in flight at the same time (one link each);
+* the consumer (the PS apply stream) waits on the receive's ``ready`` event
+  and applies; :meth:`PairLinks.release` after the apply frees the slot;
+* a reply is snapshotted on the apply stream (so it observes every apply
+  enqueued before it) into the peer's send ring, then sent on ``stream[p]``.
+
+The same code runs on CPU (gloo payloads, the multi-process tests): streams
+are null contexts, a receive blocks the calling thread until it has arrived,
+and a send slot is reused only after its previous send's ``Work`` completed.
+
+The payload transport is pluggable: :class:`PairGroupTransport` is RCCL (one
+2-rank communicator per pair, each with its own RCCL stream) or gloo, and a
+test substitutes a delayed device copy with the same stream semantics
+(``tests/test_train_gpu.py::test_ps_links_overlap_receives``).
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.distributed as dist
+
+from .messaging import OnceWork
+
+
+class PairGroupTransport:
+    """Point-to-point payloads on one process group per peer (RCCL pair comms;
+    ``groups[peer]`` carries every transfer to / from ``peer``)."""
+
+    def __init__(self, groups: dict):
+        self.groups = groups
+
+    def irecv(self, buf: torch.Tensor, peer: int):
+        return dist.irecv(buf, peer, group=self.groups[peer])
+
+    def isend(self, buf: torch.Tensor, peer: int):
+        return dist.isend(buf, peer, group=self.groups[peer])
+
+
+class _HostEvent:
+    """CPU stand-in for a stream event: complete once ``work`` (if any) is."""
+
+    __slots__ = ("work",)
+
+    def __init__(self, work=None):
+        self.work = work
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+
+    def query(self) -> bool:
+        return self.work is None or self.work.is_completed()
+
+
+_DONE = _HostEvent()
+
+
+def wait_on(stream, ev):
+    """Order ``stream`` after ``ev`` (GPU: a stream wait, the host never blocks;
+    CPU: the calling thread waits for the host event)."""
+    if ev is None:
+        return
+    if isinstance(ev, _HostEvent):
+        ev.wait()
+    else:
+        stream.wait_event(ev)
+
+
+class _Slot:
+    __slots__ = ("buf", "free", "work")
+
+    def __init__(self, buf):
+        self.buf = buf
+        self.free = None     # event after which buf may be overwritten
+        self.work = None     # keeps the last transfer's Work alive
+
+
+class _Ring:
+    __slots__ = ("slots", "i")
+
+    def __init__(self):
+        self.slots: list[_Slot] = []
+        self.i = 0
+
+
+class PairLinks:
+    """Per-peer streams and buffer rings (see module docstring).
+
+    ``depth`` buffers per (peer, direction, shape): a peer may have that many
+    transfers of one kind in flight before a new one waits for the oldest.
+    ``trace=True`` (GPU) records timing-event spans ``(kind, peer, start, end)``
+    of every transfer in :attr:`spans` (tests, diagnostics)."""
+
+    def __init__(self, device, transport, depth: int = 2, trace: bool = False):
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.transport = transport
+        self.depth = max(1, depth)
+        self.trace = trace and self.cuda
+        self.spans: list = []
+        self.counts = {"recv": 0, "send": 0, "reused": 0}
+        self._streams: dict[int, torch.cuda.Stream] = {}
+        self._rx: dict = {}
+        self._tx: dict = {}
+
+    def stream(self, peer: int):
+        if not self.cuda:
+            return None
+        s = self._streams.get(peer)
+        if s is None:
+            s = torch.cuda.Stream(self.device)
+            self._streams[peer] = s
+        return s
+
+    def _ctx(self, stream):
+        return torch.cuda.stream(stream) if self.cuda else contextlib.nullcontext()
+
+    def _next(self, rings: dict, key, numel: int, dtype) -> _Slot:
+        ring = rings.get(key)
+        if ring is None:
+            ring = rings[key] = _Ring()
+        if len(ring.slots) < self.depth:
+            # zero-filled: a padded tail (alloc > payload) stays zero forever
+            slot = _Slot(torch.zeros(numel, dtype=dtype, device=self.device))
+            ring.slots.append(slot)
+            return slot
+        slot = ring.slots[ring.i]
+        ring.i = (ring.i + 1) % len(ring.slots)
+        self.counts["reused"] += 1
+        return slot
+
+    def _event(self, stream=None, timing: bool = False):
+        if not self.cuda:
+            return _DONE
+        ev = torch.cuda.Event(enable_timing=timing)
+        ev.record(stream)
+        return ev
+
+    def recv(self, peer: int, numel: int, dtype, alloc: int | None = None):
+        """Post a receive of ``numel`` elements from ``peer`` on the peer's stream
+        (into the first ``numel`` of an ``alloc``-element, zero-padded buffer).
+
+        Returns ``(slot, ready)``: ``slot.buf`` holds the payload once ``ready``
+        has completed.  The caller MUST :meth:`release` the slot after its last
+        read of ``slot.buf``."""
+        alloc = numel if alloc is None else alloc
+        slot = self._next(self._rx, (peer, alloc, dtype), alloc, dtype)
+        s = self.stream(peer)
+        self.counts["recv"] += 1
+        with self._ctx(s):
+            wait_on(s, slot.free)                # the apply that last read this slot
+            start = self._event(s, True) if self.trace else None
+            view = slot.buf if alloc == numel else slot.buf[:numel]
+            slot.work = OnceWork(self.transport.irecv(view, peer)) if not self.cuda else \
+                self.transport.irecv(view, peer)
+            slot.work.wait()                     # GPU: a stream wait; CPU: arrival
+            ready = self._event(s, self.trace)
+        if self.trace:
+            self.spans.append(("recv", peer, start, ready))
+        return slot, ready
+
+    def release(self, slot: _Slot, stream=None):
+        """Mark ``slot`` reusable after the work enqueued so far on ``stream``."""
+        slot.free = self._event(stream)
+        return slot.free
+
+    def send(self, peer: int, numel: int, dtype, fill, fill_stream) -> _Slot:
+        """``fill(buf)`` on ``fill_stream`` (after the send that last used the
+        slot completed), then send ``buf`` to ``peer`` on the peer's stream."""
+        slot = self._next(self._tx, (peer, numel, dtype), numel, dtype)
+        self.counts["send"] += 1
+        with self._ctx(fill_stream):
+            wait_on(fill_stream, slot.free)
+            fill(slot.buf)
+            filled = self._event(fill_stream)
+        s = self.stream(peer)
+        with self._ctx(s):
+            wait_on(s, filled)
+            start = self._event(s, True) if self.trace else None
+            if self.cuda:
+                slot.work = self.transport.isend(slot.buf, peer)
+                slot.work.wait()
+                slot.free = self._event(s, self.trace)
+            else:
+                # gloo reads the buffer when the peer's receive is posted: the slot
+                # is free once that send has completed
+                slot.work = OnceWork(self.transport.isend(slot.buf, peer))
+                slot.free = _HostEvent(slot.work)
+        if self.trace:
+            self.spans.append(("send", peer, start, slot.free))
+        return slot
+
+    def synchronize(self):
+        if self.cuda:
+            for s in self._streams.values():
+                s.synchronize()
+            return
+        for rings in (self._tx, self._rx):
+            for ring in rings.values():
+                for slot in ring.slots:
+                    if slot.work is not None:
+                        slot.work.wait()

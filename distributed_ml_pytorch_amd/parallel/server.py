@@ -16,8 +16,12 @@ staleness), per-worker liveness, periodic checkpoints, and two payload paths:
 * ``payload="gloo"`` - headers and payloads on the (CPU) gloo group;
 * ``payload="rccl"`` - headers on a CPU gloo control group, payloads on a
   per-(PS, worker) RCCL communicator on the PS GPU.  The shard, the apply
-  kernel and the reply snapshots stay on the GPU; one PS stream orders
-  ``recv -> apply`` and ``apply -> snapshot -> send`` without host syncs.
+  kernel and the reply snapshots stay on the GPU, and the links run
+  concurrently (:mod:`.links`): every worker's receives and sends are posted
+  on that worker's own stream and buffer ring, so transfers from different
+  workers overlap (one xGMI link each); only the applies and the reply
+  snapshots are serialised, on the apply stream, each after ITS receive's
+  event.  No host syncs anywhere.
 """
 from __future__ import annotations
 
@@ -33,6 +37,7 @@ import torch.distributed as dist
 
 from . import messaging as M
 from .arena import FlatArena
+from .links import PairGroupTransport, PairLinks, wait_on
 
 _LOG = logging.getLogger(__name__)
 
@@ -61,7 +66,8 @@ class ParameterServer:
     def __init__(self, model=None, numel: int | None = None, workers=None, control_group=None,
                  pair_groups=None, payload: str = "auto", device=None, init_policy: str = "first",
                  checkpoint_path: str | None = None, checkpoint_every: int = 0,
-                 worker_timeout: float | None = None, delta_scale: str | float = "sum"):
+                 worker_timeout: float | None = None, delta_scale: str | float = "sum",
+                 transport=None, trace_links: bool = False):
         """``delta_scale``: factor on every pushed delta -- ``"sum"`` (1.0, the
         reference Downpour PS: /root/reference/asgd/optim/Asynchronous.py:48-55
         ships raw accumulated updates that the PS adds), ``"mean"`` (1 / #workers:
@@ -84,10 +90,14 @@ class ParameterServer:
         self.payload = payload
         self.ctrl = control_group
         self.pairs = pair_groups or {}
+        self.links = None
         if payload == "rccl":
-            if not self.pairs:
+            if not self.pairs and transport is None:
                 raise ValueError("payload='rccl' needs pair_groups from make_ps_groups()")
             self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
+            # ``transport``: the pair groups (RCCL) unless a test substitutes one
+            self.links = PairLinks(self.device, transport or PairGroupTransport(self.pairs),
+                                   trace=trace_links)
         else:
             self.device = torch.device(device or "cpu")
         if model is not None:
@@ -117,9 +127,7 @@ class ParameterServer:
         self.checkpoint_every = checkpoint_every
         self._tracker = M.SendTracker()
         self._hq = None
-        self._send_bufs: dict[int, torch.Tensor] = {}
-        self._send_work: dict[int, object] = {}
-        self._recv_bufs = defaultdict(dict)
+        self._recv_bufs = defaultdict(dict)      # gloo payload path
         self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         if self.device.type == "cuda":
             from ..ops._ext import native
@@ -129,43 +137,43 @@ class ParameterServer:
             self._native = None
 
     # -------------------------------------------------------------- payload io
-    def _recv_payload(self, sender: int, nelem: int, dtype: torch.dtype) -> torch.Tensor:
+    def _recv_payload(self, sender: int, nelem: int, dtype: torch.dtype):
+        """Receive ``sender``'s payload -> ``(buf, ready_event, slot)``.
+
+        Device path: posted on the sender's own link stream (:class:`PairLinks`);
+        ``ready`` marks arrival, ``slot`` is released by the consumer.  gloo
+        path: a blocking receive, ``ready`` and ``slot`` are ``None``."""
         if nelem != self.numel:
             raise RuntimeError(f"PS: worker {sender} sent {nelem} elements, the shard has "
                                f"{self.numel} (model/arena layout mismatch)")
         padded = nelem + ((-nelem) % 4)
+        self.bytes_in += nelem * torch.empty(0, dtype=dtype).element_size()
+        if self.links is not None:
+            slot, ready = self.links.recv(sender, nelem, dtype, alloc=padded)
+            return slot.buf, ready, slot
         bufs = self._recv_bufs[sender]
         buf = bufs.get(dtype)
         if buf is None or buf.numel() != padded:
             buf = torch.zeros(padded, dtype=dtype, device=self.device)
             bufs[dtype] = buf
-        view = buf[:nelem]
-        if self.payload == "rccl":
-            with torch.cuda.stream(self.stream):
-                work = dist.irecv(view, src=sender, group=self.pairs[sender])
-                work.wait()   # PS stream waits on the RCCL stream; host not blocked
-        else:
-            dist.recv(view, src=sender, group=self.ctrl, tag=M.TAG_PAYLOAD)
-        self.bytes_in += nelem * view.element_size()
-        return buf
+        dist.recv(buf[:nelem], src=sender, group=self.ctrl, tag=M.TAG_PAYLOAD)
+        return buf, None, None
 
     def _reply(self, dst: int):
         """ParameterUpdate to ``dst``: the shard followed by one fp32 element holding
         the PS version (number of applied deltas) the snapshot was taken at, so
         the worker can report its staleness on its next push."""
         n = self.numel
-        if self.payload == "rccl":
-            with torch.cuda.stream(self.stream):
-                prev = self._send_work.pop(dst, None)
-                if prev is not None:
-                    prev.wait()
-                buf = self._send_bufs.get(dst)
-                if buf is None:
-                    buf = torch.empty(n + 1, dtype=torch.float32, device=self.device)
-                    self._send_bufs[dst] = buf
-                buf[:n].copy_(self.shard[:n])   # snapshot: later applies never tear the reply
-                buf[n:].fill_(float(self.version))
-                self._send_work[dst] = dist.isend(buf, dst, group=self.pairs[dst])
+        if self.links is not None:
+            version = float(self.version)
+
+            def fill(buf):
+                buf[:n].copy_(self.shard[:n])   # snapshot: later applies never tear it
+                buf[n:].fill_(version)
+
+            # snapshot on the apply stream (after every apply enqueued so far),
+            # send on dst's own link stream
+            self.links.send(dst, n + 1, torch.float32, fill, self.stream)
         else:
             snap = torch.empty(n + 1, dtype=torch.float32)
             snap[:n].copy_(self.shard[:n])
@@ -174,34 +182,44 @@ class ParameterServer:
             self._tracker.add(w, snap)
         self.bytes_out += (n + 1) * 4
 
-    def _apply(self, delta: torch.Tensor):
+    def _apply(self, delta: torch.Tensor, ready=None, slot=None):
+        """``shard += scale * delta``; on GPU on the apply stream, after ``ready``
+        (the delta's receive), releasing the receive ``slot`` when done."""
         if self._native is not None:
             with torch.cuda.stream(self.stream):
+                wait_on(self.stream, ready)
                 self._native.ps_apply(self.shard, delta, None, self.delta_scale)
+                if slot is not None:
+                    self.links.release(slot, self.stream)
         else:
             self.shard[: self.numel].add_(delta[: self.numel].to(torch.float32),
                                           alpha=self.delta_scale)
         self.version += 1
 
-    def _set(self, params: torch.Tensor):
+    def _set(self, params: torch.Tensor, ready=None, slot=None):
         with torch.cuda.stream(self.stream) if self.stream is not None else _null():
+            wait_on(self.stream, ready)
             self.shard[: self.numel].copy_(params[: self.numel])
+            if slot is not None:
+                self.links.release(slot, self.stream)
 
     # -------------------------------------------------------------------- loop
     def handle(self, code, sender: int, step: int, version: int, nelem: int, dtype):
         self.counts[code.name] += 1
         self.last_seen[sender] = time.monotonic()
         if code == M.MessageCode.GradientUpdate:
-            delta = self._recv_payload(sender, nelem, dtype)
+            delta, ready, slot = self._recv_payload(sender, nelem, dtype)
             self.staleness.append(self.version - version)
-            self._apply(delta)
+            self._apply(delta, ready, slot)
             if self.checkpoint_every and self.version % self.checkpoint_every == 0:
                 self.save_checkpoint()
         elif code == M.MessageCode.ParameterUpdate:
-            params = self._recv_payload(sender, nelem, dtype)
+            params, ready, slot = self._recv_payload(sender, nelem, dtype)
             if not self.initialized or self.init_policy == "last":
-                self._set(params)
+                self._set(params, ready, slot)
                 self.initialized = True
+            elif slot is not None:
+                slot.free = ready        # never read: free once it has arrived
         elif code == M.MessageCode.ParameterRequest:
             self._reply(sender)
         elif code == M.MessageCode.Checkpoint:
@@ -283,10 +301,9 @@ class ParameterServer:
         return self.stats()
 
     def finish(self):
-        for w in list(self._send_work.values()):
-            w.wait()
-        self._send_work.clear()
         self._tracker.drain()
+        if self.links is not None:
+            self.links.synchronize()
         if self.stream is not None:
             self.stream.synchronize()
         if self.checkpoint_path:

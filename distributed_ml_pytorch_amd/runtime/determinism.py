@@ -14,10 +14,13 @@ What the mode does (:func:`enable_determinism`):
 
 * compute in fp32 on PyTorch's own kernels -- the framework's fp32 oracle
   path (``--dtype fp32``: ops/functional.py routes every fp32 GPU op to ATen /
-  MIOpen / hipBLASLt) -- with ``torch.use_deterministic_algorithms(True)``,
-  MIOpen's deterministic algorithm selection (``cudnn.deterministic``, no
-  benchmark autotuning) and a fixed hipBLASLt workspace, so no kernel reduces
-  through atomics;
+  MIOpen / hipBLASLt) -- with ``torch.use_deterministic_algorithms(True)``
+  (errors, not warnings: an op without a deterministic implementation stops
+  the run instead of silently breaking the guarantee), MIOpen's deterministic
+  algorithm selection (``cudnn.deterministic``, no benchmark autotuning) and
+  PyTorch's fixed BLAS workspace (``CUBLAS_WORKSPACE_CONFIG``, which PyTorch
+  reads for its hipBLAS(Lt) handles on ROCm too; set before any handle exists),
+  so no kernel reduces through atomics;
 * keep everything else of the framework unchanged: the flat fp32 arena, the
   fused elementwise optimizer kernels (one thread per element: deterministic),
   the PS machinery and its push/pull cadence, the hipGraph capture.
@@ -44,8 +47,7 @@ _LOG = logging.getLogger(__name__)
 def enable_determinism(cfg):
     """Switch the process to deterministic kernels; return ``cfg`` with fp32 compute."""
     os.environ.setdefault("CUBLAS_WORKSPACE_CONFIG", ":4096:8")
-    os.environ.setdefault("HIPBLASLT_WORKSPACE_CONFIG", ":4096:8")
-    torch.use_deterministic_algorithms(True, warn_only=True)
+    torch.use_deterministic_algorithms(True, warn_only=False)
     torch.backends.cudnn.deterministic = True
     torch.backends.cudnn.benchmark = False
     if cfg.dtype != "fp32":

@@ -196,10 +196,12 @@ class Worker:
         """
         can = self.device.type == "cuda"
         if self.ddp is not None and self.info.is_distributed:
-            # gloo collectives cannot be captured; RCCL ones can, but capturing
-            # them at N > 1 is opt-in (DMP_GRAPH_SYNC=1) until measured on a
-            # multi-GPU node -- eager bucket all-reduces otherwise
-            can = can and self.info.backend == "nccl" and os.environ.get("DMP_GRAPH_SYNC") == "1"
+            # gloo collectives cannot be captured; RCCL ones are, by default: eager
+            # sync DP pays the host launch of every dispatch (~350 per ResNet-50
+            # step, profiles/sync_capture_ab_r4.txt).  A capture that fails falls
+            # back to eager stepping (_capture); DMP_GRAPH_SYNC=0 forces eager.
+            can = can and self.info.backend == "nccl" and \
+                os.environ.get("DMP_GRAPH_SYNC", "1") != "0"
         self.use_graph = bool(enabled) and can
         self.graph = None
         return self.use_graph

@@ -168,6 +168,28 @@ class DeviceBatchPool:
         return self.next()
 
 
+TTL_TRAIN_SEED = 100
+TTL_HELDOUT_SEED = 100 + 7919
+
+
+def ttl_pools(batch: int, shape, num_classes: int, device, n_train: int, n_heldout: int,
+              dtype=torch.bfloat16, signal: float = 0.05):
+    """Train and held-out pools of the time-to-target data.
+
+    Both draw ``signal * template[label] + N(0, 1)`` from the SAME class
+    templates (so the held-out split measures generalisation of the same task)
+    with different generator seeds, so no held-out sample is a training sample
+    (``tests/test_core_cpu.py::test_ttl_heldout_split_is_disjoint``).  The
+    reference scores training by its test set the same way
+    (/root/reference/example/main.py:83-89,110-131)."""
+    train = DeviceBatchPool(batch, shape, num_classes, device, n_batches=n_train, dtype=dtype,
+                            seed=TTL_TRAIN_SEED, learnable=True, signal=signal)
+    held = DeviceBatchPool(batch, shape, num_classes, device, n_batches=n_heldout, dtype=dtype,
+                           seed=TTL_HELDOUT_SEED, learnable=True, signal=signal) \
+        if n_heldout > 0 else None
+    return train, held
+
+
 def env_int(name: str, default: int) -> int:
     try:
         return int(os.environ.get(name, default))

@@ -74,6 +74,52 @@ def test_async_sharded_every_push_applied_once():
         assert st["pushes"] == steps
 
 
+def _math_delayed(rank, world, steps, lr, delay):
+    """n_push=1 < n_pull=4 with one slow rank: every ring slot of the link path
+    (parallel/links.py) is reused many times while the slow peer's pushes and
+    pull requests arrive late and interleaved with the fast ranks'."""
+    from distributed_ml_pytorch_amd.parallel.async_sharded import AsyncShardedPSClient
+    from distributed_ml_pytorch_amd.parallel.asgd import Asynchronous
+
+    torch.manual_seed(0)
+    m = nn.Linear(6, 5)
+    opt = Asynchronous(m.parameters(), lr=lr, n_push=1, n_pull=4, model=m,
+                       client=AsyncShardedPSClient(staleness=2), shadow_dtype=None)
+    for k in range(steps):
+        if rank == world - 1:
+            time.sleep(delay)
+        opt.zero_grad()
+        for p in m.parameters():
+            p.grad.copy_(_grad(rank, k, p))
+        opt.step()
+    opt.finish()
+    st = opt.stats()
+    shards = [torch.zeros_like(opt.client.master) for _ in range(world)]
+    dist.all_gather(shards, opt.client.master)
+    return {"master": torch.cat(shards).numpy(), "stats": st}
+
+
+def test_async_sharded_link_rings_with_a_slow_peer():
+    world, steps, lr = 3, 12, 0.1
+    out = _run(_math_delayed, world, steps, lr, 0.05)
+    want = _sum_of_pushes(world, steps, lr)
+    n_pulls = len(range(0, steps, 4))
+    for r in range(world):
+        got = torch.from_numpy(out[r]["master"])
+        # every delta applied exactly once, none lost to a reused slot
+        torch.testing.assert_close(got[: want.numel()], want, rtol=1e-5, atol=1e-5)
+        st = out[r]["stats"]
+        assert st["shard_version"] == world * steps
+        links = st["shard_links"]
+        assert links["recv"] == (world - 1) * steps
+        assert links["reused"] >= (world - 1) * (steps - 2)     # depth-2 rings
+        assert links["sends"] == (world - 1) * n_pulls
+        # landed versions: one per shard, the base version is their minimum
+        assert len(st["shard_versions"]) == world
+        assert st["version"] == min(st["shard_versions"])
+        assert st["shard_staleness_max"] >= 0
+
+
 def _straggler(rank, world, kind, pause):
     from distributed_ml_pytorch_amd.parallel.async_sharded import AsyncShardedPSClient
     from distributed_ml_pytorch_amd.parallel.asgd import Asynchronous

@@ -233,6 +233,28 @@ def test_synthetic_data_is_learnable():
     assert (pred == ds2.y).float().mean() > 0.5
 
 
+def test_ttl_heldout_split_is_disjoint():
+    """bench.py's held-out split: same class templates as the TTL training data,
+    no sample in common with it, and a template classifier fitted on the
+    training split scores it far above chance (same task)."""
+    from distributed_ml_pytorch_amd.utils.data import ttl_pools
+
+    tr, he = ttl_pools(64, (3, 8, 8), 10, "cpu", n_train=6, n_heldout=3,
+                       dtype=torch.float32, signal=0.5)
+    xtr, ytr = torch.cat(tr.x).flatten(1), torch.cat(tr.y)
+    xhe, yhe = torch.cat(he.x).flatten(1), torch.cat(he.y)
+    assert xhe.shape == (3 * 64, 3 * 8 * 8)
+    # disjoint: no held-out row equals any training row
+    d = torch.cdist(xhe, xtr)
+    assert float(d.min()) > 1.0
+    # same templates: nearest class mean of the TRAINING split classifies held-out
+    t = torch.stack([xtr[ytr == c].mean(0) for c in range(10)])
+    acc = ((xhe @ t.t()).argmax(1) == yhe).float().mean()
+    assert acc > 0.5, acc
+    # both pools cover every class
+    assert set(yhe.tolist()) == set(range(10)) == set(ytr.tolist())
+
+
 def test_cifar_binary_reader(tmp_path):
     import numpy as np
 

@@ -48,11 +48,12 @@ def test_bench_self_spawns_n_ranks():
     assert out["config"]["global_batch"] == 32
     assert out["backend"] == "gloo" and out["dtype"].startswith("fp32")
     assert "sharded" in out["config"]["parallelism"]
-    # after the line: the reference topology (1 PS + 3 workers) over the pair
-    # payload communicators, reported on stderr
+    # after the timed runs: the reference topology (1 PS + 3 workers) over the
+    # pair payload communicators, reported in the line (and on stderr)
     chk = [ln for ln in r.stderr.splitlines() if ln.startswith("[central-check] ")]
     assert len(chk) == 1, r.stderr[-3000:]
     rep = json.loads(chk[0].split(" ", 1)[1])
+    assert out["central_check"] == rep
     assert rep["ok"] and rep["payload"] == "gloo" and len(rep["workers"]) == 3
     assert rep["ps"]["counts"]["GradientUpdate"] == 3 * 6     # 12 steps / n_push 2, 3 workers
     assert all(wk["pushes"] == 6 and wk["pulls"] == 6 for wk in rep["workers"])
@@ -102,6 +103,11 @@ def test_bench_central_ps_with_time_to_target():
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     out = json.loads(lines[0])
     assert out["ttl_reached"] and out["ttl_steps"] <= 200
+    # held-out split scored through the no-grad path (worker means, on the PS's line)
+    assert 0.0 <= out["ttl_heldout_acc"] <= 1.0 and out["ttl_heldout_loss"] > 0
+    assert out["ttl_heldout_target_acc"] == 0.8
+    if out["ttl_heldout_reached"]:
+        assert out["ttl_heldout_steps"] % 50 == 0
 
 
 def test_bench_rejects_world_size_mismatch():

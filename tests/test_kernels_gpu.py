@@ -469,3 +469,35 @@ def test_xent_ignore_index_grad_is_mean_over_valid_rows(C):
     torch.testing.assert_close(loss.float(), lr, rtol=1e-2, atol=1e-3)
     assert float((x.grad.float() - xr.grad).norm() / xr.grad.norm()) < 1e-2
     assert float(x.grad[::3].float().abs().max()) == 0.0
+
+
+def test_relu_mask_hand_off_with_two_consumers():
+    """A fused-ReLU conv output feeding BOTH a max-pool (whose backward marks its
+    gradient as already relu'-masked) and a second consumer: autograd sums the
+    two gradients (possibly in place into the pool's tensor), so the conv must
+    mask the SUM.  Compared against fp32 PyTorch."""
+    import torch.nn.functional as F
+
+    from distributed_ml_pytorch_amd.ops.functional import max_pool2d
+    from distributed_ml_pytorch_amd.ops.layers import Conv2d
+
+    torch.manual_seed(0)
+    conv = Conv2d(64, 64, 3, padding=1, bias=False).cuda()
+    x = torch.randn(4, 64, 16, 16, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    c = torch.randn(4, 64, 16, 16, device="cuda")
+    ga = torch.randn(4, 64, 8, 8, device="cuda")
+    for order in ("pool_first", "mul_first"):
+        conv.weight.grad = None
+        y = conv(x, relu=True)
+        if order == "pool_first":
+            loss = (max_pool2d(y, 2).float() * ga).sum() + (y.float() * c).sum()
+        else:
+            loss = (y.float() * c).sum() + (max_pool2d(y, 2).float() * ga).sum()
+        loss.backward()
+        wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+        yr = F.relu(F.conv2d(x.float(), wr, None, 1, 1))
+        lr = (F.max_pool2d(yr, 2) * ga).sum() + (yr * c).sum()
+        lr.backward()
+        rel = float((conv.weight.grad - wr.grad).norm() / wr.grad.norm())
+        assert rel < 2e-2, (order, rel)
