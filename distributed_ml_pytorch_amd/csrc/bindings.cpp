@@ -470,7 +470,7 @@ ConvGeom conv_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad
 
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bool want_stats,
                              int64_t cfg, optional<Tensor> slots, optional<Tensor> bias,
-                             bool relu) {
+                             bool relu, optional<Tensor> addend) {
   check_nhwc_bf16(x, "x");
   check_gpu(w, "w");
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -491,13 +491,60 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, bo
     G = dmp::kBnSlots;
     part = bn_slots(slots, g.CO, x.options());
   }
+  const uint16_t* add_ptr = nullptr;
+  Tensor add_t;
+  if (addend.has_value() && addend->defined()) {
+    // residual added before the ReLU (inference-time BatchNorm fold, ops/eval_fold.py)
+    add_t = addend->contiguous(at::MemoryFormat::ChannelsLast);
+    check_nhwc_bf16(add_t, "addend");
+    TORCH_CHECK(add_t.sizes() == y.sizes(), "conv_fwd: addend must have the output's shape");
+    add_ptr = reinterpret_cast<const uint16_t*>(add_t.data_ptr());
+  }
   dmp::launch_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                        reinterpret_cast<const uint16_t*>(w.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()),
                        want_stats ? part.data_ptr<float>() : nullptr, g.B, g.H, g.W, g.CI, g.OH,
                        g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream(),
-                       bias ? bias->data_ptr<float>() : nullptr, relu);
+                       bias ? bias->data_ptr<float>() : nullptr, relu, add_ptr);
   return {y, part, at::scalar_tensor(G, at::kLong)};
+}
+
+// Inference-time BatchNorm fold into the producing conv / GEMM (csrc/bn.hip):
+// returns (w16 = bf16(w * s) with w's shape and memory format, t fp32 [CO],
+// t bf16 [CO]), s = gamma / sqrt(running_var + eps), t = beta + (cbias - mean) * s.
+std::vector<Tensor> bn_fold_weights(Tensor w, optional<Tensor> gamma, optional<Tensor> beta,
+                                    Tensor rmean, Tensor rvar, optional<Tensor> cbias,
+                                    double eps) {
+  check_gpu(w, "w");
+  TORCH_CHECK(w.scalar_type() == at::kFloat, "bn_fold_weights: fp32 master weight");
+  const bool cl = w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(cl || w.is_contiguous(), "bn_fold_weights: contiguous or channels_last weight");
+  const int64_t CO = w.size(0);
+  const int64_t n = w.numel();
+  TORCH_CHECK(n % (4 * CO) == 0, "bn_fold_weights: elements per output channel % 4 != 0");
+  for (auto* t : {&gamma, &beta, &cbias}) {
+    if (t->has_value() && (*t)->defined()) {
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat &&
+                      (*t)->is_contiguous() && (*t)->numel() == CO,
+                  "bn_fold_weights: affine / bias tensors must be contiguous fp32 [CO]");
+    } else {
+      t->reset();
+    }
+  }
+  for (auto* t : {&rmean, &rvar})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                    t->numel() == CO,
+                "bn_fold_weights: running stats must be contiguous fp32 [CO]");
+  auto w16 = at::empty_like(w, w.options().dtype(at::kBFloat16));
+  auto b32 = at::empty({CO}, w.options());
+  auto b16 = at::empty({CO}, w.options().dtype(at::kBFloat16));
+  dmp::launch_bn_fold_weights(w.data_ptr<float>(), ptr_or_null<float>(gamma),
+                              ptr_or_null<float>(beta), rmean.data_ptr<float>(),
+                              rvar.data_ptr<float>(), ptr_or_null<float>(cbias),
+                              reinterpret_cast<uint16_t*>(w16.data_ptr()), b32.data_ptr<float>(),
+                              reinterpret_cast<uint16_t*>(b16.data_ptr()), n, (int)CO, (float)eps,
+                              cur_stream());
+  return {w16, b32, b16};
 }
 
 void conv_weight_transpose_batched(Tensor src, Tensor dst, Tensor table, int64_t max_elems) {
@@ -1477,7 +1524,11 @@ PYBIND11_MODULE(_native, m) {
   m.def("conv_fwd", &conv_fwd, "NHWC bf16 implicit-GEMM conv forward (+BN partials)",
         py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("want_stats"),
         py::arg("cfg") = -1, py::arg("slots") = py::none(), py::arg("bias") = py::none(),
-        py::arg("relu") = false);
+        py::arg("relu") = false, py::arg("addend") = py::none());
+  m.def("bn_fold_weights", &bn_fold_weights,
+        "inference-time BatchNorm fold: (bf16 w * s, fp32 shift, bf16 shift)", py::arg("w"),
+        py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
+        py::arg("cbias") = py::none(), py::arg("eps") = 1e-5);
   m.def("conv_dgrad", &conv_dgrad, "NHWC bf16 implicit-GEMM conv data gradient", py::arg("dy"),
         py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"),
         py::arg("cfg") = -1, py::arg("wt") = py::none(), py::arg("addend") = py::none(),

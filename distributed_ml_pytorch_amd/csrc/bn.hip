@@ -770,3 +770,52 @@ void launch_bn_fwd_partials(const u16* x, const u16* res, u16* y, const float* g
   bn_apply(x, res, stats, y, mask, M, C, relu, s);
 }
 }  // namespace dmp
+
+namespace dmp {
+// ------------------------------------------------ inference-time BatchNorm folding
+// Eval-mode BN is a per-channel affine map of its input, so BN(conv(x, W)) +
+// residual, ReLU = conv(x, W * s) + t (+ residual), ReLU with
+//   s[co] = gamma / sqrt(running_var + eps),  t[co] = beta + (conv_bias - running_mean) * s:
+// the conv's own epilogue (bias, residual addend, ReLU) then IS the BN -- no
+// statistics, finalize or apply pass (the reference's evaluation loop,
+// /root/reference/example/main.py:110-125).  One launch per conv: every
+// thread scales 4 consecutive weights of one output channel (fp32 master ->
+// bf16 compute weight, ONE rounding as the arena's bf16 shadow has); threads
+// co < CO also write t (fp32 for the conv epilogues, bf16 for the GEMM route).
+__global__ void __launch_bounds__(256) bn_fold_weights_kernel(
+    const float4* __restrict__ w, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ rmean, const float* __restrict__ rvar, const float* __restrict__ cbias,
+    bf16x4* __restrict__ w16, float* __restrict__ b32, u16* __restrict__ b16, long long n4,
+    int per_co4, int CO, float eps) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n4) {
+    const int co = (int)(i / per_co4);
+    const float s = (gamma ? gamma[co] : 1.f) * rsqrtf(rvar[co] + eps);
+    const float4 v = w[i];
+    bf16x4 o;
+    o.v[0] = f2bf(v.x * s);
+    o.v[1] = f2bf(v.y * s);
+    o.v[2] = f2bf(v.z * s);
+    o.v[3] = f2bf(v.w * s);
+    w16[i] = o;
+  }
+  if (i < CO) {
+    const int co = (int)i;
+    const float s = (gamma ? gamma[co] : 1.f) * rsqrtf(rvar[co] + eps);
+    const float t = (beta ? beta[co] : 0.f) + ((cbias ? cbias[co] : 0.f) - rmean[co]) * s;
+    if (b32) b32[co] = t;
+    if (b16) b16[co] = f2bf(t);
+  }
+}
+
+void launch_bn_fold_weights(const float* w, const float* gamma, const float* beta,
+                            const float* rmean, const float* rvar, const float* cbias,
+                            uint16_t* w16, float* b32, uint16_t* b16, long long n, int CO,
+                            float eps, hipStream_t s) {
+  const long long n4 = n / 4;
+  const long long threads = n4 > CO ? n4 : CO;
+  hipLaunchKernelGGL(bn_fold_weights_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     s, reinterpret_cast<const float4*>(w), gamma, beta, rmean, rvar, cbias,
+                     reinterpret_cast<bf16x4*>(w16), b32, b16, n4, (int)(n / CO / 4), CO, eps);
+}
+}  // namespace dmp

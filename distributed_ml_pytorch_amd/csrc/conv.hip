@@ -32,6 +32,14 @@
 #include "common.h"
 #include "launchers.h"
 
+// Roofline ablations (scripts/conv_roofline.py builds a separate library with
+// -DDMP_ABLATE=N; the extension itself is always built with 0):
+//   1 = staging only (every global->LDS DMA, no MFMA work),
+//   2 = MFMA only (the first stage is staged, later ones re-read it).
+#ifndef DMP_ABLATE
+#define DMP_ABLATE 0
+#endif
+
 namespace dmp {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -337,8 +345,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.y, 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
   // dgrad accumulate: dX = dgrad + addend (the residual branch's gradient of the
-  // same input, fused here instead of an autograd add over the whole tensor)
-  const bool add_in = MODE == 1 && a.addend != nullptr && (!a.addend_sub || blockIdx.z == 0);
+  // same input, fused here instead of an autograd add over the whole tensor);
+  // forward: the residual of an inference-time BatchNorm fold, before the ReLU
+  const bool add_in = a.addend != nullptr && (MODE == 0 || !a.addend_sub || blockIdx.z == 0);
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
   constexpr bool BNB = MODE == 1 && STATS;   // fused BN(+ReLU) backward
@@ -524,7 +533,7 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
   const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.y, 0, (int)(2LL * Mtot * a.CO), 0x00020000);
   const bool add_in = S2 ? (a.addend != nullptr && (!a.addend_sub || cls == 0))
-                         : (FLIP && a.addend != nullptr);
+                         : (a.addend != nullptr);   // dgrad residual grad / fwd BN-fold residual
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
   constexpr bool BNB = FLIP && STATS;   // fused BN(+ReLU) backward
@@ -814,19 +823,19 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
       wait_vm<0>();                       // chunk c landed (this wave's DMAs) ...
       __builtin_amdgcn_s_barrier();       // ... for every wave; chunk c-1's slot is free
       asm volatile("" ::: "memory");
-      if (c + 1 < KC) stage((c + 1) & 1, c + 1);
-      compute(c & 1);
+      if (c + 1 < KC && DMP_ABLATE != 2) stage((c + 1) & 1, c + 1);
+      if (DMP_ABLATE != 1) compute(DMP_ABLATE == 2 ? 0 : c & 1);
     }
   } else {
     // one stage: half the LDS, so two or three blocks share a CU and one
     // block's load / epilogue overlaps another's MFMA work
     for (int c = 0; c < KC; ++c) {
       if (c > 0) __syncthreads();         // everyone done reading chunk c-1
-      stage(0, c);
+      if (c == 0 || DMP_ABLATE != 2) stage(0, c);
       wait_vm<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      compute(0);
+      if (DMP_ABLATE != 1) compute(0);
     }
   }
   __syncthreads();   // all stage reads done before the epilogue reuses LDS
@@ -1205,7 +1214,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   // loaded (inline asm, counted by hand) BEFORE the next tile's DMA is issued,
   // so the deferred epilogue waits only for them, never for that DMA
   typedef unsigned int u32x2_a __attribute__((ext_vector_type(2)));
-  const bool add_in = FLIP && a.addend != nullptr;
+  const bool add_in = a.addend != nullptr;   // dgrad residual grad / fwd BN-fold residual
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * P * a.CO), 0x00020000);
   u32x2_a ad[TM][TN];
@@ -1305,13 +1314,13 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     __builtin_amdgcn_s_barrier();       // ... for every wave; slot (k-1) % NS is free
     asm volatile("" ::: "memory");
     if (k > 0 && add_in) aload(k - 1);
-    stage((k + NS - 1) % NS, k + NS - 1);
+    if (DMP_ABLATE != 2) stage((k + NS - 1) % NS, k + NS - 1);
     if (k > 0) epilogue(k - 1, false);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    compute(k % NS);
+    if (DMP_ABLATE != 1) compute(DMP_ABLATE == 2 ? 0 : k % NS);
   }
   if (add_in) aload(nt - 1);
   epilogue(nt - 1, true);
@@ -1745,9 +1754,12 @@ int conv_fwd_num_mblocks(long long M, int CO, int cfg) {
 
 void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int H, int W,
                      int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
-                     hipStream_t s, const float* bias, bool relu) {
+                     hipStream_t s, const float* bias, bool relu, const u16* addend) {
+  // addend: a [B][OH][OW][CO] residual added before the ReLU (the inference-time
+  // BatchNorm fold: BN(conv) + shortcut, ReLU = conv with folded weights + bias
+  // + addend, ReLU -- ops/eval_fold.py)
   ConvArgs a{x, w, y, part, B, H, W, CI, OH, OW, CO, R, S, stride, pad,
-             (long long)B * OH * OW, bias, nullptr, relu ? 1 : 0};
+             (long long)B * OH * OW, bias, addend, relu ? 1 : 0};
   if (cfg >= kHaloBase) {
     if (part ? launch_halo<false, true>(a, cfg, s) : launch_halo<false, false>(a, cfg, s)) return;
     cfg = -1;   // not applicable to this geometry: heuristic implicit-GEMM tile

@@ -26,6 +26,10 @@
 
 #include "common.h"
 
+#ifndef DMP_ABLATE
+#define DMP_ABLATE 0   // roofline ablations: see conv.hip
+#endif
+
 namespace dmp {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -531,8 +535,8 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
     else wait_vm_rt(vm_wait);           // tile `it` landed (this wave's DMAs) ...
     __builtin_amdgcn_s_barrier();       // ... for every wave; slot (it-1) % NS is free
     asm volatile("" ::: "memory");
-    stage((it + NS - 1) % NS, t_begin + it + NS - 1);
-    compute(it % NS);
+    if (DMP_ABLATE != 2) stage((it + NS - 1) % NS, t_begin + it + NS - 1);
+    if (DMP_ABLATE != 1) compute(DMP_ABLATE == 2 ? 0 : it % NS);
   }
   wait_vm<0>();
   if constexpr (PG == 2) {

@@ -36,6 +36,13 @@ void launch_softmax_xent_f32(const float* logits, const int64_t* labels, float* 
 
 // bn.hip
 int bn_num_partials(long long M, int C);
+// inference-time BN folding into the producing conv (bn.hip): w16 = bf16(w * s),
+// b32 / b16 (either may be null) = beta + (conv_bias - running_mean) * s, per output channel
+// s = gamma / sqrt(running_var + eps); w is the fp32 [CO][...] master, n % (4 * CO) == 0
+void launch_bn_fold_weights(const float* w, const float* gamma, const float* beta,
+                            const float* rmean, const float* rvar, const float* cbias,
+                            uint16_t* w16, float* b32, uint16_t* b16, long long n, int CO,
+                            float eps, hipStream_t s);
 void launch_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma,
                    const float* beta, float* running_mean, float* running_var, float* stats,
                    float* part, long long M, int C, float momentum, float eps, bool training,
@@ -130,7 +137,8 @@ long long conv_wgrad_halo_slab_elems(int cfg, int B, int H, int W, int CI, int C
                                      int stride, int pad);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int B, int H,
                      int W, int CI, int OH, int OW, int CO, int R, int S, int stride, int pad,
-                     int cfg, hipStream_t s, const float* bias = nullptr, bool relu = false);
+                     int cfg, hipStream_t s, const float* bias = nullptr, bool relu = false,
+                     const uint16_t* addend = nullptr);
 // Backward of the BatchNorm(+ReLU) that produced a conv's input, fused into the
 // conv's data-gradient epilogue (conv.hip bnb_*): the dgrad stores dz and adds
 // sum(dz), sum(dz * xhat) per channel into the BN's backward slot buffer.

@@ -9,7 +9,10 @@ the north-star metric is ResNet-18 samples/s.  Two stems:
   25,557,032 parameters.
 
 Every conv is followed by a fused BN(+residual)(+ReLU) kernel pair; the
-block output ``relu(bn2(conv2(h)) + shortcut)`` is ONE kernel on GPU.
+block output ``relu(bn2(conv2(h)) + shortcut)`` is ONE kernel on GPU.  In eval
+mode under ``no_grad`` (the reference's evaluation loop) every BatchNorm is
+folded into its conv instead (ops/eval_fold.py): one launch per conv, none
+per BatchNorm.
 """
 from __future__ import annotations
 
@@ -19,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import layers as L
+from ..ops.eval_fold import conv_bn, fold_enabled
 
 
 # 1x1 / stride-2 shortcuts on conv1's subsampled alias (DMP_SC_SUB=0: full-res
@@ -46,7 +50,20 @@ class BasicBlock(nn.Module):
             self.shortcut = nn.Sequential(
                 L.Conv2d(cin, planes, 1, stride=stride, bias=False), L.BatchNorm2d(planes))
 
+    def _forward_folded(self, x):
+        h = conv_bn(x, self.conv1, self.bn1)
+        if h is None:
+            return None
+        sc = x if self.shortcut is None else conv_bn(x, self.shortcut[0], self.shortcut[1])
+        if sc is None:
+            return None
+        return conv_bn(h, self.conv2, self.bn2, residual=sc)
+
     def forward(self, x):
+        if fold_enabled(x, self):
+            y = self._forward_folded(x)
+            if y is not None:
+                return y
         # the shortcut reads x through conv1's alias: its gradient is summed into
         # x's gradient by conv1's dgrad epilogue (no autograd add).  A 1x1 /
         # stride-2 shortcut takes conv1's subsampled alias x[:, :, ::2, ::2] and
@@ -81,7 +98,21 @@ class Bottleneck(nn.Module):
             self.shortcut = nn.Sequential(
                 L.Conv2d(cin, out, 1, stride=stride, bias=False), L.BatchNorm2d(out))
 
+    def _forward_folded(self, x):
+        h = conv_bn(x, self.conv1, self.bn1)
+        h = conv_bn(h, self.conv2, self.bn2) if h is not None else None
+        if h is None:
+            return None
+        sc = x if self.shortcut is None else conv_bn(x, self.shortcut[0], self.shortcut[1])
+        if sc is None:
+            return None
+        return conv_bn(h, self.conv3, self.bn3, residual=sc)
+
     def forward(self, x):
+        if fold_enabled(x, self):
+            y = self._forward_folded(x)
+            if y is not None:
+                return y
         # a 1x1 / stride-2 shortcut reads conv1's subsampled alias and runs at
         # stride 1 (a GEMM); its gradient is added onto dX's even pixels after
         # conv1's dgrad (see BasicBlock)
@@ -136,7 +167,9 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn2.weight)
 
     def forward(self, x):
-        h = self.bn1(self.conv1(x))
+        h = conv_bn(x, self.conv1, self.bn1) if fold_enabled(x, self) else None
+        if h is None:
+            h = self.bn1(self.conv1(x))
         if self.pool is not None:
             h = self.pool(h)
         h = self.layer4(self.layer3(self.layer2(self.layer1(h))))

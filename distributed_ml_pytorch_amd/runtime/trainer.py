@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 
 from ..models import build_model
+from ..ops.eval_fold import fold_session
 from ..ops.functional import softmax_cross_entropy, unit_grad
 from ..parallel.arena import attach_arena
 from ..parallel.asgd import Asynchronous
@@ -311,22 +312,23 @@ class Worker:
         conf = torch.zeros(c * c, device=self.device, dtype=torch.int64) if per_class else None
         n = 0
         nb = 0
-        for xb, yb in loader:
-            xb, yb = self.prepare(xb, yb)
-            out = self.model(xb)
-            loss, hits = softmax_cross_entropy(out, yb)
-            tot_loss += loss.float() * yb.numel()
-            tot_hits += hits.to(torch.int64)
-            if conf is not None:
-                pred = out.float().argmax(1)
-                # rows with an ignored / out-of-range label are skipped, as the
-                # loss kernel skips them (bincount rejects negative indices)
-                ok = (yb >= 0) & (yb < c)
-                conf += torch.bincount((yb * c + pred)[ok], minlength=c * c)
-            n += yb.numel()
-            nb += 1
-            if max_batches and nb >= max_batches:
-                break
+        with fold_session():                 # eval BatchNorms folded into their convs once
+            for xb, yb in loader:
+                xb, yb = self.prepare(xb, yb)
+                out = self.model(xb)
+                loss, hits = softmax_cross_entropy(out, yb)
+                tot_loss += loss.float() * yb.numel()
+                tot_hits += hits.to(torch.int64)
+                if conf is not None:
+                    pred = out.float().argmax(1)
+                    # rows with an ignored / out-of-range label are skipped, as the
+                    # loss kernel skips them (bincount rejects negative indices)
+                    ok = (yb >= 0) & (yb < c)
+                    conf += torch.bincount((yb * c + pred)[ok], minlength=c * c)
+                n += yb.numel()
+                nb += 1
+                if max_batches and nb >= max_batches:
+                    break
         self.model.train(was)
         if n == 0:
             res = (float("nan"), float("nan"))

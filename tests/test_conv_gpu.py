@@ -142,6 +142,105 @@ def test_halo_conv_configs(B, C, H, W, CO):
         assert _rel(dw, 2 * wr.grad) < 1e-2, cfg
 
 
+@pytest.mark.parametrize("B,H", [(3, 32), (1, 32), (2, 56), (5, 16)])
+@pytest.mark.parametrize("with_add", [False, True])
+def test_halo64p_addend_matrix(B, H, with_add):
+    """The persistent 64-channel kernels (ids 115-117) load their residual addend
+    with inline-asm loads whose completion the epilogue counts by hand (vmcnt):
+    every config x {no addend, full addend} x {odd batch, B = 1, 56x56, a tile
+    count that does not fill the grid evenly}, forward (+fp32 bias, ReLU: the
+    inference-time BN fold) and data gradient vs fp32."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    torch.manual_seed(1)
+    C = 64
+    x = torch.randn(B, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(C, C, 3, 3, device="cuda") / (C * 9) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    bias = torch.randn(C, device="cuda") * 0.1
+    add = torch.randn_like(x) if with_add else None
+    xr = x.float().requires_grad_(True)
+    yr = F.conv2d(xr, w.float(), None, 1, 1)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr.backward(dy.float())
+    ref_f = torch.relu(yr.detach() + bias.view(1, -1, 1, 1) + (add.float() if with_add else 0))
+    ref_d = xr.grad + (add.float() if with_add else 0)
+    ran = 0
+    for cfg in (115, 116, 117):
+        if cfg not in list(nat.conv_halo_configs(H, H, C, 3, 3, 1, 1)):
+            continue
+        ran += 1
+        y, _, _ = nat.conv_fwd(x, w, 1, 1, False, cfg, None, bias, True, add)
+        assert torch.isfinite(y.float()).all(), cfg
+        assert _rel(y, ref_f) < 1e-2, (cfg, _rel(y, ref_f))
+        dx = nat.conv_dgrad(dy, w, H, H, 1, 1, cfg, None, add)
+        assert torch.isfinite(dx.float()).all(), cfg
+        assert _rel(dx, ref_d) < 1e-2, (cfg, _rel(dx, ref_d))
+    assert ran > 0
+
+
+@pytest.mark.parametrize("cfg_kind", ["halo", "igemm"])
+def test_conv_fwd_bias_addend_relu_epilogue(cfg_kind):
+    """Forward epilogue of the inference-time BN fold on the non-persistent tiles:
+    relu(conv(x) + bias + addend), every applicable config."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    torch.manual_seed(2)
+    B, C, H, CO = 3, 128, 16, 128
+    x = torch.randn(B, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(CO, C, 3, 3, device="cuda") / (C * 9) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    bias = torch.randn(CO, device="cuda") * 0.1
+    add = torch.randn(B, CO, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    ref = torch.relu(F.conv2d(x.float(), w.float(), None, 1, 1) + bias.view(1, -1, 1, 1)
+                     + add.float())
+    from distributed_ml_pytorch_amd.ops.conv import _igemm_candidates
+
+    cfgs = list(nat.conv_halo_configs(H, H, C, 3, 3, 1, 1)) if cfg_kind == "halo" else \
+        _igemm_candidates(CO)
+    for cfg in cfgs:
+        y, _, _ = nat.conv_fwd(x, w, 1, 1, False, cfg, None, bias, True, add)
+        assert _rel(y, ref) < 1e-2, (cfg, _rel(y, ref))
+
+
+@pytest.mark.parametrize("model,shape", [("resnet18", (3, 32, 32)), ("resnet50", (3, 64, 64))])
+def test_eval_bn_fold_matches_unfolded_eval(model, shape):
+    """Eval forward with every BatchNorm folded into its conv (ops/eval_fold.py)
+    == the regular eval forward (running-statistics BN passes), after a few
+    training steps moved the running statistics away from their init."""
+    import os
+
+    from distributed_ml_pytorch_amd.models import build_model
+    from distributed_ml_pytorch_amd.ops import eval_fold
+    from distributed_ml_pytorch_amd.ops.functional import softmax_cross_entropy
+    from distributed_ml_pytorch_amd.parallel.arena import attach_arena
+
+    torch.manual_seed(0)
+    m, _, nc = build_model(model)
+    m = m.cuda()
+    attach_arena(m, shadow_dtype=torch.bfloat16, channels_last=True)
+    x = torch.randn(6, *shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    y = torch.randint(0, nc, (6,), device="cuda")
+    for _ in range(3):                       # move the running stats (train mode)
+        loss, _ = softmax_cross_entropy(m(x), y)
+        loss.backward()
+    m.eval()
+    with torch.no_grad():
+        eval_fold._FOLD = False
+        try:
+            ref = m(x).float()
+        finally:
+            eval_fold._FOLD = True
+        with eval_fold.fold_session():
+            out = m(x).float()
+            out2 = m(x).float()                # cached fold
+    assert _rel(out, ref) < 2e-2, _rel(out, ref)
+    assert torch.equal(out, out2)
+    m.train()
+
+
 def test_conv_layer_autograd_and_bn_fusion():
     """Conv2d(native) -> BatchNorm2d(partials) matches the stock fp32 chain."""
     from distributed_ml_pytorch_amd.ops import layers as L
