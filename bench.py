@@ -20,11 +20,15 @@ Topologies (``--ps``):
   predictor (loss ln 10, profiles/ttl_n8_delta_scale_r2.txt).
   The collectives make it lock-step at pull time (bounded drift).
 * ``sharded_async``: the same 1/N shards, each served by its own PS thread
-  (point-to-point gloo push/pull, host-staged payloads): no collective after
-  start-up, so a late rank delays only its own shard's replies.
+  (parallel/async_sharded.py): gloo headers, point-to-point payloads on one
+  2-rank group per direction (RCCL on GPUs, device-resident shards, every peer
+  on its own link stream: parallel/links.py); no collective after start-up, so
+  a late rank delays only its own shard's replies.  Its GPU test runs at world
+  1 (no peer): the multi-rank link code is exercised by the CPU gloo tests.
 * ``central``: the reference topology (/root/reference/Makefile:13-20,
   example/main.py:135-138): rank 0 is the parameter server (fp32 master on its
-  GPU, payloads over one RCCL communicator per (PS, worker) pair, headers on a
+  GPU, payloads over one RCCL communicator per (PS, worker) pair, each pair on
+  its own stream so transfers to different workers overlap, headers on a
   gloo control group), ranks 1..N-1 are workers; pushed deltas are averaged
   over the workers by default (``--delta-scale auto``; ``sum`` = the reference).  Whole-node samples/s counts
   the workers' samples only (the PS GPU trains nothing).
@@ -95,9 +99,11 @@ def parse(argv=None):
                          "data until the mean loss of 10 steps <= target and report the "
                          "wall time (the metric's time-to-target-loss half); 0 skips")
     ap.add_argument("--ttl-max-steps", type=int, default=4000)
-    ap.add_argument("--ttl-signal", type=float, default=0.05,
-                    help="class-template amplitude of the time-to-target images (0.05: ~1000 "
-                         "steps to loss 0.5 at N=1, profiles/ttl_calibration_r2.txt)")
+    ap.add_argument("--ttl-signal", type=float, default=0.1,
+                    help="class-template amplitude of the time-to-target images (0.1: ~540 "
+                         "steps to training loss 0.5 and held-out accuracy 0.7 at ~650 steps at "
+                         "N=1; at 0.05 the training loss fell by memorising the set while the "
+                         "held-out accuracy stayed at 0.26: profiles/ttl_heldout_calibration_r4.txt)")
     ap.add_argument("--ttl-batches", type=int, default=128, help="distinct TTL batches (one dataset, all ranks)")
     ap.add_argument("--ttl-heldout-batches", type=int, default=8,
                     help="held-out split of the TTL data: same class templates, disjoint samples "
@@ -105,7 +111,7 @@ def parse(argv=None):
                          "--ttl-eval-every steps as the reference evaluates on its test set "
                          "(/root/reference/example/main.py:83-89,110-131); 0 skips")
     ap.add_argument("--ttl-eval-every", type=int, default=50)
-    ap.add_argument("--ttl-heldout-acc", type=float, default=0.8,
+    ap.add_argument("--ttl-heldout-acc", type=float, default=0.7,
                     help="held-out accuracy target: ttl_heldout_steps = first evaluation at or above it")
     ap.add_argument("--central-check", type=int, default=-1,
                     help="after the JSON line, at N>1: STEPS of the reference topology (rank 0 "

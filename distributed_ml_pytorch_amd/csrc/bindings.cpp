@@ -521,7 +521,7 @@ std::vector<Tensor> bn_fold_weights(Tensor w, optional<Tensor> gamma, optional<T
   TORCH_CHECK(cl || w.is_contiguous(), "bn_fold_weights: contiguous or channels_last weight");
   const int64_t CO = w.size(0);
   const int64_t n = w.numel();
-  TORCH_CHECK(n % (4 * CO) == 0, "bn_fold_weights: elements per output channel % 4 != 0");
+  TORCH_CHECK(n % CO == 0, "bn_fold_weights: weight [CO, ...] expected");
   for (auto* t : {&gamma, &beta, &cbias}) {
     if (t->has_value() && (*t)->defined()) {
       TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat &&

@@ -778,26 +778,22 @@ namespace dmp {
 //   s[co] = gamma / sqrt(running_var + eps),  t[co] = beta + (conv_bias - running_mean) * s:
 // the conv's own epilogue (bias, residual addend, ReLU) then IS the BN -- no
 // statistics, finalize or apply pass (the reference's evaluation loop,
-// /root/reference/example/main.py:110-125).  One launch per conv: every
-// thread scales 4 consecutive weights of one output channel (fp32 master ->
-// bf16 compute weight, ONE rounding as the arena's bf16 shadow has); threads
-// co < CO also write t (fp32 for the conv epilogues, bf16 for the GEMM route).
+// /root/reference/example/main.py:110-125).  One launch per conv, once per
+// evaluation pass (ops/eval_fold.py): every thread scales one weight of one
+// output channel (fp32 master -> bf16 compute weight, ONE rounding as the
+// arena's bf16 shadow has; any elements-per-channel count, e.g. the 27 of a
+// 3x3x3 stem); threads co < CO also write t (fp32 for the conv epilogues, bf16
+// for the GEMM route).
 __global__ void __launch_bounds__(256) bn_fold_weights_kernel(
-    const float4* __restrict__ w, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ w, const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ rmean, const float* __restrict__ rvar, const float* __restrict__ cbias,
-    bf16x4* __restrict__ w16, float* __restrict__ b32, u16* __restrict__ b16, long long n4,
-    int per_co4, int CO, float eps) {
+    u16* __restrict__ w16, float* __restrict__ b32, u16* __restrict__ b16, long long n,
+    int per_co, int CO, float eps) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n4) {
-    const int co = (int)(i / per_co4);
+  if (i < n) {
+    const int co = (int)(i / per_co);
     const float s = (gamma ? gamma[co] : 1.f) * rsqrtf(rvar[co] + eps);
-    const float4 v = w[i];
-    bf16x4 o;
-    o.v[0] = f2bf(v.x * s);
-    o.v[1] = f2bf(v.y * s);
-    o.v[2] = f2bf(v.z * s);
-    o.v[3] = f2bf(v.w * s);
-    w16[i] = o;
+    w16[i] = f2bf(w[i] * s);
   }
   if (i < CO) {
     const int co = (int)i;
@@ -812,10 +808,9 @@ void launch_bn_fold_weights(const float* w, const float* gamma, const float* bet
                             const float* rmean, const float* rvar, const float* cbias,
                             uint16_t* w16, float* b32, uint16_t* b16, long long n, int CO,
                             float eps, hipStream_t s) {
-  const long long n4 = n / 4;
-  const long long threads = n4 > CO ? n4 : CO;
+  const long long threads = n > CO ? n : CO;
   hipLaunchKernelGGL(bn_fold_weights_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                     s, reinterpret_cast<const float4*>(w), gamma, beta, rmean, rvar, cbias,
-                     reinterpret_cast<bf16x4*>(w16), b32, b16, n4, (int)(n / CO / 4), CO, eps);
+                     s, w, gamma, beta, rmean, rvar, cbias, w16, b32, b16, n, (int)(n / CO), CO,
+                     eps);
 }
 }  // namespace dmp

@@ -35,7 +35,10 @@
 // Roofline ablations (scripts/conv_roofline.py builds a separate library with
 // -DDMP_ABLATE=N; the extension itself is always built with 0):
 //   1 = staging only (every global->LDS DMA, no MFMA work),
-//   2 = MFMA only (the first stage is staged, later ones re-read it).
+//   2 = MFMA only (the first stage is staged, later ones re-read it),
+//   3 = no epilogue (accumulators kept live, nothing stored),
+//   4 = no fragment reads after a stage's first steps (MFMAs on stale
+//       registers: the LDS read path removed from the MFMA loop).
 #ifndef DMP_ABLATE
 #define DMP_ABLATE 0
 #endif
@@ -779,6 +782,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
     constexpr int KS = BK / 32, NSTEP = 9 * KS;
     bf16x8 af[2][TM], bw[2][TN];
     auto load = [&](int st, int slot) {
+      if (DMP_ABLATE == 4 && st >= 2) return;
       const int t = st / KS, ks = st % KS;
       const int rowoff = (t / 3) * HW2 + (t % 3);
       const int wt = FLIP ? 8 - t : t;
@@ -839,6 +843,13 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
     }
   }
   __syncthreads();   // all stage reads done before the epilogue reuses LDS
+  if constexpr (DMP_ABLATE == 3) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   halo_epilogue<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h);
 }
 
@@ -1159,6 +1170,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     constexpr int PD = (TM * TN <= 8 && NW == 4) ? 2 : 1, NB = PD + 1;
     bf16x8 af[NB][TM], bw[NB][TN];
     auto load = [&](int st, int slot) {
+      if (DMP_ABLATE == 4 && st >= PD) return;
       const int t = st / KS, ks = st % KS;
       const int rowoff = (t / 3) * W2 + (t % 3);
       const int wt = FLIP ? 8 - t : t;
@@ -1315,7 +1327,14 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     asm volatile("" ::: "memory");
     if (k > 0 && add_in) aload(k - 1);
     if (DMP_ABLATE != 2) stage((k + NS - 1) % NS, k + NS - 1);
-    if (k > 0) epilogue(k - 1, false);
+    if (DMP_ABLATE == 3) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else if (k > 0) {
+      epilogue(k - 1, false);
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1323,7 +1342,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     if (DMP_ABLATE != 1) compute(DMP_ABLATE == 2 ? 0 : k % NS);
   }
   if (add_in) aload(nt - 1);
-  epilogue(nt - 1, true);
+  if (DMP_ABLATE != 3) epilogue(nt - 1, true);
   if (STATS) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)

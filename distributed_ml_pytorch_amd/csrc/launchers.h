@@ -38,7 +38,7 @@ void launch_softmax_xent_f32(const float* logits, const int64_t* labels, float* 
 int bn_num_partials(long long M, int C);
 // inference-time BN folding into the producing conv (bn.hip): w16 = bf16(w * s),
 // b32 / b16 (either may be null) = beta + (conv_bias - running_mean) * s, per output channel
-// s = gamma / sqrt(running_var + eps); w is the fp32 [CO][...] master, n % (4 * CO) == 0
+// s = gamma / sqrt(running_var + eps); w is the fp32 [CO][...] master
 void launch_bn_fold_weights(const float* w, const float* gamma, const float* beta,
                             const float* rmean, const float* rvar, const float* cbias,
                             uint16_t* w16, float* b32, uint16_t* b16, long long n, int CO,

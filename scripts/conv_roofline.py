@@ -10,6 +10,9 @@ process (cdna_hip_programming.md §5.4 rule 24):
 * ``fill``  -- DMP_ABLATE=1: every global->LDS DMA of the kernel, no MFMA;
 * ``mfma``  -- DMP_ABLATE=2: the MFMA work (and epilogue) on the first staged
   tile, no further DMA;
+* ``noepi`` -- DMP_ABLATE=3: everything but the epilogue (halo fwd / dgrad);
+* ``nolds`` -- DMP_ABLATE=4: the fragment reads of the MFMA loop removed
+  (halo fwd / dgrad; the wgrad kernels are unchanged in 3 and 4);
 
 and the fill ceiling of the chip (a DMA-only microkernel streaming 1-KiB
 ``buffer_load ... lds`` pieces per wave from an L2-resident and an HBM-sized
@@ -46,7 +49,7 @@ def build_libs(force=False):
     srcs = [CSRC / "conv.hip", CSRC / "conv_wgrad.hip", CSRC / "ablate" / "ablate_entry.hip"]
     hdrs = list(CSRC.glob("*.h"))
     procs = []
-    for n in (0, 1, 2):
+    for n in (0, 1, 2, 3, 4):
         out = LIBDIR / f"abl{n}.so"
         if not force and out.exists() and all(out.stat().st_mtime > s.stat().st_mtime
                                               for s in srcs + hdrs):
@@ -151,7 +154,7 @@ def main():
     from distributed_ml_pytorch_amd.ops._ext import native
 
     nat = native()
-    libs = {n: ctypes.CDLL(str(LIBDIR / f"abl{n}.so")) for n in (0, 1, 2)}
+    libs = {n: ctypes.CDLL(str(LIBDIR / f"abl{n}.so")) for n in (0, 1, 2, 3, 4)}
     for lib in libs.values():
         for fn in ("abl_conv_fwd", "abl_conv_dgrad", "abl_conv_wgrad", "abl_dma_ceiling"):
             getattr(lib, fn).restype = ctypes.c_int
@@ -188,7 +191,7 @@ def main():
     ]
     print("\n== per kernel (us; interleaved rounds, median of 3)", flush=True)
     hdr = (f"{'layer':16s} {'pass':5s} {'cfg':>5s} {'full':>7s} {'abl0':>7s} {'fill':>7s} "
-           f"{'mfma':>7s} {'TF/s':>6s} {'%peak':>5s} {'MB stg':>7s} {'GB/s/CU':>7s} "
+           f"{'mfma':>7s} {'noepi':>7s} {'nolds':>7s} {'TF/s':>6s} {'%peak':>5s} {'MB stg':>7s} {'GB/s/CU':>7s} "
            f"{'B/clk':>5s} {'fill%':>5s} {'mfma%':>5s}")
     print(hdr, flush=True)
     rows = []
@@ -207,8 +210,9 @@ def main():
         dx = torch.empty_like(x)
         flop = 2.0 * B * H * W * CO * CI * 9
         for op in ("fwd", "dgrad", "wgrad"):
-            key = ([op, B, CI, H, W, CO, 3, 3, 1, 1] if op != "wgrad"
-                   else [op, B, CI, H, W, CO, CI, 3, 3, 1, 1])
+            key = {"fwd": [op, B, CI, H, W, CO, 3, 3, 1, 1],
+                   "dgrad": [op, B, CO, H, W, CI, H, W, 3, 3, 1, 1],
+                   "wgrad": [op, B, CI, H, W, CO, CI, 3, 3, 1, 1]}[op]
             cfg = tune.get(json.dumps(key))
             if cfg is None:
                 continue
@@ -238,7 +242,8 @@ def main():
                                                   ptr(slab) if slab is not None and slab.numel() > 1
                                                   else P(0), stream)
 
-            arms = {"full": full, "abl0": lib_fn(0), "fill": lib_fn(1), "mfma": lib_fn(2)}
+            arms = {"full": full, "abl0": lib_fn(0), "fill": lib_fn(1), "mfma": lib_fn(2),
+                    "noepi": lib_fn(3), "nolds": lib_fn(4)}
             ts = {k: [] for k in arms}
             for _ in range(3):
                 for k, fn in arms.items():
@@ -255,7 +260,7 @@ def main():
                      mfma_share=round(100 * med["mfma"] / med["full"], 1))
             rows.append(r)
             print(f"{name:16s} {op:5s} {cfg:5d} {med['full']:7.1f} {med['abl0']:7.1f} "
-                  f"{med['fill']:7.1f} {med['mfma']:7.1f} {tfs:6.0f} {r['pct_peak']:5.1f} "
+                  f"{med['fill']:7.1f} {med['mfma']:7.1f} {med['noepi']:7.1f} {med['nolds']:7.1f} {tfs:6.0f} {r['pct_peak']:5.1f} "
                   f"{r['staged_mb'] or 0:7.1f} {gbcu:7.1f} {r['b_clk_cu']:5.1f} "
                   f"{r['fill_share']:5.1f} {r['mfma_share']:5.1f}", flush=True)
     print("\nJSON " + json.dumps({"ceiling_gb_s_cu": {f"{k[0] >> 20}MiB_{k[1]}w_{k[2]}k": round(v, 1)

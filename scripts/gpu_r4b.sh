@@ -2,6 +2,7 @@
 # Round 4: link test per HW-queue count, eval-fold + halo64p addend tests, eval timing inside
 # training, TTL signal calibration with held-out, conv roofline ablations.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out && export TMPDIR=/tmp
+timeout -k 10 120 python -u scripts/stream_overlap_probe.py > gpurun_out/stream_probe.log 2>&1; cat gpurun_out/stream_probe.log
 timeout -k 10 400 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider \
   tests/test_links_gpu.py "tests/test_conv_gpu.py::test_halo64p_addend_matrix" \
   "tests/test_conv_gpu.py::test_conv_fwd_bias_addend_relu_epilogue" \

@@ -105,7 +105,7 @@ def test_bench_central_ps_with_time_to_target():
     assert out["ttl_reached"] and out["ttl_steps"] <= 200
     # held-out split scored through the no-grad path (worker means, on the PS's line)
     assert 0.0 <= out["ttl_heldout_acc"] <= 1.0 and out["ttl_heldout_loss"] > 0
-    assert out["ttl_heldout_target_acc"] == 0.8
+    assert out["ttl_heldout_target_acc"] == 0.7
     if out["ttl_heldout_reached"]:
         assert out["ttl_heldout_steps"] % 50 == 0
 
