@@ -675,6 +675,132 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
   }
 }
 
+#ifndef DMP_HALO_EPI_LDS
+#define DMP_HALO_EPI_LDS 0
+#endif
+
+
+// Row-staged variant of halo_epilogue (no S2, no fused BN backward): the D^T
+// fragments (lane: 4 channels of one pixel -> 16 rows x 32-B pieces per store
+// instruction) are staged through the free LDS as a [BM][BN + 8] bf16 block
+// tile, then every wave moves whole 16-B row segments: 8 channels of one pixel
+// per lane, a pixel's BN channels contiguous -- the stores (and the residual
+// addend loads) go out as full 128-B lines (BN = 64) instead of 32-B pieces.
+// fp32 math before the staging: acc + bias (+ ReLU when no addend follows);
+// with an addend the staged bf16 value gets the addend, then the ReLU, in the
+// row phase.  BN partial sums (STATS) of the stored values: per lane over its
+// rows, shuffle-reduced over the lanes of one channel chunk, LDS across waves,
+// one atomic pair per channel per block (slot blockIdx % kBnSlots).
+template <int BM, int BN, int WM, int WN, bool FLIP, bool STATS, int TM, int TN>
+__device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&acc)[TM][TN],
+                                                   long long m0, int n0, int wm, int wn, int tid,
+                                                   int lane, u16* lds_h) {
+  constexpr int NW = WM * WN, PITCH = BN + 8, CPR = BN / 8, RPI = 64 / CPR;
+  static_assert(BN % 8 == 0 && 64 % CPR == 0, "row segments of 8 channels");
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  const long long Mtot = (long long)a.B * a.OH * a.OW;
+  const bool add_in = a.addend != nullptr;
+  const bool relu = !FLIP && a.relu;
+  // phase 1: fp32 epilogue math that needs no addend, bf16, into the block tile
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+    float bj[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bj[r] = (!FLIP && a.bias != nullptr && n0 + nl + r < a.CO) ? a.bias[n0 + nl + r] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
+      float t[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        t[r] = acc[i][j][r] + bj[r];
+        if (relu && !add_in) t[r] = fmaxf(t[r], 0.f);
+      }
+      uint2 pk;
+      pk.x = (u32)f2bf(t[0]) | ((u32)f2bf(t[1]) << 16);
+      pk.y = (u32)f2bf(t[2]) | ((u32)f2bf(t[3]) << 16);
+      *reinterpret_cast<uint2*>(lds_h + ml * PITCH + nl) = pk;
+    }
+  }
+  __syncthreads();
+  // phase 2: row segments; wave w takes rows w*RPI + k*NW*RPI + lane/CPR
+  const int wid = tid >> 6, lr = lane / CPR, ch = lane - lr * CPR;
+  const int n = n0 + ch * 8;
+  const bool nok = n < a.CO;
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.y, 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  constexpr int NR = (BM + NW * RPI - 1) / (NW * RPI);
+  unsigned off[NR];
+  u32x4_t xa[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    const int ml = (q * NW + wid) * RPI + lr;
+    const long long m = m0 + ml;
+    off[q] = (ml < BM && m < Mtot && nok) ? 2u * (unsigned)(m * a.CO + n) : kOOB;
+    if (add_in) xa[q] = __builtin_amdgcn_raw_buffer_load_b128(rsAdd, off[q], 0, 0);
+  }
+  float s_sum[8], s_sq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s_sum[e] = 0.f; s_sq[e] = 0.f; }
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    const int ml = min((q * NW + wid) * RPI + lr, BM - 1);
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(lds_h + ml * PITCH + ch * 8);
+    if (add_in) {
+      const bf16x8 xv = __builtin_bit_cast(bf16x8, xa[q]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = bf2f(v.v[e]) + bf2f(xv.v[e]);
+        if (relu) t = fmaxf(t, 0.f);
+        v.v[e] = f2bf(t);
+      }
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rsY, off[q], 0, 0);
+    if (STATS && off[q] != kOOB) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float yv = bf2f(v.v[e]);
+        s_sum[e] += yv;
+        s_sq[e] += yv * yv;
+      }
+    }
+  }
+  if constexpr (STATS) {
+    // lanes of one channel chunk differ in the bits above CPR
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s_sum[e] += __shfl_xor(s_sum[e], o, 64);
+        s_sq[e] += __shfl_xor(s_sq[e], o, 64);
+      }
+    __syncthreads();                                  // every row segment read the tile
+    float* red = reinterpret_cast<float*>(lds_h);     // [NW][BN] sums, then [NW][BN] squares
+    if (lr == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[wid * BN + ch * 8 + e] = s_sum[e];
+        red[NW * BN + wid * BN + ch * 8 + e] = s_sq[e];
+      }
+    }
+    __syncthreads();
+    for (int nl = tid; nl < BN; nl += 64 * NW) {
+      if (n0 + nl < a.CO) {
+        float ss = 0.f, qq = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) { ss += red[w * BN + nl]; qq += red[NW * BN + w * BN + nl]; }
+        const int slot = blockIdx.x % kBnSlots;
+        atomicAdd(a.part + (long long)slot * a.CO + n0 + nl, ss);
+        atomicAdd(a.part + (long long)(kBnSlots + slot) * a.CO + n0 + nl, qq);
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int BK, int WM, int WN, int NS, bool FLIP, bool STATS>
 __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, HaloGeom hg) {
   constexpr int NW = WM * WN;
@@ -850,7 +976,13 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
       for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  halo_epilogue<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h);
+  // the data gradient stores through the row-staged epilogue (-5..-9 % on the
+  // 128 / 256-channel layers, no change on the forward, whose BN sums cost
+  // more in the row layout: profiles/conv_roofline_r4.txt)
+  if constexpr ((DMP_HALO_EPI_LDS || FLIP) && !(FLIP && STATS))
+    halo_epilogue_rows<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h);
+  else
+    halo_epilogue<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h);
 }
 
 // ------------------------------- 3x3 stride-2 data gradient, halo tiles
@@ -1249,8 +1381,39 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
 #pragma unroll
   for (int j = 0; j < kHpAPW; ++j)
     if (j < APW && (NS != 2 || wid + j * NW < hg.AINS)) ++dma_pw;
-  auto epilogue = [&](int k, bool last) {
+  // the store of one 16 x 16 fragment (i, j) of tile k from accumulators `src`
+  auto epi_one = [&](int k, f32x4 (&src)[TM][TN], int i, int j) {
     const int m0 = tile_of(k) * BM;
+    const int m = m0 + wid * (BM / NW) + i * 16 + (lane & 15);
+    const bool mok = m < P;
+    const unsigned rowoff = 2u * (unsigned)(m * a.CO);
+    const int n = n0 + j * 16 + 4 * (lane >> 4);
+    const bool ok = mok && n < a.CO;
+    float av[4] = {0.f, 0.f, 0.f, 0.f};
+    if (add_in) {
+      av[0] = __uint_as_float(ad[i][j].x << 16);
+      av[1] = __uint_as_float(ad[i][j].x & 0xffff0000u);
+      av[2] = __uint_as_float(ad[i][j].y << 16);
+      av[3] = __uint_as_float(ad[i][j].y & 0xffff0000u);
+    }
+    u16 hv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float t = src[i][j][r] + bj[j][r] + av[r];
+      if (!FLIP && a.relu) t = fmaxf(t, 0.f);
+      hv[r] = f2bf(t);
+      if (STATS) {
+        const float v = ok ? bf2f(hv[r]) : 0.f;
+        s_sum[j][r] += v;
+        s_sq[j][r] += v * v;
+      }
+    }
+    const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
+    __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
+  };
+  // addend rows of the tile being stored have landed (they were issued BEFORE
+  // the next stage's DMA: wait until only those dma_pw pieces may be in flight)
+  auto addend_wait = [&](bool last) {
     if (add_in) {
       if (last) wait_vm<0>();
       else wait_vm_n(dma_pw);
@@ -1259,38 +1422,13 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
 #pragma unroll
         for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(ad[i][j]));
     }
+  };
+  auto epilogue = [&](int k, bool last) {
+    addend_wait(last);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wid * (BM / NW) + i * 16 + (lane & 15);
-      const bool mok = m < P;
-      const unsigned rowoff = 2u * (unsigned)(m * a.CO);
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + j * 16 + 4 * (lane >> 4);
-        const bool ok = mok && n < a.CO;
-        float av[4] = {0.f, 0.f, 0.f, 0.f};
-        if (add_in) {
-          av[0] = __uint_as_float(ad[i][j].x << 16);
-          av[1] = __uint_as_float(ad[i][j].x & 0xffff0000u);
-          av[2] = __uint_as_float(ad[i][j].y << 16);
-          av[3] = __uint_as_float(ad[i][j].y & 0xffff0000u);
-        }
-        u16 hv[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float t = acc[i][j][r] + bj[j][r] + av[r];
-          if (!FLIP && a.relu) t = fmaxf(t, 0.f);
-          hv[r] = f2bf(t);
-          if (STATS) {
-            const float v = ok ? bf2f(hv[r]) : 0.f;
-            s_sum[j][r] += v;
-            s_sq[j][r] += v * v;
-          }
-        }
-        const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
-        __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
-      }
-    }
+      for (int j = 0; j < TN; ++j) epi_one(k, acc, i, j);
   };
 
 #pragma unroll
@@ -1544,7 +1682,8 @@ static bool halo_geom(int cfg, int H, int W, int C, int R, int S, int stride, in
   h.A_INS = (h.HROWS + rpi - 1) / rpi;
   if (h.A_INS > kHaloAPW * nw) return false;
   const size_t stage = (size_t)h.A_INS * rpi * bk + (size_t)9 * bn * bk;
-  const size_t bytes = (size_t)ns * stage * 2;
+  size_t bytes = (size_t)ns * stage * 2;
+  if (bytes < (size_t)bm * (bn + 8) * 2) bytes = (size_t)bm * (bn + 8) * 2;   // row epilogue tile
   if (bytes > 160 * 1024) return false;
   *g = h;
   *lds = bytes;

@@ -116,10 +116,11 @@ class ShardServer:
         # (peer, direction), so pushes from different ranks land concurrently and
         # only the applies serialise, on self.stream.  The same code path runs on
         # CPU (gloo groups, host waits) -- the multi-process tests exercise it.
+        peers = [r for r in range(world) if r != rank]
         self.rx = PairLinks(self.device, transport or PairGroupTransport(
-            {s: g for (s, _o), g in push_groups.items()}))
+            {s: g for (s, _o), g in push_groups.items()}), peers=peers)
         self.tx = PairLinks(self.device, transport or PairGroupTransport(
-            {d: g for (_o, d), g in reply_groups.items()}))
+            {d: g for (_o, d), g in reply_groups.items()}), peers=peers)
         self.req = req_group
         self.push_g = push_groups
         self.reply_g = reply_groups
@@ -130,6 +131,10 @@ class ShardServer:
         self.staleness: list[int] = []
         self.error: BaseException | None = None
         self.n = self.master.numel()
+        for p in peers:                  # payload rings up front (see PairLinks.reserve)
+            for dt in (torch.float32, torch.bfloat16):
+                self.rx.reserve(p, self.n, dt)
+            self.tx.reserve(p, self.n + 1, torch.float32, send=True)
         self.thread = threading.Thread(target=self._run, daemon=True, name=f"shard-ps-{rank}")
 
     def start(self):

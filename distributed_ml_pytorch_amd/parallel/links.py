@@ -26,7 +26,7 @@ and a send slot is reused only after its previous send's ``Work`` completed.
 The payload transport is pluggable: :class:`PairGroupTransport` is RCCL (one
 2-rank communicator per pair, each with its own RCCL stream) or gloo, and a
 test substitutes a delayed device copy with the same stream semantics
-(``tests/test_train_gpu.py::test_ps_links_overlap_receives``).
+(``tests/test_links_gpu.py::test_ps_links_overlap_receives``).
 """
 from __future__ import annotations
 
@@ -107,7 +107,11 @@ class PairLinks:
     ``trace=True`` (GPU) records timing-event spans ``(kind, peer, start, end)``
     of every transfer in :attr:`spans` (tests, diagnostics)."""
 
-    def __init__(self, device, transport, depth: int = 2, trace: bool = False):
+    def __init__(self, device, transport, depth: int = 2, trace: bool = False, peers=()):
+        """``peers``: create their streams NOW.  A HIP stream created while other
+        streams have work queued serialised that work behind it on MI355X
+        (profiles/links_stream_creation_r4.txt: two peers' transfers ran back to
+        back with lazily created link streams, overlapped with pre-created ones)."""
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.transport = transport
@@ -118,6 +122,8 @@ class PairLinks:
         self._streams: dict[int, torch.cuda.Stream] = {}
         self._rx: dict = {}
         self._tx: dict = {}
+        for p in peers:
+            self.stream(p)
 
     def stream(self, peer: int):
         if not self.cuda:
@@ -130,6 +136,19 @@ class PairLinks:
 
     def _ctx(self, stream):
         return torch.cuda.stream(stream) if self.cuda else contextlib.nullcontext()
+
+    def reserve(self, peer: int, numel: int, dtype, alloc: int | None = None,
+                send: bool = False):
+        """Allocate ``peer``'s ring for payloads of this shape NOW: a first-use
+        allocation in the middle of other peers' transfers can synchronise the
+        device (like a stream creation)."""
+        alloc = numel if alloc is None else alloc
+        rings = self._tx if send else self._rx
+        ring = rings.get((peer, alloc, dtype))
+        if ring is None:
+            ring = rings[(peer, alloc, dtype)] = _Ring()
+        while len(ring.slots) < self.depth:
+            ring.slots.append(_Slot(torch.zeros(alloc, dtype=dtype, device=self.device)))
 
     def _next(self, rings: dict, key, numel: int, dtype) -> _Slot:
         ring = rings.get(key)

@@ -97,7 +97,7 @@ class ParameterServer:
             self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
             # ``transport``: the pair groups (RCCL) unless a test substitutes one
             self.links = PairLinks(self.device, transport or PairGroupTransport(self.pairs),
-                                   trace=trace_links)
+                                   trace=trace_links, peers=self.workers)
         else:
             self.device = torch.device(device or "cpu")
         if model is not None:
@@ -129,6 +129,15 @@ class ParameterServer:
         self._hq = None
         self._recv_bufs = defaultdict(dict)      # gloo payload path
         self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        if self.links is not None:
+            # every worker's payload rings up front (fp32 and bf16 wire), not at
+            # the first transfer while other workers' transfers are in flight
+            padded = self.numel + pad
+            for w in self.workers:
+                for dt in (torch.float32, torch.bfloat16):
+                    self.links.reserve(w, self.numel, dt, alloc=padded)
+                self.links.reserve(w, self.numel + 1, torch.float32, send=True)
+            torch.cuda.synchronize(self.device)
         if self.device.type == "cuda":
             from ..ops._ext import native
 

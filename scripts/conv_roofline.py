@@ -13,6 +13,8 @@ process (cdna_hip_programming.md §5.4 rule 24):
 * ``noepi`` -- DMP_ABLATE=3: everything but the epilogue (halo fwd / dgrad);
 * ``nolds`` -- DMP_ABLATE=4: the fragment reads of the MFMA loop removed
   (halo fwd / dgrad; the wgrad kernels are unchanged in 3 and 4);
+* ``epirow`` -- not an ablation: the row-staged epilogue (DMP_HALO_EPI_LDS=1)
+  on every halo forward too (the extension uses it for the data gradient);
 
 and the fill ceiling of the chip (a DMA-only microkernel streaming 1-KiB
 ``buffer_load ... lds`` pieces per wave from an L2-resident and an HBM-sized
@@ -49,13 +51,15 @@ def build_libs(force=False):
     srcs = [CSRC / "conv.hip", CSRC / "conv_wgrad.hip", CSRC / "ablate" / "ablate_entry.hip"]
     hdrs = list(CSRC.glob("*.h"))
     procs = []
-    for n in (0, 1, 2, 3, 4):
+    for n in (0, 1, 2, 3, 4, 5):
         out = LIBDIR / f"abl{n}.so"
         if not force and out.exists() and all(out.stat().st_mtime > s.stat().st_mtime
                                               for s in srcs + hdrs):
             continue
+        # 5: not an ablation -- the candidate row-staged halo epilogue (DMP_HALO_EPI_LDS)
+        flags = ["-DDMP_ABLATE=0", "-DDMP_HALO_EPI_LDS=1"] if n == 5 else [f"-DDMP_ABLATE={n}"]
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "-std=c++17", "--offload-arch=gfx950",
-               "-shared", f"-DDMP_ABLATE={n}", "-I", str(CSRC), *map(str, srcs),
+               "-shared", *flags, "-I", str(CSRC), *map(str, srcs),
                "-Wl,--no-undefined", "-o", str(out)]
         procs.append(subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
     for p in procs:
@@ -154,7 +158,7 @@ def main():
     from distributed_ml_pytorch_amd.ops._ext import native
 
     nat = native()
-    libs = {n: ctypes.CDLL(str(LIBDIR / f"abl{n}.so")) for n in (0, 1, 2, 3, 4)}
+    libs = {n: ctypes.CDLL(str(LIBDIR / f"abl{n}.so")) for n in (0, 1, 2, 3, 4, 5)}
     for lib in libs.values():
         for fn in ("abl_conv_fwd", "abl_conv_dgrad", "abl_conv_wgrad", "abl_dma_ceiling"):
             getattr(lib, fn).restype = ctypes.c_int
@@ -191,7 +195,7 @@ def main():
     ]
     print("\n== per kernel (us; interleaved rounds, median of 3)", flush=True)
     hdr = (f"{'layer':16s} {'pass':5s} {'cfg':>5s} {'full':>7s} {'abl0':>7s} {'fill':>7s} "
-           f"{'mfma':>7s} {'noepi':>7s} {'nolds':>7s} {'TF/s':>6s} {'%peak':>5s} {'MB stg':>7s} {'GB/s/CU':>7s} "
+           f"{'mfma':>7s} {'noepi':>7s} {'nolds':>7s} {'epirow':>7s} {'TF/s':>6s} {'%peak':>5s} {'MB stg':>7s} {'GB/s/CU':>7s} "
            f"{'B/clk':>5s} {'fill%':>5s} {'mfma%':>5s}")
     print(hdr, flush=True)
     rows = []
@@ -243,12 +247,33 @@ def main():
                                                   else P(0), stream)
 
             arms = {"full": full, "abl0": lib_fn(0), "fill": lib_fn(1), "mfma": lib_fn(2),
-                    "noepi": lib_fn(3), "nolds": lib_fn(4)}
+                    "noepi": lib_fn(3), "nolds": lib_fn(4), "epirow": lib_fn(5)}
             ts = {k: [] for k in arms}
             for _ in range(3):
                 for k, fn in arms.items():
                     ts[k].append(timeit(fn))
             med = {k: sorted(v)[1] for k, v in ts.items()}
+            check = None
+            if op in ("fwd", "dgrad"):
+                # the candidate epilogue must reproduce the extension's output (and
+                # the forward's BN partial sums)
+                check = []
+                for cand in (5,):
+                    if op == "fwd":
+                        ref, rpart, _ = nat.conv_fwd(x, w, 1, 1, True, cfg)
+                        part.zero_()
+                        lib_fn(cand)()
+                        got = y
+                        ps_ref = rpart[:2 * 64 * CO].view(2, 64, CO).sum(1)
+                        ps_got = part[:2 * 64 * CO].view(2, 64, CO).sum(1)
+                        pe = float((ps_ref - ps_got).abs().max() / ps_ref.abs().max())
+                    else:
+                        ref = nat.conv_dgrad(dy, w, H, W, 1, 1, cfg)
+                        lib_fn(cand)()
+                        got = dx
+                        pe = 0.0
+                    torch.cuda.synchronize()
+                    check += [float((ref.float() - got.float()).norm() / ref.float().norm()), pe]
             byts, blocks = staged_bytes(op, cfg, B, CI, H, W, CO)
             tfs = flop / med["full"] / 1e6
             gbcu = (byts / med["full"] / 1e3 / CUS) if byts else float("nan")
@@ -256,13 +281,15 @@ def main():
                      tflops=round(tfs, 1), pct_peak=round(100 * tfs * 1e12 / PEAK, 1),
                      staged_mb=round(byts / 1e6, 1) if byts else None, blocks=blocks,
                      gb_s_cu=round(gbcu, 1), b_clk_cu=round(gbcu * 1e9 / CLK, 1),
+                     epirow_check=check,
                      fill_share=round(100 * med["fill"] / med["full"], 1),
                      mfma_share=round(100 * med["mfma"] / med["full"], 1))
             rows.append(r)
             print(f"{name:16s} {op:5s} {cfg:5d} {med['full']:7.1f} {med['abl0']:7.1f} "
-                  f"{med['fill']:7.1f} {med['mfma']:7.1f} {med['noepi']:7.1f} {med['nolds']:7.1f} {tfs:6.0f} {r['pct_peak']:5.1f} "
+                  f"{med['fill']:7.1f} {med['mfma']:7.1f} {med['noepi']:7.1f} {med['nolds']:7.1f} {med['epirow']:7.1f} {tfs:6.0f} {r['pct_peak']:5.1f} "
                   f"{r['staged_mb'] or 0:7.1f} {gbcu:7.1f} {r['b_clk_cu']:5.1f} "
-                  f"{r['fill_share']:5.1f} {r['mfma_share']:5.1f}", flush=True)
+                  f"{r['fill_share']:5.1f} {r['mfma_share']:5.1f}"
+                  + (f"  err row {check[0]:.1e}/{check[1]:.1e}" if check else ""), flush=True)
     print("\nJSON " + json.dumps({"ceiling_gb_s_cu": {f"{k[0] >> 20}MiB_{k[1]}w_{k[2]}k": round(v, 1)
                                                       for k, v in ceil.items()},
                                   "rows": rows}), flush=True)
