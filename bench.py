@@ -416,6 +416,14 @@ def run(a):
     from distributed_ml_pytorch_amd.runtime.trainer import TrainConfig, Worker
     from distributed_ml_pytorch_amd.utils.data import DeviceBatchPool
 
+    if a.mode == "asgd" and a.ps in ("central", "sharded_async") and \
+            int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # a parameter server keeps one HIP stream per peer (parallel/links.py) plus
+        # RCCL's per-pair streams: at HIP's default 4 hardware queues two peers'
+        # transfers landed on one queue and ran back to back, from 8 queues on they
+        # overlapped (profiles/links_stream_creation_r4.txt).  HIP reads this once,
+        # at initialisation: set before the first torch.cuda call
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     cuda = torch.cuda.is_available()
     info = init_distributed(use_cuda=cuda)
     world = info.world_size

@@ -45,6 +45,11 @@ def launch(script: str, script_args, nproc: int, gpus: bool = False, port: int |
         env.update({"RANK": str(r), "WORLD_SIZE": str(nproc), "LOCAL_RANK": str(r),
                     "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if r == 0 and gpus:
+            # rank 0 is the parameter server of the reference topology: one HIP
+            # stream per worker link needs more than HIP's default 4 hardware
+            # queues to run the links concurrently (parallel/links.py)
+            env.setdefault("GPU_MAX_HW_QUEUES", "16")
         if env_extra:
             env.update(env_extra)
         args = [python, script, *script_args, "--rank", str(r), "--world-size", str(nproc),

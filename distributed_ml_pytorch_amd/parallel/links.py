@@ -108,10 +108,11 @@ class PairLinks:
     of every transfer in :attr:`spans` (tests, diagnostics)."""
 
     def __init__(self, device, transport, depth: int = 2, trace: bool = False, peers=()):
-        """``peers``: create their streams NOW.  A HIP stream created while other
-        streams have work queued serialised that work behind it on MI355X
-        (profiles/links_stream_creation_r4.txt: two peers' transfers ran back to
-        back with lazily created link streams, overlapped with pre-created ones)."""
+        """``peers``: create their streams NOW (no stream creation or first-use
+        allocation in the middle of transfers).  Concurrency across peers also
+        needs enough HIP hardware queues: at HIP's default of 4, two peers' link
+        streams shared a queue and ran back to back; bench.py / launch.py give a
+        PS process 16 (profiles/links_stream_creation_r4.txt)."""
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.transport = transport

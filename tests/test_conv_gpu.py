@@ -142,14 +142,17 @@ def test_halo_conv_configs(B, C, H, W, CO):
         assert _rel(dw, 2 * wr.grad) < 1e-2, cfg
 
 
-@pytest.mark.parametrize("B,H", [(3, 32), (1, 32), (2, 56), (5, 16)])
+@pytest.mark.parametrize("B,H", [(3, 32), (1, 32), (5, 16), (7, 8)])
 @pytest.mark.parametrize("with_add", [False, True])
 def test_halo64p_addend_matrix(B, H, with_add):
     """The persistent 64-channel kernels (ids 115-117) load their residual addend
     with inline-asm loads whose completion the epilogue counts by hand (vmcnt):
-    every config x {no addend, full addend} x {odd batch, B = 1, 56x56, a tile
-    count that does not fill the grid evenly}, forward (+fp32 bias, ReLU: the
-    inference-time BN fold) and data gradient vs fp32."""
+    every config x {no addend, full addend} x {odd batch, B = 1, whole-row and
+    whole-image tiles, tile counts that do not fill the grid evenly}, forward
+    (+fp32 bias, ReLU: the inference-time BN fold) and data gradient vs fp32.
+    (ImageNet 56 x 56 rows are not a divisor of the 256 / 128-pixel tiles: no
+    persistent config is offered there -- checked below -- and those layers run
+    the 224-pixel halo tiles of test_halo_conv_configs.)"""
     from distributed_ml_pytorch_amd.ops._ext import native
 
     nat = native()
@@ -178,6 +181,7 @@ def test_halo64p_addend_matrix(B, H, with_add):
         assert torch.isfinite(dx.float()).all(), cfg
         assert _rel(dx, ref_d) < 1e-2, (cfg, _rel(dx, ref_d))
     assert ran > 0
+    assert not set(nat.conv_halo_configs(56, 56, C, 3, 3, 1, 1)) & {115, 116, 117}
 
 
 @pytest.mark.parametrize("cfg_kind", ["halo", "igemm"])
@@ -228,15 +232,20 @@ def test_eval_bn_fold_matches_unfolded_eval(model, shape):
         loss.backward()
     m.eval()
     with torch.no_grad():
+        ref32 = m(x.float()).float()           # fp32 ATen path, running-stats BN
         eval_fold._FOLD = False
         try:
-            ref = m(x).float()
+            unfolded = m(x).float()
         finally:
             eval_fold._FOLD = True
         with eval_fold.fold_session():
             out = m(x).float()
             out2 = m(x).float()                # cached fold
-    assert _rel(out, ref) < 2e-2, _rel(out, ref)
+    # the folded bf16 forward is as close to fp32 as the unfolded bf16 forward
+    # (the two round at different points: bf16(w * s) vs the bf16 pre-BN output)
+    e_fold, e_unf = _rel(out, ref32), _rel(unfolded, ref32)
+    assert e_fold < 1.5 * e_unf + 5e-3, (e_fold, e_unf)
+    assert _rel(out, unfolded) < 6e-2, _rel(out, unfolded)
     assert torch.equal(out, out2)
     m.train()
 

@@ -500,4 +500,6 @@ def test_relu_mask_hand_off_with_two_consumers():
         lr = (F.max_pool2d(yr, 2) * ga).sum() + (yr * c).sum()
         lr.backward()
         rel = float((conv.weight.grad - wr.grad).norm() / wr.grad.norm())
-        assert rel < 2e-2, (order, rel)
+        # bf16 outputs move a few max-pool argmaxes (near-ties): a few % of noise;
+        # a skipped ReLU mask on the summed gradient is an O(1) error
+        assert rel < 5e-2, (order, rel)
