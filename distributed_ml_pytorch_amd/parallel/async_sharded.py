@@ -51,7 +51,7 @@ import torch.distributed as dist
 
 from . import messaging as M
 from .clients import PSClient, _EventWork, _Pending
-from .links import PairGroupTransport, PairLinks, wait_on
+from .links import PairGroupTransport, PairLinks, wait_on, warm_stream
 
 _LOG = logging.getLogger(__name__)
 
@@ -135,6 +135,16 @@ class ShardServer:
             for dt in (torch.float32, torch.bfloat16):
                 self.rx.reserve(p, self.n, dt)
             self.tx.reserve(p, self.n + 1, torch.float32, send=True)
+        if self.cuda and peers:
+            # load the apply kernels before any transfer: a kernel's first launch
+            # loads its code object, and that waited for the transfers in flight
+            # (ParameterServer._warm_kernels); a zero delta changes nothing
+            with torch.cuda.stream(self.stream):
+                for dt in (torch.float32, torch.bfloat16):
+                    self.nat.ps_apply(self.master, torch.zeros(self.n, dtype=dt,
+                                                               device=self.device),
+                                      None, self.scale)
+            self.stream.synchronize()
         self.thread = threading.Thread(target=self._run, daemon=True, name=f"shard-ps-{rank}")
 
     def start(self):
@@ -312,6 +322,8 @@ class AsyncShardedPSClient(PSClient):
         self._pull_free: deque = deque()      # reusable reply staging sets (+ free event)
         self._push_work: list = [[], []]      # per hand-off slot: payload sends
         self.side = torch.cuda.Stream(self.device) if self.cuda else None
+        if self.side is not None:
+            warm_stream(self.side)     # bind its queue now, not mid-step
 
     def _bounds(self, o: int):
         return o * self.shard_n, (o + 1) * self.shard_n

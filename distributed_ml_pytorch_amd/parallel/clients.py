@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 
 from . import messaging as M
+from .links import warm_stream
 
 _LOG = logging.getLogger(__name__)
 
@@ -248,6 +249,8 @@ class LocalPSClient(PSClient):
         self.master = self.arena.p32.detach().clone()
         self.ps_version = 0
         self.side = torch.cuda.Stream(self.device) if self.cuda else None
+        if self.side is not None:
+            warm_stream(self.side)     # bind its queue now, not mid-step
 
     def push(self, step: int):
         buf = self._handoff()
@@ -535,6 +538,8 @@ class ShardedPSClient(PSClient):
             self.delta_shard = torch.zeros(self.shard_n, dtype=self.wire_dtype,
                                            device=self.device)
         self.side = torch.cuda.Stream(self.device) if self.cuda else None
+        if self.side is not None:
+            warm_stream(self.side)     # bind its queue now, not mid-step
         self._pull_bufs: deque = deque()
         self._push_event = None
 

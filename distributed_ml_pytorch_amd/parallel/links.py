@@ -82,6 +82,13 @@ def wait_on(stream, ev):
         stream.wait_event(ev)
 
 
+def warm_stream(stream):
+    """Submit one tiny kernel to a fresh HIP stream (binds its hardware queue
+    while nothing is in flight; see :class:`PairLinks`)."""
+    with torch.cuda.stream(stream):
+        torch.zeros(1, device=stream.device)
+
+
 class _Slot:
     __slots__ = ("buf", "free", "work")
 
@@ -108,8 +115,10 @@ class PairLinks:
     of every transfer in :attr:`spans` (tests, diagnostics)."""
 
     def __init__(self, device, transport, depth: int = 2, trace: bool = False, peers=()):
-        """``peers``: create their streams NOW (no stream creation or first-use
-        allocation in the middle of transfers).  Concurrency across peers also
+        """``peers``: create AND first-use their streams now.  The first
+        submission to a fresh HIP stream blocked the host ~5 ms (its hardware
+        queue is bound then): two peers' first transfers ran back to back with
+        cold streams, overlapped with warmed ones.  Concurrency across peers also
         needs enough HIP hardware queues: at HIP's default of 4, two peers' link
         streams shared a queue and ran back to back; bench.py / launch.py give a
         PS process 16 (profiles/links_stream_creation_r4.txt)."""
@@ -125,6 +134,8 @@ class PairLinks:
         self._tx: dict = {}
         for p in peers:
             self.stream(p)
+        if self.cuda and self._streams:
+            torch.cuda.synchronize(self.device)
 
     def stream(self, peer: int):
         if not self.cuda:
@@ -133,6 +144,7 @@ class PairLinks:
         if s is None:
             s = torch.cuda.Stream(self.device)
             self._streams[peer] = s
+            warm_stream(s)
         return s
 
     def _ctx(self, stream):

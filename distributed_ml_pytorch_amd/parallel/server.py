@@ -144,6 +144,24 @@ class ParameterServer:
             self._native = native()
         else:
             self._native = None
+        if self.links is not None:
+            self._warm_kernels(padded)
+
+    def _warm_kernels(self, padded: int):
+        """Launch every kernel of the apply / reply path once, before any transfer.
+        HIP loads a kernel's code object at its first launch, and that load waited
+        for the work in flight: the PS's first apply stalled every other link until
+        the first receive had landed (tests/test_links_gpu.py).  A zero delta leaves
+        the shard unchanged."""
+        with torch.cuda.stream(self.stream):
+            for dt in (torch.float32, torch.bfloat16):
+                self._native.ps_apply(self.shard, torch.zeros(padded, dtype=dt,
+                                                              device=self.device),
+                                      None, self.delta_scale)
+            snap = torch.empty(self.numel + 1, dtype=torch.float32, device=self.device)
+            snap[: self.numel].copy_(self.shard[: self.numel])
+            snap[self.numel:].fill_(0.0)
+        torch.cuda.synchronize(self.device)
 
     # -------------------------------------------------------------- payload io
     def _recv_payload(self, sender: int, nelem: int, dtype: torch.dtype):

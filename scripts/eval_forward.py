@@ -17,6 +17,7 @@ os.environ.setdefault("DMP_CONV_TUNE_SEED", os.path.join(
 import torch  # noqa: E402
 
 from distributed_ml_pytorch_amd.models import build_model  # noqa: E402
+from distributed_ml_pytorch_amd.ops.eval_fold import fold_session  # noqa: E402
 from distributed_ml_pytorch_amd.ops.functional import softmax_cross_entropy  # noqa: E402
 from distributed_ml_pytorch_amd.parallel.arena import attach_arena  # noqa: E402
 
@@ -35,7 +36,8 @@ def main():
     if x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, nc, (a.batch,), device="cuda")
-    with torch.no_grad():
+    # one fold per evaluation pass, as Worker.evaluate does
+    with torch.no_grad(), fold_session():
         for _ in range(2):                     # tuning + warm-up
             softmax_cross_entropy(m(x), y)
         torch.cuda.synchronize()

@@ -30,5 +30,29 @@ def main(path):
     print(f"library kernels: {len(lib)}; ATen compute kernels: {len(aten)}")
 
 
+def per_forward(trace, marker="softmax_xent"):
+    """Dispatches of ONE timed forward: between the last two loss-kernel dispatches
+    of a kernel_trace.csv (each forward ends in exactly one)."""
+    rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+    if len(marks) < 2:
+        print(f"per-forward census: only {len(marks)} '{marker}' dispatches")
+        return
+    win = rows[marks[-2] + 1:marks[-1] + 1]
+    cnt, dur = {}, {}
+    for r in win:
+        n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:100]
+        cnt[n] = cnt.get(n, 0) + 1
+        dur[n] = dur.get(n, 0.0) + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    print(f"\nONE forward (last timed): {len(win)} dispatches, busy {sum(dur.values()):.1f} us")
+    for n in sorted(cnt, key=lambda k: -dur[k]):
+        print(f"{dur[n]:9.1f} us {cnt[n]:4d}  {n}")
+    bn = sum(c for n, c in cnt.items() if "bn_" in n)
+    cp = sum(c for n, c in cnt.items() if "copyBuffer" in n or "copy_kernel" in n)
+    print(f"per forward: BatchNorm kernels {bn}, copies {cp}")
+
+
 if __name__ == "__main__":
     main(sys.argv[1])
+    if len(sys.argv) > 2:
+        per_forward(sys.argv[2])

@@ -39,7 +39,12 @@ class DelayedCopyTransport:
         self.inbox = defaultdict(list)      # peer -> tensors we sent to the peer
         # created up front, as RCCL creates a communicator's stream at its first
         # operation (the preflight ping), not in the middle of a transfer
+        # and first used there (PairLinks.warm_stream: a fresh stream's first
+        # submission blocks the host for milliseconds)
         self.comm = {p: torch.cuda.Stream() for p in peers}
+        for cs in self.comm.values():
+            with torch.cuda.stream(cs):
+                torch.cuda._sleep(1000)
         self.spans = []
 
     def _op(self, peer, kind, fn):
@@ -99,11 +104,14 @@ def _scenario():
         GU, PR = M.MessageCode.GradientUpdate, M.MessageCode.ParameterRequest
         f32 = torch.float32
         # two pushes per worker, interleaved as headers would arrive, then a pull
-        ps.handle(GU, 1, 0, 0, n, f32)
-        ps.handle(GU, 2, 0, 0, n, f32)
-        ps.handle(GU, 1, 1, 1, n, f32)
-        ps.handle(GU, 2, 1, 1, n, f32)
-        ps.handle(PR, 1, 2, 0, 0, f32)
+        import time
+
+        host = []
+        for code, w, st, v in ((GU, 1, 0, 0), (GU, 2, 0, 0), (GU, 1, 1, 1), (GU, 2, 1, 1),
+                               (PR, 1, 2, 0)):
+            t = time.perf_counter()
+            ps.handle(code, w, st, v, n if code == GU else 0, f32)
+            host.append(round(1e3 * (time.perf_counter() - t), 3))
         ps.finish()
         torch.cuda.synchronize()
         want = sum(deltas[1]) + sum(deltas[2])
@@ -122,6 +130,7 @@ def _scenario():
             "w1_second_start": a1.elapsed_time(w1[1][0]),
             "w1_first_end": a1.elapsed_time(w1[0][1]),
             "links": dict(ps.links.counts),
+            "host_ms_per_handle": host,
         }
     finally:
         if made:
