@@ -512,8 +512,12 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
 // gradient: the same conv over dY with Wt[ci][r][s][co] and the taps mirrored.
 // NS = 2: two LDS stages (halo + 9 weight tiles each), one barrier per chunk;
 // NS = 1: one stage, more resident blocks per CU.
+// MV: output pixels per tile.  = BM, except for "padded whole-image" tiles
+// (ImageNet ResNet 14x14 / 7x7 maps, where no multiple of 16 is a whole number
+// of images): TB images (MV = TB * H * W < BM) in a BM-row tile whose last
+// BM - MV rows read a valid staged row and are dropped by the epilogue.
 struct HaloGeom {
-  int TH, TB, HROWS, A_INS;
+  int TH, TB, HROWS, A_INS, MV;
 };
 
 constexpr int kHaloAPW = 8;   // max halo DMA instructions per wave per stage
@@ -528,7 +532,7 @@ constexpr int kHaloAPW = 8;   // max halo DMA instructions per wave per stage
 template <int BM, int BN, int WM, int WN, bool FLIP, bool STATS, int TM, int TN, bool S2 = false>
 __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM][TN], long long m0,
                                               int n0, int wm, int wn, int tid, int lane,
-                                              u16* lds_h, int cls = 0) {
+                                              u16* lds_h, int cls = 0, int mv = BM) {
   constexpr int NW = WM * WN;
   typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
   const long long Mtot = (long long)a.B * a.OH * a.OW;
@@ -573,8 +577,9 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const long long m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
-    const bool mok = m < Mrows;
+    const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
+    const long long m = m0 + ml;
+    const bool mok = ml < mv && m < Mrows;
     long long pix = m;
     if constexpr (S2) {
       const int mi = (int)m, gi = a.GH * a.GW;
@@ -694,7 +699,7 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
 template <int BM, int BN, int WM, int WN, bool FLIP, bool STATS, int TM, int TN>
 __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&acc)[TM][TN],
                                                    long long m0, int n0, int wm, int wn, int tid,
-                                                   int lane, u16* lds_h) {
+                                                   int lane, u16* lds_h, int mv = BM) {
   constexpr int NW = WM * WN, PITCH = BN + 8, CPR = BN / 8, RPI = 64 / CPR;
   static_assert(BN % 8 == 0 && 64 % CPR == 0, "row segments of 8 channels");
   typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -740,7 +745,7 @@ __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&ac
   for (int q = 0; q < NR; ++q) {
     const int ml = (q * NW + wid) * RPI + lr;
     const long long m = m0 + ml;
-    off[q] = (ml < BM && m < Mtot && nok) ? 2u * (unsigned)(m * a.CO + n) : kOOB;
+    off[q] = (ml < mv && m < Mtot && nok) ? 2u * (unsigned)(m * a.CO + n) : kOOB;
     if (add_in) xa[q] = __builtin_amdgcn_raw_buffer_load_b128(rsAdd, off[q], 0, 0);
   }
   float s_sum[8], s_sq[8];
@@ -815,7 +820,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const long long m0 = (long long)blockIdx.x * BM;
+  const int MV = hg.MV;
+  const long long m0 = (long long)blockIdx.x * MV;
   const int n0 = blockIdx.y * BN;
   const int H = a.GH, W = a.GW, C = a.CI, TH = hg.TH, HW2 = W + 2;
   const int img = H * W;
@@ -886,7 +892,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   int hrow[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
+    int ml = wm * (BM / WM) + i * 16 + (lane & 15);
+    if (ml >= MV) ml = 0;   // padded tile: a valid staged row, the epilogue drops it
     int tb, r2, th, tw;
     small_divmod(ml, TH * W, rcp_tw, tb, r2);
     small_divmod(r2, W, rcp_w, th, tw);
@@ -980,9 +987,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   // 128 / 256-channel layers, no change on the forward, whose BN sums cost
   // more in the row layout: profiles/conv_roofline_r4.txt)
   if constexpr ((DMP_HALO_EPI_LDS || FLIP) && !(FLIP && STATS))
-    halo_epilogue_rows<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h);
+    halo_epilogue_rows<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h, MV);
   else
-    halo_epilogue<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h);
+    halo_epilogue<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h, 0, MV);
 }
 
 // ------------------------------- 3x3 stride-2 data gradient, halo tiles
@@ -1668,14 +1675,19 @@ static bool halo_geom(int cfg, int H, int W, int C, int R, int S, int stride, in
   if (R != 3 || S != 3 || stride != 1 || pad != 1 || C % bk != 0) return false;
   const int img = H * W;
   HaloGeom h{};
+  h.MV = bm;
   if (bm <= img) {
     if (bm % W != 0 || img % bm != 0) return false;
     h.TH = bm / W;
     h.TB = 1;
   } else {
-    if (bm % img != 0) return false;
     h.TH = H;
     h.TB = bm / img;
+    // padded whole-image tiles: at most 1/8 of the tile's rows idle
+    if (bm % img != 0) {
+      h.MV = h.TB * img;
+      if (8 * (bm - h.MV) > bm) return false;
+    }
   }
   const int rpi = 64 / (bk / 8);
   h.HROWS = h.TB * (h.TH + 2) * (W + 2);
@@ -1753,7 +1765,7 @@ static void launch_halo_t(const ConvArgs& a, const HaloGeom& g, size_t lds, hipS
     attr = true;
   }
   const long long M = (long long)a.B * a.OH * a.OW;
-  const dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((a.CO + BN - 1) / BN));
+  const dim3 grid((unsigned)((M + g.MV - 1) / g.MV), (unsigned)((a.CO + BN - 1) / BN));
   hipLaunchKernelGGL(kern, grid, dim3(64 * WM * WN), lds, s, a, g);
 }
 
@@ -1859,6 +1871,7 @@ static bool s2_geom(int cfg, int H, int W, int OH, int OW, int K, int N, int R, 
   if (K % 32 != 0 || N % bn != 0) return false;
   const int img = OH * OW;
   HaloGeom h{};
+  h.MV = bm;
   if (bm <= img) {
     if (bm % OW != 0 || img % bm != 0) return false;
     h.TH = bm / OW;

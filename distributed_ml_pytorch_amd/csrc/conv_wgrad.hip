@@ -297,8 +297,10 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 // Blocks are mapped XCD-aware: the tiles of one pixel split share an XCD's L2.
 // Partial sums go to dW with fp32 atomics, or plain read-add-write when one
 // block owns the tile (splits == 1).
+// MV: pixels per tile (= BM, or TB * H * W < BM for padded whole-image tiles on
+// 14x14 / 7x7 maps: the dY rows past MV stage zeros, so they add nothing)
 struct WgradHaloGeom {
-  int TH, TB, THX, XROWS, XPW, ntiles, tiles_per_split;
+  int TH, TB, THX, XROWS, XPW, ntiles, tiles_per_split, MV;
 };
 
 constexpr int kWhXPW = 12;   // max X-row DMA instructions per wave per stage
@@ -357,6 +359,7 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
   const int H = a.GH, W = a.GW, C = a.CI, CO = a.CO, TH = hg.TH, THX = hg.THX, W2 = W + 2;
   const int img = H * W;
   const int P = (int)a.P;
+  const int MV = hg.MV;
 
   // DMA slots, fixed per lane: byte offsets RELATIVE to the tile's first pixel.
   // dY: row of the tile + swizzled source column.  X: staged row -> (image in
@@ -375,7 +378,9 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
   for (int j = 0; j < D_PW; ++j) {
     const int row = (wid + j * NW) * 8 + lane / 8, pch = lane % 8;
     d_row[j] = row;
-    d_rel[j] = 2u * (unsigned)(row * CO + co0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8);
+    d_rel[j] = row < MV ? 2u * (unsigned)(row * CO + co0 + (((pch >> 1) ^ wg_f<CW>(row)) * 16) +
+                                          (pch & 1) * 8)
+                        : kOOBw;   // padded tile: zeros
   }
   const bool whole_img = TH == H;   // tiles of whole images: h0 == 0 for every tile
   unsigned x_rel[kWhXPW];
@@ -407,8 +412,8 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
   // tile cursor (image b0, first row h0 of the tile stage() issues next): the
   // stages are issued for consecutive tiles, so it advances by one tile per
   // call instead of dividing per tile
-  int cb0 = (t_begin * BM) / img;
-  int ch0 = (t_begin * BM - cb0 * img) / W;
+  int cb0 = (t_begin * MV) / img;
+  int ch0 = (t_begin * MV - cb0 * img) / W;
   const int lo_dh = r0 - 1, hi_dh = THX - 2 + r0;   // staged rows relative to h0
 
   // issue stage `t` into ring slot `buf`; a tile past the run loads zeros so
@@ -417,7 +422,7 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
     u16* Ds = lds_w + buf * STAGE;
     u16* Xs = Ds + D_EL;
     const bool live = t < t_end;
-    const int m0 = t * BM;
+    const int m0 = t * MV;
     const int b0 = cb0, h0 = ch0;
     if (whole_img) {
       cb0 += hg.TB;
@@ -426,7 +431,7 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
       if (ch0 >= H) { ch0 = 0; cb0 += 1; }
     }
     const unsigned dbase = 2u * (unsigned)(m0 * CO), xbase = 2u * (unsigned)(m0 * C);
-    const bool interior = live && m0 + BM <= P && b0 + hg.TB <= a.B &&
+    const bool interior = live && m0 + MV <= P && b0 + hg.TB <= a.B &&
                           (whole_img || (h0 + lo_dh >= 0 && h0 + hi_dh < H));
     if (interior) {
 #pragma unroll
@@ -458,7 +463,8 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
   for (int pk = 0; pk < BM / 32 / PG; ++pk) {
 #pragma unroll
     for (int hsel = 0; hsel < 2; ++hsel) {
-      const int pl = (grp * (BM / 32 / PG) + pk) * 32 + 8 * g + q + 4 * hsel;
+      int pl = (grp * (BM / 32 / PG) + pk) * 32 + 8 * g + q + 4 * hsel;
+      if (pl >= MV) pl = 0;   // padded tile: its dY row is zero, read any staged X row
       const int tb = pl / (TH * W), r2 = pl - tb * TH * W;
       const int th = r2 / W, tw = r2 - th * W;
       const int xr = (tb * THX + th) * W2 + tw;
@@ -612,14 +618,18 @@ static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R,
   if (tr == 3 && bm > 128) return false;   // 36 accumulator tiles + hoisted addresses spill
   const int img = H * W;
   WgradHaloGeom h{};
+  h.MV = bm;
   if (bm <= img) {
     if (bm % W != 0 || img % bm != 0) return false;
     h.TH = bm / W;
     h.TB = 1;
   } else {
-    if (bm % img != 0) return false;
     h.TH = H;
     h.TB = bm / img;
+    if (bm % img != 0) {   // padded whole-image tiles: at most 1/8 of the rows idle
+      h.MV = h.TB * img;
+      if (8 * (bm - h.MV) > bm) return false;
+    }
   }
   h.THX = h.TH + tr - 1;
   h.XROWS = h.TB * h.THX * (W + 2);
@@ -628,7 +638,7 @@ static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R,
   if ((ns - 2) * (bm / 32 + h.XPW) > 40) return false;
   const long long M = (long long)B * img;
   if (2LL * M * (CO > CI ? CO : CI) >= (1LL << 31)) return false;
-  h.ntiles = (int)((M + bm - 1) / bm);
+  h.ntiles = (int)((M + h.MV - 1) / h.MV);
   const int per = (CI / 64) * (CO / 64) * (3 / tr);
   int sp = target / per;
   if (sp < 1) sp = 1;

@@ -31,12 +31,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--shapes", default="r18", choices=["r18", "r50"],
-                    help="r18: CIFAR ResNet-18 layers; r50: ImageNet ResNet-50 stage 1-2 3x3 convs")
+                    help="r18: CIFAR ResNet-18 layers; r50: ImageNet ResNet-50 3x3 stride-1 convs "
+                         "(14x14 / 7x7: padded whole-image tiles)")
     ap.add_argument("--igemm", type=int, default=0, help="also time the implicit-GEMM tiles")
     a = ap.parse_args()
     nat = native()
     shapes = ((64, 32), (128, 16), (256, 8), (512, 4)) if a.shapes == "r18" else \
-        ((64, 56), (128, 28), (256, 14))
+        ((64, 56), (128, 28), (256, 14), (512, 7))
     for C, HW in shapes:
         B = a.batch
         x = torch.randn(B, C, HW, HW, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
@@ -49,7 +50,16 @@ def main():
             if a.igemm:
                 cands += list(range(nat.conv_num_configs() if hasattr(nat, "conv_num_configs")
                                     else len(nat.conv_configs())))
-            res = {c: t_us(lambda c=c: run(c)) for c in cands}
+            ref = run(-1)[0] if name == "fwd" else run(-1)
+            res = {}
+            for c in cands:
+                out = run(c)
+                out = out[0] if name == "fwd" else out
+                err = float((out.float() - ref.float()).abs().max() / ref.float().abs().max())
+                if not err < 2e-2:
+                    print(f"  cfg {c}: MISMATCH rel err {err:.3e}", flush=True)
+                    continue
+                res[c] = t_us(lambda c=c: run(c))
             best = min(res, key=res.get)
             print(f"C={C:3d} {HW:2d}x{HW:<2d} {name:5s} best {best} {res[best]:6.1f} us "
                   f"{tf / res[best] * 1e6:5.0f} TF/s | " +

@@ -32,7 +32,8 @@ def main():
     nat = native()
     r18 = os.environ.get("SHAPES", "r50") == "r18"
     B = int(os.environ.get("B", "512" if r18 else "128"))
-    shapes = ((64, 32), (128, 16), (256, 8), (512, 4)) if r18 else ((64, 56), (128, 28))
+    shapes = ((64, 32), (128, 16), (256, 8), (512, 4)) if r18 else \
+        ((64, 56), (128, 28), (256, 14), (512, 7))
     for C, HW in shapes:
         x = torch.randn(B, C, HW, HW, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
         dy = torch.randn(B, C, HW, HW, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)

@@ -97,6 +97,8 @@ HALO_SHAPES = [
     (2, 64, 8, 8, 128),
     (2, 64, 56, 56, 64),      # ImageNet ResNet stage 1: 7x16-pixel row tiles (224 / 112 / 448)
     (3, 128, 28, 28, 128),    # stage 2: 4 rows of 28 (no halo wgrad tile fits 28-pixel rows)
+    (3, 256, 14, 14, 256),    # stage 3: padded whole-image tiles (1 image in 224 rows, 2 in 448)
+    (5, 512, 7, 7, 512),      # stage 4: 2 / 4 / 5 / 9 / 10 images in 112 / 224 / 256 / 448 / 512 rows
 ]
 
 
@@ -133,7 +135,7 @@ def test_halo_conv_configs(B, C, H, W, CO):
         dxa = nat.conv_dgrad(dy, w, H, W, 1, 1, cfg, None, add)
         assert _rel(dxa, xr.grad + add.float()) < 1e-2, cfg
     wcfgs = list(nat.conv_wgrad_halo_configs(B, H, W, C, CO, 3, 3, 1, 1))
-    assert wcfgs or W == 28, "no halo wgrad config applies"
+    assert wcfgs or W in (28, 14, 7), "no halo wgrad config applies"
     for cfg in wcfgs:
         dw = torch.zeros(CO, C, 3, 3, device="cuda").contiguous(memory_format=CL)
         nat.conv_wgrad(dy, x, dw, 1, 1, cfg)
