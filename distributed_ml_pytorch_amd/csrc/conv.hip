@@ -1677,9 +1677,16 @@ static bool halo_geom(int cfg, int H, int W, int C, int R, int S, int stride, in
   HaloGeom h{};
   h.MV = bm;
   if (bm <= img) {
-    if (bm % W != 0 || img % bm != 0) return false;
     h.TH = bm / W;
     h.TB = 1;
+    if (bm % W != 0 || img % bm != 0) {
+      // padded row tiles: the most whole rows that tile the image, at most 1/8 idle
+      // (ImageNet 28x28: 7 rows = 196 pixels in 224; 56x56: 4 rows in 256)
+      while (h.TH > 0 && img % (h.TH * W) != 0) --h.TH;
+      if (h.TH == 0) return false;
+      h.MV = h.TH * W;
+      if (8 * (bm - h.MV) > bm) return false;
+    }
   } else {
     h.TH = H;
     h.TB = bm / img;

@@ -3,7 +3,7 @@
 # are new candidates), then A/B the ResNet-50 step: committed cache vs re-tuned cache.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out/r4i && export TMPDIR=/tmp
 cp tuning/mi355x_tune_cache.json gpurun_out/r4i/tc.json
-python3 scripts/retune_drop.py gpurun_out/r4i/tc.json '3, 3, 1, 1]' '14, 14|7, 7' || exit 1
+python3 scripts/retune_drop.py gpurun_out/r4i/tc.json '3, 3, 1, 1]' '28, 28|56, 56' '"fwd", 128|"dgrad", 128|"wgrad", 128' || exit 1
 DMP_CONV_TUNE_SEED=: DMP_CONV_TUNE_CACHE=gpurun_out/r4i/tc.json DMP_CONV_TUNE_ROUNDS=4 DMP_CONV_TUNE_REPS=10 timeout -k 10 400 python bench.py --model resnet50 --batch 128 --steps 5 --warmup 2 --ttl-target 0 --ref-batch 0 > gpurun_out/r4i/tune.log 2>&1 || exit $?
 python3 - <<'PY'
 import json
