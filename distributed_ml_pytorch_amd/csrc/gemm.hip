@@ -193,7 +193,22 @@ __device__ __forceinline__ bf16x8 frag(const u16* img, int r, int ks, int lane) 
 // before the single flush.  One 8-wave block per CU then does the work of two
 // 4-wave blocks with HALF the split-K partials through the fp32 atomics / slab
 // (the ViT weight gradients spend ~25-30 % of their time there).
-template <int BM, int BN, int BK, int WM, int WN, int NS, bool AT, bool BT, int EPI, int KG = 1>
+//
+// PP = true: "ping-pong" k-loop for 8-wave tiles (WM = 2): the two wave rows run
+// one barrier apart, so on every SIMD (waves w and w + 4) one wave issues its
+// fragment reads and LDS DMA while the other runs its MFMA cluster.  Per k-tile
+// (BK = 32, a 4-deep ring) and wave: [ds_read k-tile t | DMA k-tile t+3 | vmcnt:
+// k-tile t+1 landed | lgkmcnt(0)] barrier [setprio 1, MFMAs, setprio 0] barrier.
+// Row 0's read section of k-tile t lies between global barriers 2t-1 and 2t, row
+// 1's between 2t and 2t+1 (it enters the loop one barrier late), so:
+//   * k-tile t+1's DMAs were waited by every wave before barrier 2t+1, and its
+//     first read (row 0) is after it;
+//   * the DMA into ring slot (t+3) % 4 = (t-1) % 4 is issued after barrier 2t-1,
+//     by which row 1's reads of k-tile t-1 completed (lgkmcnt(0) before it);
+//   * past the last k-tile the DMAs read zeros into slots nobody reads again, so
+//     every wave's vmcnt count stays uniform.
+template <int BM, int BN, int BK, int WM, int WN, int NS, bool AT, bool BT, int EPI, int KG = 1,
+          bool PP = false>
 __global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
   constexpr int NWG = WM * WN, NW = NWG * KG;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
@@ -484,6 +499,49 @@ __global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
 
   // bias (fwd) into the accumulators before any DMA is in flight
   tile_init(m0, n0);
+  if constexpr (PP) {
+    static_assert(WM == 2 && KG == 1 && NS == 4 && BK == 32, "ping-pong tiles: 2 wave rows, BK 32, 4 slots");
+    static_assert(SA::INS % NW == 0 && SB::INS % NW == 0, "uniform DMA count per wave");
+    constexpr int PWK = SA::PW_MIN + SB::PW_MIN;   // DMAs per wave per k-tile
+    const bool late = wm == 1;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) stage(s, s);        // k-tiles past KT load zeros
+    gwait_vm<2 * PWK>();                            // k-tile 0 landed (this wave)
+    __builtin_amdgcn_s_barrier();
+    if (late) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    for (int kt = 0; kt < KT; ++kt) {
+      const u16* As = lds + (kt & 3) * STAGE;
+      const u16* Bs = As + SA::EL;
+      bf16x8 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag<BM, AT, BK>(As, ra + i * 16, 0, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = frag<BN, BT, BK>(Bs, rb + j * 16, 0, lane);
+      stage((kt + 3) & 3, kt + 3);
+      gwait_vm<2 * PWK>();                          // k-tile kt+1 landed; fragments read
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = TRANS_OUT ? mfma_bf16(bf[j], af[i], acc[i][j])
+                                : mfma_bf16(af[i], bf[j], acc[i][j]);
+      if (EPI == EPI_ACC32 && do_bias) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) accb[i] = mfma_bf16(af[i], ones, accb[i]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!late) __builtin_amdgcn_s_barrier();
+    gwait_vm<0>();
+  } else {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < KT) stage(s, s);
@@ -496,6 +554,7 @@ __global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
     asm volatile("" ::: "memory");
     if (kt + NS - 1 < KT) stage((kt + NS - 1) % NS, kt + NS - 1);
     compute(kt % NS);
+  }
   }
   if constexpr (KG == 2) {
     // group 1 parks its partial sums in the drained ring, group 0 adds them
@@ -673,7 +732,7 @@ void launch_small(const GemmArgs& g, int splits, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ configs
-struct Cfg { int bm, bn, bk, wm, wn, ns, kg = 1; };
+struct Cfg { int bm, bn, bk, wm, wn, ns, kg = 1, pp = 0; };
 // LDS = ns * (bm + bn) * bk * 2 B.  Tile heights 160 / 192 exist for tile
 // counts: M = 12608 tokens x N = 768 is 150 tiles of 256x256 (59 % of 256 CUs)
 // but 237 of 160x256.  A k-strided (transposed) operand needs a tile side that
@@ -689,6 +748,9 @@ constexpr Cfg kCfgs[] = {
     {128, 128, 32, 2, 2, 4},   // 7:  64 KiB, 4 waves, 2 blocks/CU, 3 k-tiles in flight
     {256, 128, 64, 2, 2, 3},   // 8: 144 KiB, 4 waves of 128x64 (1 wave / SIMD)
     {128, 128, 64, 2, 2, 2, 2},   // 9: wgrad only, 2 k-groups of 4 waves: 128 KiB, 1 block/CU
+    {256, 256, 32, 2, 4, 4, 1, 1},   // 10: ping-pong k-loop (PP), 128 KiB, 8 waves of 128x64
+    {128, 256, 32, 2, 4, 4, 1, 1},   // 11: PP, 96 KiB, 8 waves of 64x64
+    {256, 128, 32, 2, 4, 4, 1, 1},   // 12: PP, 96 KiB, 8 waves of 128x32
 };
 // (4 waves of 128x128 per 256x256 / 192x256 tile, accumulators in AGPRs: 20-40 %
 // slower than the 8-wave tiles on every ViT shape -- profiles/gemm_vs_hipblaslt_r2.txt)
@@ -708,7 +770,8 @@ void launch_cfg(const GemmArgs& a, int splits, hipStream_t s) {
     g.tiles_n = (g.N + c.bn - 1) / c.bn;
     const int tiles = ((g.M + c.bm - 1) / c.bm) * g.tiles_n;
     if constexpr (c.kg == 1 || EPI == EPI_ACC32)
-      hipLaunchKernelGGL((gemm_kernel<c.bm, c.bn, c.bk, c.wm, c.wn, c.ns, AT, BT, EPI, c.kg>),
+      hipLaunchKernelGGL((gemm_kernel<c.bm, c.bn, c.bk, c.wm, c.wn, c.ns, AT, BT, EPI, c.kg,
+                                      c.pp != 0>),
                          dim3((unsigned)tiles, (unsigned)splits), dim3(64 * c.wm * c.wn * c.kg), 0,
                          s, g);
     else
@@ -729,7 +792,10 @@ void launch_mode(int cfg, const GemmArgs& a, int splits, hipStream_t s) {
     case 6: launch_cfg<6, AT, BT, EPI>(a, splits, s); break;
     case 7: launch_cfg<7, AT, BT, EPI>(a, splits, s); break;
     case 8: launch_cfg<8, AT, BT, EPI>(a, splits, s); break;
-    default: launch_cfg<9, AT, BT, EPI>(a, splits, s); break;
+    case 9: launch_cfg<9, AT, BT, EPI>(a, splits, s); break;
+    case 10: launch_cfg<10, AT, BT, EPI>(a, splits, s); break;
+    case 11: launch_cfg<11, AT, BT, EPI>(a, splits, s); break;
+    default: launch_cfg<12, AT, BT, EPI>(a, splits, s); break;
   }
 }
 
