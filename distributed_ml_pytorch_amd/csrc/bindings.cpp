@@ -1552,7 +1552,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("cfg") = -1, py::arg("dbias") = py::none());
   m.def("conv_configs", &conv_configs, "[(id, BM, BN, BK, threads)] of the compiled conv tiles");
   m.def("conv_wgrad_halo_configs", &conv_wgrad_halo_configs,
-        "3x3/stride-1 halo wgrad cfg ids applicable to (B, H, W, CI, CO, R, S, stride, pad)");
+        "3x3 stride-1 / stride-2 halo wgrad cfg ids applicable to (B, H, W, CI, CO, R, S, stride, pad)");
   m.def("conv_dgrad_s2_configs", &conv_dgrad_s2_configs,
         "3x3/stride-2 halo data-gradient cfg ids for (H, W, OH, OW, CO, CI, R, S, stride, pad)");
   m.def("conv_halo_configs", &conv_halo_configs,

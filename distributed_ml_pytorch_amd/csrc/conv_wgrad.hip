@@ -330,9 +330,17 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
 // One such block per CU replaces two 4-wave blocks: the same two waves per
 // SIMD, half the fp32 partials through the memory-side atomic units (~1.3
 // TB/s chip-wide, ~25 % of the 4-wave kernel's time: profiles/conv_kernels_r2.txt).
-template <int BM, int NS, int TR, int PG = 1>
+//
+// S2: the 3x3 / stride-2 / pad-1 weight gradient (TR = 1).  Tiles are dY pixels
+// (OH x OW); for tap row r0 the block stages, per output row th of the tile, the
+// ONE input row 2 (h0 + th) - 1 + r0 (W + 2 columns), and output pixel (th, tw)
+// reads tap s at staged column 2 tw + s: the same DMA slots and transposing
+// reads as stride 1, with the pixel -> staged-row map doubled along w (the
+// implicit-GEMM gather ran these at 345-420 TF/s, profiles/resnet18_steady_state_r4.txt).
+template <int BM, int NS, int TR, int PG = 1, bool S2 = false>
 __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, WgradHaloGeom hg,
                                                                    int atomic) {
+  static_assert(!S2 || TR == 1, "stride-2 halo wgrad: one tap row per block");
   constexpr int NW = 4 * PG, CW = 64;             // 64-channel rows (128 B)
   constexpr int D_PW = BM / 8 / NW;               // dY DMA instructions per wave per tile
   constexpr int NT = 3 * TR;                      // taps per block
@@ -357,7 +365,8 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
   const int t_end = min(hg.ntiles, t_begin + hg.tiles_per_split);
   if (t_begin >= t_end) return;
   const int H = a.GH, W = a.GW, C = a.CI, CO = a.CO, TH = hg.TH, THX = hg.THX, W2 = W + 2;
-  const int img = H * W;
+  const int img = H * W;                           // input (X) image
+  const int OHd = S2 ? a.OH : H, OWd = S2 ? a.OW : W, imgd = OHd * OWd;   // dY image
   const int P = (int)a.P;
   const int MV = hg.MV;
 
@@ -382,7 +391,7 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
                                           (pch & 1) * 8)
                         : kOOBw;   // padded tile: zeros
   }
-  const bool whole_img = TH == H;   // tiles of whole images: h0 == 0 for every tile
+  const bool whole_img = TH == OHd;   // tiles of whole images: h0 == 0 for every tile
   unsigned x_rel[kWhXPW];
   int x_dh[kWhXPW], x_tb[kWhXPW];
 #pragma unroll
@@ -394,7 +403,7 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
       const int row = (wid + j * NW) * 8 + lane / 8, pch = lane % 8;
       const int tb = row / (THX * W2), rem = row - tb * THX * W2;
       const int th = rem / W2, w = rem - th * W2 - 1;
-      const int dh = th - 1 + r0;
+      const int dh = (S2 ? 2 * th : th) - 1 + r0;   // relative to the tile's first X row
       const bool ok = row < hg.XROWS && tb < hg.TB && (unsigned)w < (unsigned)W &&
                       (!whole_img || (unsigned)dh < (unsigned)H);
       if (ok)
@@ -412,9 +421,10 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
   // tile cursor (image b0, first row h0 of the tile stage() issues next): the
   // stages are issued for consecutive tiles, so it advances by one tile per
   // call instead of dividing per tile
-  int cb0 = (t_begin * MV) / img;
-  int ch0 = (t_begin * MV - cb0 * img) / W;
-  const int lo_dh = r0 - 1, hi_dh = THX - 2 + r0;   // staged rows relative to h0
+  int cb0 = (t_begin * MV) / imgd;
+  int ch0 = (t_begin * MV - cb0 * imgd) / OWd;
+  // staged X rows relative to the tile's first X row (h0, or 2 h0 for S2)
+  const int lo_dh = r0 - 1, hi_dh = S2 ? 2 * (TH - 1) - 1 + r0 : THX - 2 + r0;
 
   // issue stage `t` into ring slot `buf`; a tile past the run loads zeros so
   // every wave's DMA count per stage stays D_PW + XPW
@@ -428,11 +438,13 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
       cb0 += hg.TB;
     } else {
       ch0 += TH;
-      if (ch0 >= H) { ch0 = 0; cb0 += 1; }
+      if (ch0 >= OHd) { ch0 = 0; cb0 += 1; }
     }
-    const unsigned dbase = 2u * (unsigned)(m0 * CO), xbase = 2u * (unsigned)(m0 * C);
+    const int hx0 = S2 ? 2 * h0 : h0;   // the tile's first X row
+    const unsigned dbase = 2u * (unsigned)(m0 * CO);
+    const unsigned xbase = S2 ? 2u * (unsigned)((b0 * img + hx0 * W) * C) : 2u * (unsigned)(m0 * C);
     const bool interior = live && m0 + MV <= P && b0 + hg.TB <= a.B &&
-                          (whole_img || (h0 + lo_dh >= 0 && h0 + hi_dh < H));
+                          (whole_img || (hx0 + lo_dh >= 0 && hx0 + hi_dh < H));
     if (interior) {
 #pragma unroll
       for (int j = 0; j < D_PW; ++j) bdma16w(rsD, d_rel[j] + dbase, Ds + (wid + j * NW) * 512);
@@ -449,7 +461,7 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
       for (int j = 0; j < kWhXPW; ++j) {
         if (j < XPW) {
           const bool ok = live && x_rel[j] != kOOBw && b0 + x_tb[j] < a.B &&
-                          (whole_img || (unsigned)(h0 + x_dh[j]) < (unsigned)H);
+                          (whole_img || (unsigned)(hx0 + x_dh[j]) < (unsigned)H);
           bdma16w(rsX, ok ? x_rel[j] + xbase : kOOBw, Xs + (wid + j * NW) * 512);
         }
       }
@@ -465,9 +477,9 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
     for (int hsel = 0; hsel < 2; ++hsel) {
       int pl = (grp * (BM / 32 / PG) + pk) * 32 + 8 * g + q + 4 * hsel;
       if (pl >= MV) pl = 0;   // padded tile: its dY row is zero, read any staged X row
-      const int tb = pl / (TH * W), r2 = pl - tb * TH * W;
-      const int th = r2 / W, tw = r2 - th * W;
-      const int xr = (tb * THX + th) * W2 + tw;
+      const int tb = pl / (TH * OWd), r2 = pl - tb * TH * OWd;
+      const int th = r2 / OWd, tw = r2 - th * OWd;
+      const int xr = (tb * THX + th) * W2 + (S2 ? 2 * tw : tw);
       if (hsel) xr_hi[pk] = xr; else xr_lo[pk] = xr;
     }
   }
@@ -614,8 +626,13 @@ static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R,
   const int bm = kWhBM[var] != 0 ? kWhBM[var] : 64 << (rest / 4), target = 128 << (rest % 4);
   const int ns = kWhNS[var], tr = kWhTR[var], pg = kWhPG[var];
   if (pg == 2 && bm < 128) return false;
-  if (R != 3 || S != 3 || stride != 1 || pad != 1 || CI % 64 || CO % 64) return false;
+  if (R != 3 || S != 3 || pad != 1 || CI % 64 || CO % 64) return false;
+  const bool s2 = stride == 2;
+  if (stride != 1 && !(s2 && tr == 1 && H % 2 == 0 && W % 2 == 0 && ns <= 3 && kWhBM[var] == 0))
+    return false;
   if (tr == 3 && bm > 128) return false;   // 36 accumulator tiles + hoisted addresses spill
+  const int XW = W;                        // staged X row width - 2 (input columns)
+  if (s2) { H /= 2; W /= 2; }              // tiles run over the dY (output) geometry
   const int img = H * W;
   WgradHaloGeom h{};
   h.MV = bm;
@@ -639,12 +656,12 @@ static bool wgrad_halo_geom(int cfg, int B, int H, int W, int CI, int CO, int R,
     }
   }
   h.THX = h.TH + tr - 1;
-  h.XROWS = h.TB * h.THX * (W + 2);
+  h.XROWS = h.TB * h.THX * (XW + 2);
   h.XPW = ((h.XROWS + 7) / 8 + 4 * pg - 1) / (4 * pg);
   if (h.XPW > kWhXPW || h.THX + 1 > 127 || h.TB > 0x7fff) return false;
   if ((ns - 2) * (bm / 32 + h.XPW) > 40) return false;
   const long long M = (long long)B * img;
-  if (2LL * M * (CO > CI ? CO : CI) >= (1LL << 31)) return false;
+  if (2LL * M * (CO > CI ? CO : CI) * (s2 ? 4 : 1) >= (1LL << 31)) return false;
   h.ntiles = (int)((M + h.MV - 1) / h.MV);
   const int per = (CI / 64) * (CO / 64) * (3 / tr);
   int sp = target / per;
@@ -721,13 +738,13 @@ __global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const float* __r
   }
 }
 
-template <int BM, int NS, int TR, int PG = 1>
+template <int BM, int NS, int TR, int PG = 1, bool S2 = false>
 static void launch_wgrad_halo_t(const WgradArgs& a, const WgradHaloGeom& g, size_t lds, int splits,
                                 hipStream_t s) {
   static bool attr = false;
   static int diag = -1;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<BM, NS, TR, PG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<BM, NS, TR, PG, S2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
@@ -737,8 +754,8 @@ static void launch_wgrad_halo_t(const WgradArgs& a, const WgradHaloGeom& g, size
   }
   const dim3 grid((unsigned)(a.CI / 64), (unsigned)(a.CO / 64 * (3 / TR)), (unsigned)splits);
   const int mode = diag ? 2 : (splits > 1 ? (a.slab != nullptr ? 3 : 1) : 0);
-  hipLaunchKernelGGL((conv_wgrad_halo_kernel<BM, NS, TR, PG>), grid, dim3(256 * PG), lds, s, a, g,
-                     mode);
+  hipLaunchKernelGGL((conv_wgrad_halo_kernel<BM, NS, TR, PG, S2>), grid, dim3(256 * PG), lds, s, a,
+                     g, mode);
   if (mode == 3) {
     const long long n4 = (long long)a.CO * 9 * a.CI / 4;
     hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0,
@@ -789,6 +806,21 @@ void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int
     size_t lds;
     if (wgrad_halo_geom(cfg, B, H, W, CI, CO, R, S, stride, pad, &g, &bm, &ns, &tr, &pg, &lds,
                         &sp)) {
+      if (stride == 2) {   // (geometry: TR 1, NS 2-3, BM 64 / 128 / 256)
+        if (pg == 2) {
+          if (bm == 128) launch_wgrad_halo_t<128, 2, 1, 2, true>(a, g, lds, sp, s);
+          else launch_wgrad_halo_t<256, 2, 1, 2, true>(a, g, lds, sp, s);
+        } else if (ns == 2) {
+          if (bm == 64) launch_wgrad_halo_t<64, 2, 1, 1, true>(a, g, lds, sp, s);
+          else if (bm == 128) launch_wgrad_halo_t<128, 2, 1, 1, true>(a, g, lds, sp, s);
+          else launch_wgrad_halo_t<256, 2, 1, 1, true>(a, g, lds, sp, s);
+        } else {
+          if (bm == 64) launch_wgrad_halo_t<64, 3, 1, 1, true>(a, g, lds, sp, s);
+          else if (bm == 128) launch_wgrad_halo_t<128, 3, 1, 1, true>(a, g, lds, sp, s);
+          else launch_wgrad_halo_t<256, 3, 1, 1, true>(a, g, lds, sp, s);
+        }
+        return;
+      }
       if (pg == 2) {
         if (bm == 128) launch_wgrad_halo_t<128, 2, 1, 2>(a, g, lds, sp, s);
         else launch_wgrad_halo_t<256, 2, 1, 2>(a, g, lds, sp, s);

@@ -30,32 +30,38 @@ def t_us(fn, it=10, rounds=3):
 
 def main():
     nat = native()
-    r18 = os.environ.get("SHAPES", "r50") == "r18"
+    which = os.environ.get("SHAPES", "r50")
+    r18 = which.startswith("r18")
+    st = int(os.environ.get("STRIDE", "1"))
     B = int(os.environ.get("B", "512" if r18 else "128"))
-    shapes = ((64, 32), (128, 16), (256, 8), (512, 4)) if r18 else \
-        ((64, 56), (128, 28), (256, 14), (512, 7))
-    for C, HW in shapes:
+    # (C in, H in, C out); stride 2: the ResNet stride-2 3x3 convs (H in -> H / 2)
+    shapes = {"r18": ((64, 32, 64), (128, 16, 128), (256, 8, 256), (512, 4, 512)),
+              "r50": ((64, 56, 64), (128, 28, 128), (256, 14, 256), (512, 7, 512)),
+              "r18s2": ((64, 32, 128), (128, 16, 256), (256, 8, 512)),
+              "r50s2": ((128, 56, 128),)}[which]
+    for C, HW, CO in shapes:
         x = torch.randn(B, C, HW, HW, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
-        dy = torch.randn(B, C, HW, HW, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
-        dw = torch.zeros(C, C, 3, 3, device="cuda").contiguous(memory_format=CL)
+        OH = HW // st
+        dy = torch.randn(B, CO, OH, OH, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+        dw = torch.zeros(CO, C, 3, 3, device="cuda").contiguous(memory_format=CL)
         # numerics: every candidate against fp32 autograd of the same conv
         xr = x.float().requires_grad_(False)
-        wr = torch.zeros(C, C, 3, 3, device="cuda", requires_grad=True)
-        y = torch.nn.functional.conv2d(xr, wr, None, 1, 1)
+        wr = torch.zeros(CO, C, 3, 3, device="cuda", requires_grad=True)
+        y = torch.nn.functional.conv2d(xr, wr, None, st, 1)
         y.backward(dy.float())
         ref = wr.grad
-        cands = list(nat.conv_wgrad_halo_configs(B, HW, HW, C, C, 3, 3, 1, 1)) + \
-            _wgrad_candidates(9 * C, C)
+        cands = list(nat.conv_wgrad_halo_configs(B, HW, HW, C, CO, 3, 3, st, 1)) + \
+            _wgrad_candidates(9 * C, CO)
         res = {}
         for c in cands:
             dw.zero_()
-            nat.conv_wgrad(dy, x, dw, 1, 1, c)
+            nat.conv_wgrad(dy, x, dw, st, 1, c)
             err = float((dw - ref).norm() / ref.norm())
-            res[c] = (t_us(lambda c=c: nat.conv_wgrad(dy, x, dw, 1, 1, c)), err)
+            res[c] = (t_us(lambda c=c: nat.conv_wgrad(dy, x, dw, st, 1, c)), err)
         best = min(res, key=lambda c: res[c][0])
         atom = [c for c in res if c < 3000]
         best_atomic = min(atom, key=lambda c: res[c][0])
-        tf = 2.0 * B * HW * HW * C * C * 9 / 1e12
+        tf = 2.0 * B * OH * OH * C * CO * 9 / 1e12
         print(f"C={C} {HW}x{HW} B={B} wgrad best {best} {res[best][0]:.1f} us "
               f"{tf / res[best][0] * 1e6:.0f} TF/s (best without slab: {best_atomic} "
               f"{res[best_atomic][0]:.1f} us) | " +

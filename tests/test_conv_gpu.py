@@ -144,6 +144,33 @@ def test_halo_conv_configs(B, C, H, W, CO):
         assert _rel(dw, 2 * wr.grad) < 1e-2, cfg
 
 
+@pytest.mark.parametrize("B,C,H,CO", [
+    (3, 64, 32, 128), (5, 128, 16, 256), (9, 256, 8, 512),      # ResNet-18 stride-2 3x3 convs
+    (2, 128, 56, 128),                                          # ResNet-50 (v1.5) stage-2 stride-2 3x3
+])
+def test_halo_wgrad_stride2(B, C, H, CO):
+    """3x3 / stride-2 halo weight gradient (conv_wgrad_halo_kernel<S2>), every
+    applicable config (atomic and slab split-K) vs fp32 autograd, accumulating."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    torch.manual_seed(0)
+    x = torch.randn(B, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    xr = x.float()
+    wr = torch.zeros(CO, C, 3, 3, device="cuda", requires_grad=True)
+    yr = F.conv2d(xr, wr, None, 2, 1)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr.backward(dy.float())
+    cfgs = list(nat.conv_wgrad_halo_configs(B, H, H, C, CO, 3, 3, 2, 1))
+    assert cfgs, "no stride-2 halo wgrad config applies"
+    for cfg in cfgs:
+        dw = torch.zeros(CO, C, 3, 3, device="cuda").contiguous(memory_format=CL)
+        nat.conv_wgrad(dy, x, dw, 2, 1, cfg)
+        assert _rel(dw, wr.grad) < 1e-2, cfg
+        nat.conv_wgrad(dy, x, dw, 2, 1, cfg)
+        assert _rel(dw, 2 * wr.grad) < 1e-2, cfg
+
+
 @pytest.mark.parametrize("B,H", [(3, 32), (1, 32), (5, 16), (7, 8)])
 @pytest.mark.parametrize("with_add", [False, True])
 def test_halo64p_addend_matrix(B, H, with_add):
