@@ -304,6 +304,64 @@ Tensor bn_bwd_from_partials(Tensor x, Tensor dz, optional<Tensor> gamma, Tensor 
 }
 
 // ------------------------------------------------------------------ pooling
+// fused GAP + Linear head: [y [B, N] bf16, f [B, C] bf16 (pooled features, kept
+// for the weight gradient)]
+std::vector<Tensor> gap_linear_fwd(Tensor x, Tensor w, optional<Tensor> bias) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4, "gap_linear expects NCHW (channels_last) input");
+  const int B = (int)x.size(0), C = (int)x.size(1), HW = (int)(x.size(2) * x.size(3));
+  check_gpu(w, "w");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.size(1) == C &&
+                  w.is_contiguous(), "gap_linear: w must be contiguous bf16 [N, C]");
+  const int N = (int)w.size(0);
+  TORCH_CHECK(dmp::gap_linear_supported(C, N), "gap_linear: unsupported C / N");
+  if (bias) {
+    check_gpu(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->numel() == N && bias->is_contiguous(),
+                "gap_linear: bias must be contiguous bf16 [N]");
+  }
+  auto y = at::empty({B, N}, x.options().memory_format(at::MemoryFormat::Contiguous));
+  auto f = at::empty({B, C}, x.options().memory_format(at::MemoryFormat::Contiguous));
+  dmp::launch_gap_linear_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                             reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                             bias ? reinterpret_cast<const uint16_t*>(bias->data_ptr()) : nullptr,
+                             reinterpret_cast<uint16_t*>(y.data_ptr()),
+                             reinterpret_cast<uint16_t*>(f.data_ptr()), B, HW, C, N, cur_stream());
+  return {y, f};
+}
+
+// dx [B, C, H, W] channels-last; gw [N, C] fp32 (+=), gb [N] fp32 (+=)
+Tensor gap_linear_bwd(Tensor dy, Tensor f, Tensor w, Tensor gw, optional<Tensor> gb, int64_t H,
+                      int64_t W) {
+  dy = dy.contiguous();
+  check_gpu(dy, "dy");
+  check_gpu(f, "f");
+  check_gpu(w, "w");
+  check_gpu(gw, "gw");
+  const int B = (int)f.size(0), C = (int)f.size(1), N = (int)w.size(0);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 2 && dy.size(0) == B &&
+                  dy.size(1) == N, "gap_linear_bwd: dy must be bf16 [B, N]");
+  TORCH_CHECK(f.scalar_type() == at::kBFloat16 && f.is_contiguous(), "gap_linear_bwd: f bf16 [B, C]");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.size(1) == C,
+              "gap_linear_bwd: w bf16 [N, C]");
+  TORCH_CHECK(gw.scalar_type() == at::kFloat && gw.is_contiguous() && gw.numel() == (int64_t)N * C,
+              "gap_linear_bwd: gw fp32 [N, C]");
+  TORCH_CHECK(dmp::gap_linear_supported(C, N), "gap_linear: unsupported C / N");
+  if (gb) {
+    check_gpu(*gb, "gb");
+    TORCH_CHECK(gb->scalar_type() == at::kFloat && gb->numel() == N && gb->is_contiguous(),
+                "gap_linear_bwd: gb fp32 [N]");
+  }
+  auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dmp::launch_gap_linear_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                             reinterpret_cast<const uint16_t*>(f.data_ptr()),
+                             reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                             reinterpret_cast<uint16_t*>(dx.data_ptr()), gw.data_ptr<float>(),
+                             gb ? gb->data_ptr<float>() : nullptr, B, (int)(H * W), C, N,
+                             cur_stream());
+  return dx;
+}
+
 Tensor gap_fwd(Tensor x) {
   check_nhwc_bf16(x, "x");
   TORCH_CHECK(x.dim() == 4, "gap expects NCHW (channels_last) input");
@@ -1635,6 +1693,14 @@ PYBIND11_MODULE(_native, m) {
   m.def("dropout_fwd", &dropout_fwd, "Philox dropout forward -> (y, keep mask)");
   m.def("dropout_bwd", &dropout_bwd, "dropout backward from the saved keep mask");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pool forward");
+  m.def("gap_linear_fwd", &gap_linear_fwd, "fused NHWC global average pool + Linear forward",
+        py::arg("x"), py::arg("w"), py::arg("bias") = py::none());
+  m.def("gap_linear_bwd", &gap_linear_bwd, "fused GAP + Linear backward (dx, dW +=, db +=)",
+        py::arg("dy"), py::arg("f"), py::arg("w"), py::arg("gw"), py::arg("gb") = py::none(),
+        py::arg("H"), py::arg("W"));
+  m.def("gap_linear_supported",
+        [](int64_t C, int64_t N) { return dmp::gap_linear_supported((int)C, (int)N); },
+        "fused GAP + Linear head applies to C channels / N classes");
   m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC KxK / stride S / pad P max pool forward",
         py::arg("x"), py::arg("K"), py::arg("S") = -1, py::arg("P") = 0,

@@ -67,6 +67,12 @@ void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y, con
 // pool.hip
 void launch_gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s);
 void launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s);
+// fused global-average-pool + Linear head (csrc/head.hip)
+bool gap_linear_supported(int C, int N);
+void launch_gap_linear_fwd(const uint16_t* x, const uint16_t* w, const uint16_t* bias, uint16_t* y,
+                           uint16_t* f, int B, int HW, int C, int N, hipStream_t s);
+void launch_gap_linear_bwd(const uint16_t* dy, const uint16_t* f, const uint16_t* w, uint16_t* dx,
+                           float* gw, float* gb, int B, int HW, int C, int N, hipStream_t s);
 int maxpool_out(int H, int K, int S, int P);
 void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C,
                         int K, int S, int P, hipStream_t s, bool nchw_out = false,

@@ -23,6 +23,7 @@ import torch.nn as nn
 
 from ..ops import layers as L
 from ..ops.eval_fold import conv_bn, fold_enabled
+from ..ops.linear import gap_linear, gap_linear_ok
 
 
 # 1x1 / stride-2 shortcuts on conv1's subsampled alias (DMP_SC_SUB=0: full-res
@@ -173,6 +174,8 @@ class ResNet(nn.Module):
         if self.pool is not None:
             h = self.pool(h)
         h = self.layer4(self.layer3(self.layer2(self.layer1(h))))
+        if gap_linear_ok(h, self.linear):
+            return gap_linear(h, self.linear)     # pool + classifier: one launch each way
         return self.linear(self.avgpool(h))
 
 

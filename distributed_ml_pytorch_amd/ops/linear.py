@@ -312,6 +312,75 @@ class _ArenaLinear(Function):
         return dx, None, None, gw, gb, None
 
 
+# ------------------------------------------------ fused GAP + Linear head
+_FUSED_HEAD = os.environ.get("DMP_FUSED_HEAD", "1") != "0"
+
+
+class _GapLinear(Function):
+    """``linear(global_avg_pool(x))`` in one native launch per direction
+    (csrc/head.hip): pooled features are kept (bf16) for the weight gradient;
+    dW / db accumulate into the fp32 arena like :class:`_ArenaLinear`."""
+
+    @staticmethod
+    def forward(ctx, x, w16, b16, w, b):
+        y, f = native().gap_linear_fwd(x, w16, b16)
+        ctx.save_for_backward(f, w16)
+        ctx.params = (w, b)
+        ctx.hw = (x.shape[2], x.shape[3])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        f, w16 = ctx.saved_tensors
+        w, b = ctx.params
+        N, C = w16.shape
+        gw = _arena_grad(w) if w.requires_grad else None
+        gb = _arena_grad(b) if b is not None and b.requires_grad else None
+        tmp_w = gw is None
+        tmp_b = gb is None and b is not None and b.requires_grad
+        if tmp_w:
+            gw = torch.zeros(N, C, dtype=torch.float32, device=dy.device)
+        if tmp_b:
+            gb = torch.zeros(N, dtype=torch.float32, device=dy.device)
+        dx = native().gap_linear_bwd(dy, f, w16, gw, gb, ctx.hw[0], ctx.hw[1])
+        gw_out = gb_out = None
+        if w.requires_grad:
+            if tmp_w:
+                gw_out = gw.to(w.dtype)
+            else:
+                _notify(w)
+        if b is not None and b.requires_grad:
+            if tmp_b:
+                gb_out = gb.to(b.dtype)
+            else:
+                _notify(b)
+        return dx, None, None, gw_out, gb_out
+
+
+def gap_linear_ok(x, linear) -> bool:
+    """The fused head applies: bf16 channels-last activations, arena-backed
+    weights with a bf16 shadow, C % 8 == 0, at most 16 classes."""
+    if not (_FUSED_HEAD and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        return False
+    w, b = linear.weight, linear.bias
+    w16 = getattr(w, "_dmp_w16", None)
+    if w16 is None or w16.dtype != x.dtype or not w16.is_contiguous():
+        return False
+    if b is not None and getattr(b, "_dmp_w16", None) is None:
+        return False
+    return bool(native().gap_linear_supported(x.shape[1], w.shape[0]))
+
+
+def gap_linear(x, linear):
+    w, b = linear.weight, linear.bias
+    b16 = b._dmp_w16 if b is not None else None
+    if not _needs_graph(x, w, b):
+        return native().gap_linear_fwd(x, w._dmp_w16, b16)[0]
+    return _GapLinear.apply(x, w._dmp_w16, b16, w, b)
+
+
 def arena_linear_ok(x, w, b) -> bool:
     """The weight (and bias) live in an arena with a bf16 shadow matching ``x``
     (training or inference: under ``torch.no_grad()`` the forward runs the same

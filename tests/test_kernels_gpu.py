@@ -503,3 +503,33 @@ def test_relu_mask_hand_off_with_two_consumers():
         # bf16 outputs move a few max-pool argmaxes (near-ties): a few % of noise;
         # a skipped ReLU mask on the summed gradient is an O(1) error
         assert rel < 5e-2, (order, rel)
+
+
+@pytest.mark.parametrize("B,C,H,N", [(512, 512, 4, 10), (37, 2048, 7, 16), (5, 64, 8, 3), (9, 1000, 2, 7)])
+def test_gap_linear_head_fused(B, C, H, N):
+    """Fused global-average-pool + Linear head (csrc/head.hip): logits, dx, dW (+=)
+    and db (+=) against fp32 autograd of mean-pool + linear."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    if not nat.gap_linear_supported(C, N):
+        pytest.skip("geometry outside the fused head")
+    torch.manual_seed(0)
+    x = torch.randn(B, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(N, C, device="cuda") / C ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda").to(torch.bfloat16)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    br = b.float().requires_grad_(True)
+    yr = torch.nn.functional.linear(xr.mean(dim=(2, 3)), wr, br)
+    dy = torch.randn(B, N, device="cuda").to(torch.bfloat16)
+    yr.backward(dy.float())
+    y, f = nat.gap_linear_fwd(x, w, b)
+    assert float((y.float() - yr).norm() / yr.norm()) < 1e-2
+    gw = torch.full((N, C), 0.5, device="cuda")
+    gb = torch.full((N,), 0.25, device="cuda")
+    dx = nat.gap_linear_bwd(dy, f, w, gw, gb, H, H)
+    assert dx.is_contiguous(memory_format=torch.channels_last) and dx.shape == x.shape
+    assert float((dx.float() - xr.grad).norm() / xr.grad.norm()) < 1e-2
+    assert float((gw - 0.5 - wr.grad).norm() / wr.grad.norm()) < 1e-2
+    assert float((gb - 0.25 - br.grad).norm() / br.grad.norm()) < 1e-2
