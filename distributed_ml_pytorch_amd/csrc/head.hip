@@ -15,15 +15,16 @@
 // One wave per sample: lane l owns channels 8l + 512k (16-B vectors), so the
 // pooling reads and the dx writes are whole 1-KiB rows per wave instruction.
 // The N <= kHeadN class dot products are lane partials reduced by shuffles.
-// The backward block (4 waves x SPW samples) sums its samples' dW / db
-// contributions in registers, then through LDS across its waves, and adds them
-// to the fp32 gradient with one atomic per (n, c) per block.
+// The backward grid has a dx role (one wave per sample) and a weight-gradient
+// role (one block per 64-channel slice, all samples, owned outputs).
 #include "common.h"
 
 namespace dmp {
 
 constexpr int kHeadN = 16;      // classes per launch (more: the unfused path)
 constexpr int kHeadCV = 4;      // 16-B channel vectors per lane: C <= 64 * 8 * 4 = 2048
+constexpr int kHeadKS = 4;      // sample chunks of the weight-gradient role
+constexpr int kHeadU = 4;       // samples per thread with their loads in flight together
 
 __global__ void __launch_bounds__(256) gap_linear_fwd_kernel(
     const u16* __restrict__ x, const u16* __restrict__ w, const u16* __restrict__ bias,
@@ -84,98 +85,121 @@ __global__ void __launch_bounds__(256) gap_linear_fwd_kernel(
   }
 }
 
-// SPW samples per wave, 4 waves per block
-template <int SPW>
+// Two block roles in one grid.  Blocks [0, nbx): dx, one wave per sample (4 per
+// block).  Blocks [nbx, nbx + (C / 64) * kHeadKS): the weight gradient of one
+// 64-channel slice over one of kHeadKS sample chunks (one atomic per (n, c) per
+// dx block measured 34 us: 64 adds per address serialise; one block per slice
+// over ALL samples 36 us: a serial 16-deep load chain per thread).  dW role:
+// thread t takes channel vector t % 8 of the slice and samples t / 8 + 32 i of
+// its chunk, loads issued together; the 32 sample groups are summed through LDS
+// one class at a time and added with kHeadKS atomics per (n, c).
 __global__ void __launch_bounds__(256) gap_linear_bwd_kernel(
     const u16* __restrict__ dy, const u16* __restrict__ f, const u16* __restrict__ w,
     u16* __restrict__ dx, float* __restrict__ gw, float* __restrict__ gb, int B, int HW, int C,
-    int N) {
-  __shared__ float red[4][64 * 8];   // one class's dW partials of a channel slice, per wave
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int b0 = (blockIdx.x * 4 + wid) * SPW;
-  const float inv = 1.f / (float)HW;
-  float dbp[kHeadN];
+    int N, int nbx) {
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x < nbx) {
+    const int lane = tid & 63;
+    const int b = blockIdx.x * 4 + (tid >> 6);
+    if (b >= B) return;
+    const float inv = 1.f / (float)HW;
+    float dv[kHeadN];
 #pragma unroll
-  for (int n = 0; n < kHeadN; ++n) dbp[n] = 0.f;
+    for (int n = 0; n < kHeadN; ++n) dv[n] = n < N ? bf2f(dy[(long long)b * N + n]) : 0.f;
 #pragma unroll
-  for (int k = 0; k < kHeadCV; ++k) {
-    if (k * 512 >= C) break;                 // uniform
-    const int c = (k * 64 + lane) * 8;
-    const bool con = c < C;
-    float gwp[kHeadN][8];
-#pragma unroll
-    for (int n = 0; n < kHeadN; ++n)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) gwp[n][e] = 0.f;
-    bf16x8 wv[kHeadN];
-#pragma unroll
-    for (int n = 0; n < kHeadN; ++n)
-      if (n < N && con) wv[n] = *reinterpret_cast<const bf16x8*>(w + (long long)n * C + c);
-    for (int s = 0; s < SPW; ++s) {
-      const int b = b0 + s;
-      if (b >= B) break;
+    for (int k = 0; k < kHeadCV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c >= C) break;
       float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      float fv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (con) {
-        const bf16x8 fr = *reinterpret_cast<const bf16x8*>(f + (long long)b * C + c);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) fv[e] = bf2f(fr.v[e]);
-      }
-      float dv[kHeadN];
-#pragma unroll
-      for (int n = 0; n < kHeadN; ++n) dv[n] = n < N ? bf2f(dy[(long long)b * N + n]) : 0.f;
 #pragma unroll
       for (int n = 0; n < kHeadN; ++n) {
         if (n < N) {
-          const float d = dv[n];
-          if (k == 0) dbp[n] += d;
-          if (con) {
+          const bf16x8 wr = *reinterpret_cast<const bf16x8*>(w + (long long)n * C + c);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              g[e] += d * bf2f(wv[n].v[e]);
-              gwp[n][e] += d * fv[e];
-            }
-          }
+          for (int e = 0; e < 8; ++e) g[e] += dv[n] * bf2f(wr.v[e]);
         }
       }
-      if (con) {
-        bf16x8 o;
+      bf16x8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o.v[e] = f2bf(g[e] * inv);
-        u16* pd = dx + (long long)b * HW * C + c;
+      for (int e = 0; e < 8; ++e) o.v[e] = f2bf(g[e] * inv);
+      u16* pd = dx + (long long)b * HW * C + c;
 #pragma unroll 4
-        for (int p = 0; p < HW; ++p) *reinterpret_cast<bf16x8*>(pd + (long long)p * C) = o;
+      for (int p = 0; p < HW; ++p) *reinterpret_cast<bf16x8*>(pd + (long long)p * C) = o;
+    }
+    return;
+  }
+  __shared__ float red[32][64];                 // [sample group][channel of the slice]
+  const int role = blockIdx.x - nbx, slice = role / kHeadKS, chunk = role % kHeadKS;
+  const int cv = tid & 7, sg = tid >> 3;
+  const int c = slice * 64 + cv * 8;
+  const int per = (B + kHeadKS - 1) / kHeadKS;
+  const int bbeg = chunk * per, bend = min(B, bbeg + per);
+  float gwp[kHeadN][8];
+#pragma unroll
+  for (int n = 0; n < kHeadN; ++n)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gwp[n][e] = 0.f;
+  float dbp[kHeadN];
+#pragma unroll
+  for (int n = 0; n < kHeadN; ++n) dbp[n] = 0.f;
+  for (int b = bbeg + sg; b < bend; b += 32 * kHeadU) {
+    bf16x8 fr[kHeadU];
+    float dv[kHeadU][kHeadN];
+#pragma unroll
+    for (int u = 0; u < kHeadU; ++u) {       // every load of kHeadU samples in flight
+      const int bu = b + 32 * u;
+      const bool ok = bu < bend;
+      fr[u] = ok ? *reinterpret_cast<const bf16x8*>(f + (long long)bu * C + c) : bf16x8{};
+#pragma unroll
+      for (int n = 0; n < kHeadN; ++n) dv[u][n] = ok && n < N ? bf2f(dy[(long long)bu * N + n]) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kHeadU; ++u)
+#pragma unroll
+      for (int n = 0; n < kHeadN; ++n) {
+        if (n < N) {
+          dbp[n] += dv[u][n];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gwp[n][e] += dv[u][n] * bf2f(fr[u].v[e]);
+        }
+      }
+  }
+#pragma unroll
+  for (int n = 0; n < kHeadN; ++n) {
+    if (n < N) {
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[sg][cv * 8 + e] = gwp[n][e];
+      __syncthreads();
+      if (tid < 64) {
+        float v = 0.f;
+#pragma unroll 8
+        for (int q = 0; q < 32; ++q) v += red[q][tid];
+        atomicAdd(gw + (long long)n * C + slice * 64 + tid, v);
       }
     }
-    // the block's 4 waves hold partials of the same channels: sum them through
-    // LDS, one class at a time, and let wave 0 add them (one atomic per (n, c))
+  }
+  if (slice == 0 && gb != nullptr) {
+    // every channel-vector lane of a sample group summed the same dy: take cv 0's
 #pragma unroll
     for (int n = 0; n < kHeadN; ++n) {
       if (n < N) {
         __syncthreads();
-#pragma unroll
-        for (int e = 0; e < 8; ++e) red[wid][lane * 8 + e] = gwp[n][e];
+        if (cv == 0) red[sg][0] = dbp[n];
         __syncthreads();
-        if (wid == 0 && con) {
-          float* dst = gw + (long long)n * C + c;
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            atomicAdd(dst + e, red[0][lane * 8 + e] + red[1][lane * 8 + e] +
-                                   red[2][lane * 8 + e] + red[3][lane * 8 + e]);
+        if (tid == 0) {
+          float v = 0.f;
+          for (int q = 0; q < 32; ++q) v += red[q][0];
+          atomicAdd(gb + n, v);
         }
       }
     }
   }
-  // db: every lane of a wave summed the same dy values; one atomic per class per wave
-  if (gb != nullptr && lane < N) {
-    float v = 0.f;
-#pragma unroll
-    for (int n = 0; n < kHeadN; ++n) v = n == lane ? dbp[n] : v;
-    atomicAdd(gb + lane, v);
-  }
 }
 
-bool gap_linear_supported(int C, int N) { return N >= 1 && N <= kHeadN && C % 8 == 0 && C <= 64 * 8 * kHeadCV; }
+bool gap_linear_supported(int C, int N) {
+  return N >= 1 && N <= kHeadN && C % 64 == 0 && C <= 64 * 8 * kHeadCV;
+}
 
 void launch_gap_linear_fwd(const u16* x, const u16* w, const u16* bias, u16* y, u16* f, int B, int HW,
                            int C, int N, hipStream_t s) {
@@ -185,9 +209,9 @@ void launch_gap_linear_fwd(const u16* x, const u16* w, const u16* bias, u16* y, 
 
 void launch_gap_linear_bwd(const u16* dy, const u16* f, const u16* w, u16* dx, float* gw, float* gb,
                            int B, int HW, int C, int N, hipStream_t s) {
-  constexpr int SPW = 2;
-  hipLaunchKernelGGL(gap_linear_bwd_kernel<SPW>, dim3((unsigned)((B + 4 * SPW - 1) / (4 * SPW))),
-                     dim3(256), 0, s, dy, f, w, dx, gw, gb, B, HW, C, N);
+  const int nbx = (B + 3) / 4;
+  hipLaunchKernelGGL(gap_linear_bwd_kernel, dim3((unsigned)(nbx + C / 64 * kHeadKS)), dim3(256), 0, s, dy, f,
+                     w, dx, gw, gb, B, HW, C, N, nbx);
 }
 
 }  // namespace dmp

@@ -505,7 +505,7 @@ def test_relu_mask_hand_off_with_two_consumers():
         assert rel < 5e-2, (order, rel)
 
 
-@pytest.mark.parametrize("B,C,H,N", [(512, 512, 4, 10), (37, 2048, 7, 16), (5, 64, 8, 3), (9, 1000, 2, 7)])
+@pytest.mark.parametrize("B,C,H,N", [(512, 512, 4, 10), (37, 2048, 7, 16), (5, 64, 8, 3), (9, 1024, 2, 7), (3, 1000, 2, 7)])
 def test_gap_linear_head_fused(B, C, H, N):
     """Fused global-average-pool + Linear head (csrc/head.hip): logits, dx, dW (+=)
     and db (+=) against fp32 autograd of mean-pool + linear."""
