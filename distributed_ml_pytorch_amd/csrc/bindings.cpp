@@ -813,7 +813,8 @@ SmallGeom small_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t p
 
 // ImageNet stem (csrc/stem.hip): x [B, 3, H, W] channels_last bf16, w [64, 3, 7, 7]
 // channels_last bf16 -> (y [B, 64, H/2, W/2] channels_last, BN slots, xs for the wgrad)
-std::vector<Tensor> stem_fwd(Tensor x, Tensor w, bool want_stats, optional<Tensor> slots) {
+std::vector<Tensor> stem_fwd(Tensor x, Tensor w, bool want_stats, optional<Tensor> slots,
+                             optional<Tensor> bias, bool relu) {
   check_gpu(x, "x");
   check_gpu(w, "w");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3 &&
@@ -831,6 +832,11 @@ std::vector<Tensor> stem_fwd(Tensor x, Tensor w, bool want_stats, optional<Tenso
   auto y = at::empty({B, 64, H / 2, W / 2}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor part;
   if (want_stats) part = bn_slots(slots, 64, x.options());
+  if (bias) {
+    check_gpu(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == 64 && bias->is_contiguous(),
+                "stem: bias must be a contiguous fp32 [64] tensor");
+  }
   auto st = cur_stream();
   dmp::launch_stem_s2d(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                        reinterpret_cast<uint16_t*>(xs.data_ptr()), (int)B, (int)H, (int)W, st);
@@ -839,7 +845,8 @@ std::vector<Tensor> stem_fwd(Tensor x, Tensor w, bool want_stats, optional<Tenso
   dmp::launch_stem_fwd(reinterpret_cast<const uint16_t*>(xs.data_ptr()),
                        reinterpret_cast<const uint16_t*>(wp.data_ptr()),
                        reinterpret_cast<uint16_t*>(y.data_ptr()),
-                       want_stats ? part.data_ptr<float>() : nullptr, (int)B, (int)H, (int)W, st);
+                       want_stats ? part.data_ptr<float>() : nullptr, (int)B, (int)H, (int)W, st,
+                       bias ? bias->data_ptr<float>() : nullptr, relu);
   return {y, part, xs};
 }
 
@@ -1622,7 +1629,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("stem_supported", [](int64_t H, int64_t W) { return dmp::stem_supported((int)H, (int)W); },
         "ImageNet 7x7/2 stem kernel applies to an H x W input");
   m.def("stem_fwd", &stem_fwd, "ImageNet stem conv forward (+BN partials) via space-to-depth",
-        py::arg("x"), py::arg("w"), py::arg("want_stats"), py::arg("slots") = py::none());
+        py::arg("x"), py::arg("w"), py::arg("want_stats"), py::arg("slots") = py::none(),
+        py::arg("bias") = py::none(), py::arg("relu") = false);
   m.def("stem_wgrad", &stem_wgrad, "ImageNet stem conv weight gradient (fp32 +=)", py::arg("dy"),
         py::arg("xs"), py::arg("dw"));
   m.def("conv_small_fwd", &conv_small_fwd, "few-input-channel conv forward (+BN partials)",

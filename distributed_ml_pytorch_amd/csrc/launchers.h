@@ -251,7 +251,7 @@ void launch_stem_s2d(const uint16_t* x, uint16_t* xs, int B, int H, int W, hipSt
 void launch_stem_wpack(const uint16_t* w, uint16_t* wp, hipStream_t s);
 void launch_stem_wfold(const float* dwp, float* dw, hipStream_t s);
 void launch_stem_fwd(const uint16_t* xs, const uint16_t* wp, uint16_t* y, float* part, int B,
-                     int H, int W, hipStream_t s);
+                     int H, int W, hipStream_t s, const float* bias = nullptr, bool relu = false);
 void launch_stem_wgrad(const uint16_t* dy, const uint16_t* xs, float* dwp, int B, int H, int W,
                        hipStream_t s);
 

@@ -144,11 +144,15 @@ struct StemGeom {
   int OH, OW, TH, APW, ntiles;
 };
 
+// bias (fp32 [64], may be null) and relu: the inference-time BatchNorm fold
+// (ops/eval_fold.py) -- the eval forward's stem is then ONE launch instead of
+// im2col + GEMM
 template <int TM, int NS, bool STATS>
 __global__ void __launch_bounds__(256) stem_fwd_kernel(const u16* __restrict__ xs,
                                                        const u16* __restrict__ wp,
                                                        u16* __restrict__ y, float* __restrict__ part,
-                                                       int B, StemGeom sg) {
+                                                       int B, StemGeom sg,
+                                                       const float* __restrict__ bias, int relu) {
   constexpr int NW = 4, TN = kSCO / 16, NSTEP = kSK / 32;
   constexpr int OW = TM * 16, W2 = OW + 3;
   extern __shared__ __attribute__((aligned(16))) u16 lds_s[];
@@ -240,11 +244,15 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const u16* __restrict__ x
     }
   };
 
-  float s_sum[TN][4], s_sq[TN][4];
+  float s_sum[TN][4], s_sq[TN][4], bj[TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { s_sum[j][r] = 0.f; s_sq[j][r] = 0.f; }
+    for (int r = 0; r < 4; ++r) {
+      s_sum[j][r] = 0.f;
+      s_sq[j][r] = 0.f;
+      bj[j][r] = bias != nullptr ? bias[j * 16 + 4 * kg + r] : 0.f;
+    }
   auto epilogue = [&](int k) {
     const int t = tile_of(k);
     const int b = t / tpi, oh0 = (t - b * tpi) * NW;
@@ -258,7 +266,9 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const u16* __restrict__ x
         u16 hv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          hv[r] = f2bf(acc[i][j][r]);
+          float t = acc[i][j][r] + bj[j][r];
+          if (relu) t = fmaxf(t, 0.f);
+          hv[r] = f2bf(t);
           if (STATS) {
             const float v = bf2f(hv[r]);
             s_sum[j][r] += v;
@@ -509,7 +519,7 @@ void launch_stem_wfold(const float* dwp, float* dw, hipStream_t s) {
 }
 
 void launch_stem_fwd(const u16* xs, const u16* wp, u16* y, float* part, int B, int H, int W,
-                     hipStream_t s) {
+                     hipStream_t s, const float* bias, bool relu) {
   constexpr int TM = 7, NS = 3;
   StemGeom g{};
   g.OH = H / 2;
@@ -523,11 +533,11 @@ void launch_stem_fwd(const u16* xs, const u16* wp, u16* y, float* part, int B, i
   if (part) {
     allow_lds160(stem_fwd_kernel<TM, NS, true>);
     hipLaunchKernelGGL((stem_fwd_kernel<TM, NS, true>), dim3(grid), dim3(256), lds, s, xs, wp, y,
-                       part, B, g);
+                       part, B, g, bias, relu ? 1 : 0);
   } else {
     allow_lds160(stem_fwd_kernel<TM, NS, false>);
     hipLaunchKernelGGL((stem_fwd_kernel<TM, NS, false>), dim3(grid), dim3(256), lds, s, xs, wp, y,
-                       part, B, g);
+                       part, B, g, bias, relu ? 1 : 0);
   }
 }
 

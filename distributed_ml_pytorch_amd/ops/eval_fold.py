@@ -86,7 +86,7 @@ def conv_bn(x, conv, bn, residual=None):
     conv / GEMM launch (``bn.relu`` says whether a ReLU follows); ``None`` when
     the pair or geometry is not covered (the caller runs the regular path)."""
     from .conv import (_GEMM_ROUTE, _ceil8, _fwd_cfg, _pair, im2col_conv_supported,
-                       native_conv_supported)
+                       native_conv_supported, stem_conv_supported)
     from .linear import gemm
 
     if not _foldable(bn) or conv.groups != 1 or _pair(conv.dilation) != (1, 1):
@@ -110,6 +110,10 @@ def conv_bn(x, conv, bn, residual=None):
             return y2.view(B, H, W, CO).permute(0, 3, 1, 2)
         y, _, _ = native().conv_fwd(x, w16, st, pd, False, cfg, None, f["t32"], relu, residual)
         return y
+    if residual is None and stem_conv_supported(x, conv.weight, conv.stride, conv.padding,
+                                                 conv.dilation, 1):
+        # ImageNet 7x7/2 stem: the space-to-depth MFMA kernel, shift + ReLU in its epilogue
+        return native().stem_fwd(x, w16, False, None, f["t32"], relu)[0]
     if residual is None and im2col_conv_supported(x, conv.weight, conv.stride, conv.padding,
                                                    conv.dilation, 1):
         # stems (3 input channels): patch matrix + GEMM, shift + ReLU in its epilogue

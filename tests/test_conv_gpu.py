@@ -238,7 +238,8 @@ def test_conv_fwd_bias_addend_relu_epilogue(cfg_kind):
         assert _rel(y, ref) < 1e-2, (cfg, _rel(y, ref))
 
 
-@pytest.mark.parametrize("model,shape", [("resnet18", (3, 32, 32)), ("resnet50", (3, 64, 64))])
+@pytest.mark.parametrize("model,shape", [("resnet18", (3, 32, 32)), ("resnet50", (3, 64, 64)),
+                                         ("resnet50", (3, 224, 224))])   # 224: the 7x7 stem kernel
 def test_eval_bn_fold_matches_unfolded_eval(model, shape):
     """Eval forward with every BatchNorm folded into its conv (ops/eval_fold.py)
     == the regular eval forward (running-statistics BN passes), after a few
