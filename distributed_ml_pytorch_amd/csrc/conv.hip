@@ -164,7 +164,15 @@ __device__ __forceinline__ int swz(int row, int c) {
 // NS-stage LDS-DMA ring: NS-1 k-tiles in flight while one is consumed.  (A
 // register-staged variant -- global_load into VGPRs, ds_write_b128 -- measured
 // 2-4x slower on every ResNet-18 shape: profiles/igemm_ablate_r1.txt.)
-template <int BM, int BN, int BK, int WM, int WN, int MODE, bool STATS, int NS>
+template <int BM, int BN, int WM, int WN, bool FLIP, bool STATS, int TM, int TN>
+__device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&acc)[TM][TN],
+                                                   long long m0, int n0, int wm, int wn, int tid,
+                                                   int lane, u16* lds_h, int mv);
+
+// ROWS (forward only): the row-staged epilogue of the halo kernels (16-B row
+// segments out of an LDS block tile) instead of the D^T register stores --
+// for the store-bound 1x1 convs (K = 64 input channels, 4x the output bytes).
+template <int BM, int BN, int BK, int WM, int WN, int MODE, bool STATS, int NS, bool ROWS = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN;
   constexpr int CPR = BK / 8;                 // 16-B chunks per tile row
@@ -181,7 +189,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   // the minimum is conservative for it)
   constexpr int INS_MIN = A_INS / NW + B_INS / NW;
   static_assert(NS >= 2 && (NS - 2) * INS_MIN < 64, "pipeline depth");
-  __shared__ __attribute__((aligned(16))) u16 lds[NS * STAGE];
+  static_assert(!ROWS || MODE == 0, "row-staged epilogue: forward tiles");
+  constexpr int LDS_EL = (ROWS && BM * (BN + 8) > NS * STAGE) ? BM * (BN + 8) : NS * STAGE;
+  __shared__ __attribute__((aligned(16))) u16 lds[LDS_EL];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -340,6 +350,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
     }
   }
   __syncthreads();   // all ring reads done before the epilogue reuses LDS
+  if constexpr (ROWS) {
+    halo_epilogue_rows<BM, BN, WM, WN, false, STATS, TM, TN>(a, acc, m0, n0, wm, wn, tid, lane,
+                                                             lds, BM);
+    return;
+  }
 
   // epilogue: D^T layout -> lane owns channels n..n+3 of output row m.
   // Stores go through a buffer descriptor with 32-bit offsets; rows past M and
@@ -699,7 +714,7 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
 template <int BM, int BN, int WM, int WN, bool FLIP, bool STATS, int TM, int TN>
 __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&acc)[TM][TN],
                                                    long long m0, int n0, int wm, int wn, int tid,
-                                                   int lane, u16* lds_h, int mv = BM) {
+                                                   int lane, u16* lds_h, int mv) {
   constexpr int NW = WM * WN, PITCH = BN + 8, CPR = BN / 8, RPI = 64 / CPR;
   static_assert(BN % 8 == 0 && 64 % CPR == 0, "row segments of 8 channels");
   typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -987,7 +1002,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   // 128 / 256-channel layers, no change on the forward, whose BN sums cost
   // more in the row layout: profiles/conv_roofline_r4.txt)
   if constexpr ((DMP_HALO_EPI_LDS || FLIP) && !(FLIP && STATS))
-    halo_epilogue_rows<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h, MV);
+    halo_epilogue_rows<BM, BN, WM, WN, FLIP, STATS, TM, TN>(a, acc, m0, n0, wm, wn, tid, lane, lds_h,
+                                                            MV);
   else
     halo_epilogue<BM, BN, WM, WN, FLIP, STATS>(a, acc, m0, n0, wm, wn, tid, lane, lds_h, 0, MV);
 }
@@ -1563,13 +1579,21 @@ __global__ void __launch_bounds__(256) conv_weight_transpose_kernel(
   X(21, 128, 64, 64, 2, 2, 3)    \
   X(22, 64, 64, 32, 2, 2, 4)     \
   X(23, 128, 128, 32, 2, 2, 4)
+// 24-27: forward tiles with the row-staged epilogue (conv_igemm_kernel<ROWS>);
+// as data-gradient tiles they run the plain epilogue of the same geometry
+#define DMP_CONV_CONFIGS_ROWS(X) \
+  X(24, 128, 128, 32, 2, 4, 2)   \
+  X(25, 128, 128, 64, 2, 4, 2)   \
+  X(26, 256, 128, 32, 4, 2, 2)   \
+  X(27, 128, 64, 32, 2, 2, 4)
 
-constexpr int kNumConvConfigs = 24;
+constexpr int kNumConvConfigs = 28;
 
 static int config_bm(int cfg) {
   switch (cfg) {
 #define X(id, BM, BN, BK, WM, WN, NS) case id: return BM;
     DMP_CONV_CONFIGS(X)
+    DMP_CONV_CONFIGS_ROWS(X)
 #undef X
   }
   return 128;
@@ -1582,6 +1606,7 @@ void conv_config_info(int cfg, int* info) {
 #define X(id, BM, BN, BK, WM, WN, NS) \
   case id: info[0] = BM; info[1] = BN; info[2] = BK; info[3] = 64 * WM * WN; info[4] = NS; return;
     DMP_CONV_CONFIGS(X)
+    DMP_CONV_CONFIGS_ROWS(X)
 #undef X
   }
   info[0] = info[1] = info[2] = info[3] = info[4] = 0;
@@ -1601,12 +1626,12 @@ int conv_default_config(long long M, int CO) {
   return 5;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int NS, int MODE, bool STATS>
+template <int BM, int BN, int BK, int WM, int WN, int NS, int MODE, bool STATS, bool ROWS = false>
 static void launch_cfg(const ConvArgs& a, int classes, hipStream_t s) {
   const dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)((a.CO + BN - 1) / BN),
                   (unsigned)classes);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, MODE, STATS, NS>), grid,
-                     dim3(64 * WM * WN), 0, s, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, MODE, STATS, NS, ROWS && MODE == 0>),
+                     grid, dim3(64 * WM * WN), 0, s, a);
 }
 
 template <int MODE, bool STATS>
@@ -1615,6 +1640,10 @@ static void dispatch(const ConvArgs& a, int cfg, int classes, hipStream_t s) {
 #define X(id, BM, BN, BK, WM, WN, NS) \
   case id: launch_cfg<BM, BN, BK, WM, WN, NS, MODE, STATS>(a, classes, s); return;
     DMP_CONV_CONFIGS(X)
+#undef X
+#define X(id, BM, BN, BK, WM, WN, NS) \
+  case id: launch_cfg<BM, BN, BK, WM, WN, NS, MODE, STATS, true>(a, classes, s); return;
+    DMP_CONV_CONFIGS_ROWS(X)
 #undef X
   }
 }

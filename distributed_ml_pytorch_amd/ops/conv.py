@@ -100,8 +100,12 @@ def _configs():
     return _CONFIGS
 
 
-def _igemm_candidates(out_channels: int):
-    return [c[0] for c in _configs() if c[2] <= max(64, out_channels)]
+_IGEMM_ROWS_IDS = range(24, 28)   # forward tiles with the row-staged epilogue (csrc/conv.hip)
+
+
+def _igemm_candidates(out_channels: int, fwd: bool = True):
+    return [c[0] for c in _configs() if c[2] <= max(64, out_channels)
+            and (fwd or c[0] not in _IGEMM_ROWS_IDS)]
 
 
 def _wgrad_candidates(K: int, CO: int | None = None):
@@ -205,7 +209,7 @@ def _fwd_cfg(x, w16, stride, pad):
 
 def _dgrad_cfg(dy, w16, H, W, stride, pad):
     key = ("dgrad", *dy.shape, w16.shape[1], H, W, w16.shape[2], w16.shape[3], stride, pad)
-    cands = _igemm_candidates(w16.shape[1])
+    cands = _igemm_candidates(w16.shape[1], fwd=False)
     if (H, W) == tuple(dy.shape[2:]):
         cands += _halo_candidates(H, W, dy.shape[1], w16.shape[2], w16.shape[3], stride, pad)
     elif _HALO_ENABLED and stride == 2:

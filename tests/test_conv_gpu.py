@@ -144,6 +144,37 @@ def test_halo_conv_configs(B, C, H, W, CO):
         assert _rel(dw, 2 * wr.grad) < 1e-2, cfg
 
 
+@pytest.mark.parametrize("B,CI,H,CO,k,st,pd", [(3, 64, 14, 256, 1, 1, 0), (2, 256, 7, 64, 1, 1, 0),
+                                                (2, 64, 9, 128, 3, 1, 1), (3, 64, 8, 64, 3, 2, 1)])
+def test_igemm_row_epilogue_configs(B, CI, H, CO, k, st, pd):
+    """Implicit-GEMM forward tiles with the row-staged epilogue (cfg ids 24-27):
+    output + BN partial sums, and the bias / addend / ReLU inference epilogue, vs fp32."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    torch.manual_seed(0)
+    x = torch.randn(B, CI, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(CO, CI, k, k, device="cuda") / (CI * k * k) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    yr = F.conv2d(x.float(), w.float(), None, st, pd)
+    bias = torch.randn(CO, device="cuda")
+    add = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    for cfg in (24, 25, 26, 27):
+        y, part, G = nat.conv_fwd(x, w, st, pd, True, cfg)
+        assert _rel(y, yr) < 1e-2, cfg
+        ps = part[:2 * int(G) * CO].view(2, int(G), CO).sum(1)
+        yf = y.float()
+        torch.testing.assert_close(ps[0], yf.sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+        torch.testing.assert_close(ps[1], (yf * yf).sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-2)
+        y2, _, _ = nat.conv_fwd(x, w, st, pd, False, cfg, None, bias, True, add)
+        ref = torch.relu(yr + bias.view(1, -1, 1, 1) + add.float())
+        assert _rel(y2, ref) < 1e-2, cfg
+        dx = nat.conv_dgrad(add, w, H, H, st, pd, cfg)      # as a data-gradient tile: plain epilogue
+        xr = x.float().requires_grad_(True)
+        F.conv2d(xr, w.float(), None, st, pd).backward(add.float())
+        assert _rel(dx, xr.grad) < 1e-2, cfg
+
+
 @pytest.mark.parametrize("B,C,H,CO", [
     (3, 64, 32, 128), (5, 128, 16, 256), (9, 256, 8, 512),      # ResNet-18 stride-2 3x3 convs
     (2, 128, 56, 128),                                          # ResNet-50 (v1.5) stage-2 stride-2 3x3
