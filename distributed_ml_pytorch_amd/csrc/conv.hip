@@ -169,9 +169,11 @@ __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&ac
                                                    long long m0, int n0, int wm, int wn, int tid,
                                                    int lane, u16* lds_h, int mv);
 
-// ROWS (forward only): the row-staged epilogue of the halo kernels (16-B row
-// segments out of an LDS block tile) instead of the D^T register stores --
-// for the store-bound 1x1 convs (K = 64 input channels, 4x the output bytes).
+// ROWS: the row-staged epilogue of the halo kernels (16-B row segments out of
+// an LDS block tile) instead of the D^T register stores -- for the store-bound
+// 1x1 convs (K = 64 input channels, 4x the output bytes).  Forward tiles, and
+// stride-1 data-gradient tiles without the fused BN backward (output row m =
+// dX pixel m there too; the launcher checks).
 template <int BM, int BN, int BK, int WM, int WN, int MODE, bool STATS, int NS, bool ROWS = false>
 __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN;
@@ -189,7 +191,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   // the minimum is conservative for it)
   constexpr int INS_MIN = A_INS / NW + B_INS / NW;
   static_assert(NS >= 2 && (NS - 2) * INS_MIN < 64, "pipeline depth");
-  static_assert(!ROWS || MODE == 0, "row-staged epilogue: forward tiles");
+  static_assert(!ROWS || MODE == 0 || !STATS, "row-staged epilogue: no fused BN backward");
   constexpr int LDS_EL = (ROWS && BM * (BN + 8) > NS * STAGE) ? BM * (BN + 8) : NS * STAGE;
   __shared__ __attribute__((aligned(16))) u16 lds[LDS_EL];
 
@@ -351,8 +353,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   }
   __syncthreads();   // all ring reads done before the epilogue reuses LDS
   if constexpr (ROWS) {
-    halo_epilogue_rows<BM, BN, WM, WN, false, STATS, TM, TN>(a, acc, m0, n0, wm, wn, tid, lane,
-                                                             lds, BM);
+    halo_epilogue_rows<BM, BN, WM, WN, MODE == 1, MODE == 0 && STATS, TM, TN>(
+        a, acc, m0, n0, wm, wn, tid, lane, lds, BM);
     return;
   }
 
@@ -1579,8 +1581,9 @@ __global__ void __launch_bounds__(256) conv_weight_transpose_kernel(
   X(21, 128, 64, 64, 2, 2, 3)    \
   X(22, 64, 64, 32, 2, 2, 4)     \
   X(23, 128, 128, 32, 2, 2, 4)
-// 24-27: forward tiles with the row-staged epilogue (conv_igemm_kernel<ROWS>);
-// as data-gradient tiles they run the plain epilogue of the same geometry
+// 24-27: tiles with the row-staged epilogue (conv_igemm_kernel<ROWS>): forward,
+// and stride-1 data gradients without the fused BN backward; otherwise they run
+// the plain epilogue of the same geometry
 #define DMP_CONV_CONFIGS_ROWS(X) \
   X(24, 128, 128, 32, 2, 4, 2)   \
   X(25, 128, 128, 64, 2, 4, 2)   \
@@ -1630,8 +1633,15 @@ template <int BM, int BN, int BK, int WM, int WN, int NS, int MODE, bool STATS, 
 static void launch_cfg(const ConvArgs& a, int classes, hipStream_t s) {
   const dim3 grid((unsigned)((a.M + BM - 1) / BM), (unsigned)((a.CO + BN - 1) / BN),
                   (unsigned)classes);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, MODE, STATS, NS, ROWS && MODE == 0>),
-                     grid, dim3(64 * WM * WN), 0, s, a);
+  // row-staged epilogue: forward, or a stride-1 data gradient without the fused BN
+  // backward (one parity class, output row = dX pixel); otherwise the plain tile
+  constexpr bool R = ROWS && (MODE == 0 || !STATS);
+  if (R && (MODE == 0 || (a.stride == 1 && !a.addend_sub)))
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, MODE, STATS, NS, R>), grid,
+                       dim3(64 * WM * WN), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, MODE, STATS, NS, false>), grid,
+                       dim3(64 * WM * WN), 0, s, a);
 }
 
 template <int MODE, bool STATS>

@@ -209,7 +209,8 @@ def _fwd_cfg(x, w16, stride, pad):
 
 def _dgrad_cfg(dy, w16, H, W, stride, pad):
     key = ("dgrad", *dy.shape, w16.shape[1], H, W, w16.shape[2], w16.shape[3], stride, pad)
-    cands = _igemm_candidates(w16.shape[1], fwd=False)
+    # the row-staged epilogue tiles apply to stride-1 data gradients too
+    cands = _igemm_candidates(w16.shape[1], fwd=stride == 1)
     if (H, W) == tuple(dy.shape[2:]):
         cands += _halo_candidates(H, W, dy.shape[1], w16.shape[2], w16.shape[3], stride, pad)
     elif _HALO_ENABLED and stride == 2:
