@@ -29,6 +29,8 @@
 // and every output tile is written as 4 consecutive head-dim values per lane
 // (8-B stores).  Softmax statistics are saved as a base-2 log-sum-exp of the
 // scaled scores (lse2), so P = exp2(s * scale * log2e - lse2) in the backward.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dmp {
@@ -115,8 +117,14 @@ __device__ __forceinline__ void stage2(const u16* __restrict__ s0, int rs0,
 
 }  // namespace
 
+// KB > 0 would make the key / query block count a compile-time constant: measured
+// 2.2x SLOWER on the backward at N = 197 (the fully unrolled loops hoisted every
+// fragment read: 256 VGPRs, one workgroup per CU), so only KB = 0 is launched.
+// The softmax exponentials use v_exp_f32 directly (__builtin_amdgcn_exp2f: the
+// arguments are <= 0 or -inf), not exp2f's range-reduced sequence -- attention
+// fwd 35.6 -> 28.9 us, bwd -> 73.6 us per ViT-B/16 layer (profiles/attention_exp2_r4.txt).
 // ----------------------------------------------------------------- forward
-template <int NW>
+template <int NW, int KB = 0>
 __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const u16* __restrict__ qkv,
                                                           u16* __restrict__ out,
                                                           float* __restrict__ lse2, int N, int H,
@@ -132,7 +140,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const u16* __restrict
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
-  const int nkb = NP / 16, nstrips = (N + 15) / 16;
+  const int nkb = KB > 0 ? KB : NP / 16, nstrips = (N + 15) / 16;
   for (int qs = wid; qs < nstrips; qs += NW) {
     const int q = qs * 16 + l16, qc = q < N ? q : N - 1;
     const u16* qrow = base + (tok0 + qc) * 3 * D;
@@ -162,7 +170,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const u16* __restrict
       if (kb < nkb) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          s[kb][r] = exp2f(s[kb][r] - mx);
+          s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r] - mx);   // <= 0: v_exp_f32, no range fix-up
           sum += s[kb][r];
         }
       }
@@ -192,7 +200,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(const u16* __restrict
 }
 
 // ------------------------------------------------------------- backward: dQ
-template <int NW>
+template <int NW, int KB = 0>
 __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
     const u16* __restrict__ qkv, const u16* __restrict__ out, const u16* __restrict__ dout,
     const float* __restrict__ lse2, u16* __restrict__ dqkv, int N, int H, float scale_log2,
@@ -208,7 +216,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
-  const int nkb = NP / 16, nstrips = (N + 15) / 16;
+  const int nkb = KB > 0 ? KB : NP / 16, nstrips = (N + 15) / 16;
   for (int qs = wid; qs < nstrips; qs += NW) {
     const int q = qs * 16 + l16, qc = q < N ? q : N - 1;
     const u16* qrow = base + (tok0 + qc) * 3 * D;
@@ -243,7 +251,8 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
           dp = mfma(ld16(vr + 32), df1, dp);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = (kb * 16 + 4 * g + r) < N ? exp2f(st[r] * scale_log2 - L) : 0.f;
+            const float p = (kb * 16 + 4 * g + r) < N
+                                ? __builtin_amdgcn_exp2f(st[r] * scale_log2 - L) : 0.f;
             ds[hf][r] = p * (dp[r] - di);
           }
         }
@@ -262,7 +271,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dq_kernel(
 }
 
 // --------------------------------------------------------- backward: dK, dV
-template <int NW>
+template <int NW, int KB = 0>
 __global__ void __launch_bounds__(64 * NW) attn_bwd_dkv_kernel(
     const u16* __restrict__ qkv, const u16* __restrict__ out, const u16* __restrict__ dout,
     const float* __restrict__ lse2, u16* __restrict__ dqkv, int N, int H, float scale_log2,
@@ -313,7 +322,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkv_kernel(
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
-  const int nqb = NP / 16, nstrips = (N + 15) / 16;
+  const int nqb = KB > 0 ? KB : NP / 16, nstrips = (N + 15) / 16;
   for (int ks = wid; ks < nstrips; ks += NW) {
     const int key = ks * 16 + l16, kc = key < N ? key : N - 1;
     const u16* krow = base + (tok0 + kc) * 3 * D + D;
@@ -342,7 +351,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_dkv_kernel(
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int qq = qb * 16 + 4 * g + r;
-            const float p = exp2f(s[r] * scale_log2 - Ls[qq]);
+            const float p = __builtin_amdgcn_exp2f(s[r] * scale_log2 - Ls[qq]);   // Ls = +inf past N
             pp[hf][r] = p;
             ds[hf][r] = p * (dp[r] - Di[qq]);
           }
@@ -394,9 +403,10 @@ void allow_lds(K kernel, size_t bytes) {
 void launch_attention_fwd(const u16* qkv, u16* out, float* lse2, int B, int N, int H, float scale,
                           hipStream_t s) {
   const size_t lds = fwd_lds(N);
+  const float sl2 = scale * 1.4426950408889634f;
   allow_lds(attn_fwd_kernel<kFwdWaves>, lds);
   hipLaunchKernelGGL(attn_fwd_kernel<kFwdWaves>, dim3(B * H), dim3(64 * kFwdWaves), lds, s, qkv,
-                     out, lse2, N, H, scale * 1.4426950408889634f);
+                     out, lse2, N, H, sl2);
 }
 
 void launch_attention_bwd(const u16* qkv, const u16* out, const u16* dout, const float* lse2,
