@@ -486,6 +486,7 @@ __global__ void __launch_bounds__(256) stem3_fwd_kernel(Stem3Args a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s[j][r] = 0.f; q[j][r] = 0.f; }
   const long long base = ((long long)blockIdx.x * 4 + wid) * a.groups * 16;
+  __shared__ __attribute__((aligned(16))) u16 stg[4][16][72];   // per wave: 16 pixels x 64 ch (+pad)
   // the 8-tap gather of group gi+1 is issued before group gi's MFMAs and stores:
   // one dependent L2 round trip per group otherwise set the kernel time (a wave
   // walks its groups in sequence at 2 waves / SIMD)
@@ -516,6 +517,9 @@ __global__ void __launch_bounds__(256) stem3_fwd_kernel(Stem3Args a) {
     for (int j = 0; j < 4; ++j) acc[j] = s3_mfma(wf[j], xf, f32x4{0.f, 0.f, 0.f, 0.f});
     // D: lane holds channels 16j + 4kg + r of pixel `col`... of THIS group's pixel px
     // (D row = co, D col = pixel: lane = (row block kg, col))
+    // the D fragments (8 B per lane: 16 pixels x 32 B per store instruction) go
+    // through a wave-private LDS tile and leave as whole 128-B pixel rows (16 B
+    // per lane, 8 pixels per instruction); LDS ops of one wave complete in order
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bf16x4 o;
@@ -526,7 +530,14 @@ __global__ void __launch_bounds__(256) stem3_fwd_kernel(Stem3Args a) {
         s[j][r] += v;
         q[j][r] += v * v;
       }
-      if (pv) *reinterpret_cast<bf16x4*>(a.y + px * 64 + 16 * j + 4 * kg) = o;
+      *reinterpret_cast<bf16x4*>(&stg[wid][col][16 * j + 4 * kg]) = o;
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int pr = hh * 8 + (lane >> 3), ck = lane & 7;
+      const long long pxo = base + gi * 16 + pr;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(&stg[wid][pr][ck * 8]);
+      if (pxo < a.P) *reinterpret_cast<bf16x8*>(a.y + pxo * 64 + ck * 8) = v;
     }
   }
   if (a.part == nullptr) return;
