@@ -1583,6 +1583,94 @@ std::vector<Tensor> bn_bwd_fold(Tensor x, Tensor dy, optional<Tensor> y, optiona
                           (int)C, relu, cur_stream(), mptr);
   return {dx, want_dres ? dres : Tensor()};
 }
+
+// BN + ReLU + max pool 3x3/s2/p1 with the finalize folded in (bn.hip): x is the
+// raw conv output; returns the pooled output, its uint8 argmax taps and stats.
+std::vector<Tensor> bn_relu_maxpool_fwd(Tensor x, Tensor part, bool have_partials,
+                                        optional<Tensor> gamma, optional<Tensor> beta,
+                                        optional<Tensor> running_mean,
+                                        optional<Tensor> running_var, double momentum, double eps,
+                                        optional<Tensor> zero_buf, int64_t K, int64_t S,
+                                        int64_t P) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4, "bn_relu_maxpool expects 4-D input");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(dmp::bn_maxpool_supported(C, (int)K, (int)S, (int)P),
+              "bn_relu_maxpool: needs C % 64 == 0, C <= 2048 and a 3x3/s2/p1 window");
+  TORCH_CHECK(2LL * N * H * W * C < (1LL << 31), "bn_relu_maxpool: x over 2 GiB (32-bit offsets)");
+  auto fopt = x.options().dtype(at::kFloat);
+  part = bn_slots(part, C, fopt);
+  float* zb = nullptr;
+  if (zero_buf.has_value() && zero_buf->defined()) {
+    zb = bn_slots(zero_buf, C, fopt).data_ptr<float>();
+    TORCH_CHECK(zb != part.data_ptr<float>(), "bn fold: zero_buf must not alias part");
+  }
+  for (auto* t : {&gamma, &beta, &running_mean, &running_var}) {
+    if (t->has_value()) {
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == C &&
+                      (*t)->is_contiguous(),
+                  "bn affine/running tensors must be contiguous fp32 [C] on the GPU");
+    }
+  }
+  const int Ho = dmp::maxpool_out(H, (int)K, (int)S, (int)P);
+  const int Wo = dmp::maxpool_out(W, (int)K, (int)S, (int)P);
+  TORCH_CHECK(Ho > 0 && Wo > 0, "bn_relu_maxpool: window larger than input");
+  auto mf = at::MemoryFormat::ChannelsLast;
+  auto y = at::empty({N, C, Ho, Wo}, x.options().memory_format(mf));
+  auto idx = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(mf));
+  auto stats = at::empty({4, C}, fopt);
+  dmp::launch_bn_relu_maxpool_fold(
+      reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
+      idx.data_ptr<uint8_t>(), ptr_or_null<float>(gamma), ptr_or_null<float>(beta),
+      ptr_or_null<float>(running_mean), ptr_or_null<float>(running_var), stats.data_ptr<float>(),
+      part.data_ptr<float>(), zb, N, H, W, C, (float)momentum, (float)eps, have_partials,
+      cur_stream());
+  return {y, idx, stats};
+}
+
+// backward of bn_relu_maxpool_fwd: dx of the raw conv output from the pooled
+// gradient; slots = the layer's backward slots (zero on entry), zero_buf = the
+// forward slot sums the forward read
+Tensor maxpool_bn_bwd(Tensor x, Tensor dp, Tensor idx, optional<Tensor> gamma, Tensor stats,
+                      optional<Tensor> dgamma, optional<Tensor> dbeta, Tensor slots,
+                      optional<Tensor> zero_buf, int64_t K, int64_t S, int64_t P) {
+  check_nhwc_bf16(x, "x");
+  auto mf = at::MemoryFormat::ChannelsLast;
+  dp = dp.contiguous(mf);
+  check_nhwc_bf16(dp, "dp");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(dmp::bn_maxpool_supported(C, (int)K, (int)S, (int)P), "maxpool_bn_bwd: bad window");
+  TORCH_CHECK(2LL * N * H * W * C < (1LL << 31), "maxpool_bn_bwd: x over 2 GiB (32-bit offsets)");
+  TORCH_CHECK(dp.size(0) == N && dp.size(1) == C &&
+                  dp.size(2) == dmp::maxpool_out(H, (int)K, (int)S, (int)P) &&
+                  dp.size(3) == dmp::maxpool_out(W, (int)K, (int)S, (int)P),
+              "maxpool_bn_bwd: dp shape mismatch");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.sizes() == dp.sizes() &&
+                  idx.is_contiguous(mf),
+              "maxpool_bn_bwd: idx mismatch");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * C, "bad stats");
+  for (auto* t : {&gamma, &dgamma, &dbeta}) {
+    if (t->has_value()) {
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kFloat && (*t)->numel() == C &&
+                      (*t)->is_contiguous(),
+                  "bn gamma/dgamma/dbeta must be contiguous fp32 [C]");
+    }
+  }
+  auto fopt = x.options().dtype(at::kFloat);
+  auto part = bn_slots(slots, C, fopt);
+  float* zb = nullptr;
+  if (zero_buf.has_value() && zero_buf->defined()) {
+    zb = bn_slots(zero_buf, C, fopt).data_ptr<float>();
+    TORCH_CHECK(zb != part.data_ptr<float>(), "bn fold: zero_buf must not alias slots");
+  }
+  auto dx = at::empty_like(x);
+  dmp::launch_maxpool_bn_bwd_fold(
+      reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(dp.data_ptr()),
+      idx.data_ptr<uint8_t>(), ptr_or_null<float>(gamma), stats.data_ptr<float>(),
+      ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta), part.data_ptr<float>(), zb,
+      reinterpret_cast<uint16_t*>(dx.data_ptr()), N, H, W, C, cur_stream());
+  return dx;
+}
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -1656,6 +1744,20 @@ PYBIND11_MODULE(_native, m) {
         py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("gamma"), py::arg("stats"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"),
         py::arg("slots"), py::arg("mask") = py::none(), py::arg("zero_buf") = py::none());
+  m.def("bn_maxpool_supported",
+        [](int64_t C, int64_t K, int64_t S, int64_t P) {
+          return dmp::bn_maxpool_supported((int)C, (int)K, (int)S, (int)P);
+        },
+        "fused BN + ReLU + max pool applies to (C, K, S, P)");
+  m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd,
+        "BN + ReLU + max pool forward, finalize folded in -> (y, idx, stats)", py::arg("x"),
+        py::arg("part"), py::arg("have_partials"), py::arg("gamma"), py::arg("beta"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
+        py::arg("zero_buf"), py::arg("K"), py::arg("S"), py::arg("P"));
+  m.def("maxpool_bn_bwd", &maxpool_bn_bwd, "backward of bn_relu_maxpool_fwd -> dx", py::arg("x"),
+        py::arg("dp"), py::arg("idx"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("slots"), py::arg("zero_buf"), py::arg("K"), py::arg("S"),
+        py::arg("P"));
   m.def("bn_fwd", &bn_fwd, "NHWC batchnorm(+residual)(+relu) forward", py::arg("x"),
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("training"),

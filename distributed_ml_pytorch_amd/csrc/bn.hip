@@ -467,16 +467,19 @@ __device__ __forceinline__ void slice_zero(float* __restrict__ zb, int C, int cs
     zb[(long long)r * C + cs0 + threadIdx.x] = 0.f;
 }
 
-template <int CS, bool RELU, bool RES, bool MASK>
-__global__ void __launch_bounds__(256) bn_apply_fold_kernel(
-    const u16* __restrict__ x, const u16* __restrict__ res, const float* __restrict__ part,
-    float* __restrict__ zero_buf, const float* __restrict__ gamma, const float* __restrict__ beta,
-    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
-    float* __restrict__ stats, u16* __restrict__ y, uint8_t* __restrict__ mask, long long M,
-    int C) {
-  __shared__ float lS[CS], lQ[CS];
+// Forward prologue of a folded apply block: the slice's scale / shift into lS /
+// lQ (M = the statistics' row count); block 0 publishes stats and the running
+// statistics.  Ends with a barrier.
+template <int CS>
+__device__ __forceinline__ void fold_fwd_coefs(const float* __restrict__ part,
+                                               float* __restrict__ zero_buf,
+                                               const float* __restrict__ gamma,
+                                               const float* __restrict__ beta,
+                                               float* __restrict__ running_mean,
+                                               float* __restrict__ running_var, float momentum,
+                                               float eps, float* __restrict__ stats, long long M,
+                                               int C, int cs0, float* lS, float* lQ) {
   const int t = threadIdx.x;
-  const int cs0 = blockIdx.y * CS;
   slice_slot_sums<CS>(part, C, cs0, lS, lQ);
   if (t < CS) {   // same thread wrote lS[t] / lQ[t]: no barrier needed before the reuse
     const int c = cs0 + t;
@@ -501,6 +504,20 @@ __global__ void __launch_bounds__(256) bn_apply_fold_kernel(
   }
   slice_zero<CS>(zero_buf, C, cs0);
   __syncthreads();
+}
+
+template <int CS, bool RELU, bool RES, bool MASK>
+__global__ void __launch_bounds__(256) bn_apply_fold_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ res, const float* __restrict__ part,
+    float* __restrict__ zero_buf, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
+    float* __restrict__ stats, u16* __restrict__ y, uint8_t* __restrict__ mask, long long M,
+    int C) {
+  __shared__ float lS[CS], lQ[CS];
+  const int t = threadIdx.x;
+  const int cs0 = blockIdx.y * CS;
+  fold_fwd_coefs<CS>(part, zero_buf, gamma, beta, running_mean, running_var, momentum, eps, stats,
+                     M, C, cs0, lS, lQ);
   constexpr int TPR = CS / 8, RPI = 256 / TPR;
   const int cg = t % TPR, r0 = t / TPR;
   float sc[8], sh[8];
@@ -553,16 +570,17 @@ __global__ void __launch_bounds__(256) bn_apply_fold_kernel(
   }
 }
 
-template <int CS, int RELU, bool WRITE_DRES>
-__global__ void __launch_bounds__(256) bn_bwd_apply_fold_kernel(
-    const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
-    const uint8_t* __restrict__ mask, const float* __restrict__ part,
-    float* __restrict__ zero_buf, const float* __restrict__ gamma,
-    const float* __restrict__ stats, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    u16* __restrict__ dx, u16* __restrict__ dres, long long M, int C) {
-  __shared__ float lS[CS], lQ[CS], lC[CS];
+// Backward prologue of a folded apply block: dx = lS * dz + lC * x + lQ for the
+// slice; block 0 accumulates dgamma / dbeta.  Ends with a barrier.
+template <int CS>
+__device__ __forceinline__ void fold_bwd_coefs(const float* __restrict__ part,
+                                               float* __restrict__ zero_buf,
+                                               const float* __restrict__ gamma,
+                                               const float* __restrict__ stats,
+                                               float* __restrict__ dgamma,
+                                               float* __restrict__ dbeta, long long M, int C,
+                                               int cs0, float* lS, float* lQ, float* lC) {
   const int t = threadIdx.x;
-  const int cs0 = blockIdx.y * CS;
   slice_slot_sums<CS>(part, C, cs0, lS, lQ);
   if (t < CS) {
     const int c = cs0 + t;
@@ -582,6 +600,19 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fold_kernel(
   }
   slice_zero<CS>(zero_buf, C, cs0);
   __syncthreads();
+}
+
+template <int CS, int RELU, bool WRITE_DRES>
+__global__ void __launch_bounds__(256) bn_bwd_apply_fold_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
+    const uint8_t* __restrict__ mask, const float* __restrict__ part,
+    float* __restrict__ zero_buf, const float* __restrict__ gamma,
+    const float* __restrict__ stats, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    u16* __restrict__ dx, u16* __restrict__ dres, long long M, int C) {
+  __shared__ float lS[CS], lQ[CS], lC[CS];
+  const int t = threadIdx.x;
+  const int cs0 = blockIdx.y * CS;
+  fold_bwd_coefs<CS>(part, zero_buf, gamma, stats, dgamma, dbeta, M, C, cs0, lS, lQ, lC);
   constexpr int TPR = CS / 8, RPI = 256 / TPR;
   const int cg = t % TPR, r0 = t / TPR;
   const int cofs = cs0 + cg * 8;
@@ -740,6 +771,328 @@ void launch_bn_bwd_fold(const u16* x, const u16* dy, const u16* y, const float* 
   else { DMP_FOLD_BV(8) }
 #undef DMP_FOLD_BV
 #undef DMP_FOLD_B
+}
+
+// -------- BatchNorm + ReLU + max pool, fused (the ImageNet ResNet stem) --------
+// conv7x7/s2 -> BN -> ReLU -> maxpool 3x3/s2/p1 (ResNet-50 bs128: a 205 MB
+// 112x112x64 activation).  Unfused, the BN apply wrote y (205 MB) for the pool
+// to read back, and the backward materialised dy = maxpool_bwd(dp) (205 MB)
+// for both BN backward passes to read: bn_apply 94 + maxpool 110 us forward,
+// maxpool_bwd 137 + reduce 92 + apply 116 us backward
+// (profiles/resnet50_step_dispatches_r4.txt).  Fused:
+//   forward   each pooled output applies the folded scale / shift + ReLU to its
+//             K x K taps of the raw conv output x and keeps the max and its tap;
+//             y never exists.
+//   backward  both BN passes gather dz(h, w) = sum of dp over the windows whose
+//             saved argmax is this tap -- dp and the uint8 taps are 1/4 and 1/8
+//             of x's bytes -- so dy is never written or read.
+// Bit-identical to the unfused ops: the tap values are rounded to bf16 before
+// the compare (the pool saw stored bf16 y), the gathered dz is rounded to bf16
+// (the unfused dy was stored), and a window whose max is 0 records tap 255 (the
+// pool's relu_in rule: relu' = 0 everywhere in it).  The ReLU mask of the BN
+// backward is implied: only a tap with y = max > 0 can receive gradient.
+// 32-bit-offset buffer loads (one VGPR per address instead of a 64-bit pointer;
+// an out-of-range offset returns zeros without a memory access): the fused pool
+// kernels keep 10-20 loads per lane in flight
+typedef unsigned int bnu32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int bnu32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned kBnOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bn_rsrc(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ bf16x8 bn_ld16(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
+__device__ __forceinline__ uint2 bn_ld8(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  const bnu32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+  return make_uint2(v.x, v.y);
+}
+
+// One un-pooled row's gather, split into a load phase (every load of U rows is
+// issued before any is consumed: one row per trip kept ~9 loads in flight per
+// lane and ran the backward pair at 132 + 149 us) and a reduce phase.
+template <int K, int S, int P>
+struct PoolGather {
+  static constexpr int KS = (K + S - 1) / S;   // pooled outputs per input row / column, at most
+  bf16x8 gv[KS][KS];
+  uint2 iv[KS][KS];
+  bf16x8 xr;
+  int h, w, hlo, hhi, wlo, whi;
+
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rsx, __amdgpu_buffer_rsrc_t rsdp,
+                                       __amdgpu_buffer_rsrc_t rsidx, int row, bool live, int H,
+                                       int W, int C, int Ho, int Wo, int cofs) {
+    w = row % W;
+    const int r = row / W;
+    h = r % H;
+    const int n = r / H;
+    hlo = max(0, (h + P - K + S) / S);
+    hhi = live ? min(Ho - 1, (h + P) / S) : -1;     // a dead row gathers nothing
+    wlo = max(0, (w + P - K + S) / S);
+    whi = min(Wo - 1, (w + P) / S);
+    xr = bn_ld16(rsx, live ? 2u * (unsigned)(row * C + cofs) : kBnOOB);
+#pragma unroll
+    for (int a = 0; a < KS; ++a)
+#pragma unroll
+      for (int b = 0; b < KS; ++b) {
+        const bool ok = hlo + a <= hhi && wlo + b <= whi;
+        const unsigned o = (unsigned)(((n * Ho + hlo + a) * Wo + wlo + b) * C + cofs);
+        gv[a][b] = bn_ld16(rsdp, ok ? 2u * o : kBnOOB);
+        iv[a][b] = bn_ld8(rsidx, ok ? o : kBnOOB);
+      }
+  }
+
+  // dz of the 8 channels (rounded to bf16 as the unfused pool's stored dy) and x
+  __device__ __forceinline__ void reduce(float g[8], float xv[8]) const {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < KS; ++a)
+#pragma unroll
+      for (int b = 0; b < KS; ++b) {
+        const int ho = hlo + a, wo = wlo + b;
+        if (ho <= hhi && wo <= whi) {
+          const u32 me = (u32)((h - (ho * S - P)) * K + (w - (wo * S - P)));
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const u32 bi = ((k < 4 ? iv[a][b].x : iv[a][b].y) >> (8 * (k & 3))) & 0xffu;
+            if (bi == me) acc[k] += bf2f(gv[a][b].v[k]);
+          }
+        }
+      }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      g[k] = bf2f(f2bf(acc[k]));
+      xv[k] = bf2f(xr.v[k]);
+    }
+  }
+};
+
+constexpr int kPoolFwdU = 2, kPoolPartU = 2, kPoolApplyU = 2;   // rows per trip
+
+template <int CS, int K, int S, int P>
+__global__ void __launch_bounds__(256) bn_relu_maxpool_fold_kernel(
+    const u16* __restrict__ x, const float* __restrict__ part, float* __restrict__ zero_buf,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
+    float* __restrict__ stats, u16* __restrict__ y, uint8_t* __restrict__ idx, int N, int H,
+    int W, int C, int Ho, int Wo) {
+  __shared__ float lS[CS], lQ[CS];
+  const int t = threadIdx.x;
+  const int cs0 = blockIdx.y * CS;
+  fold_fwd_coefs<CS>(part, zero_buf, gamma, beta, running_mean, running_var, momentum, eps, stats,
+                     (long long)N * H * W, C, cs0, lS, lQ);
+  constexpr int TPR = CS / 8, RPI = 256 / TPR, U = kPoolFwdU;
+  const int cg = t % TPR, r0 = t / TPR;
+  const int cofs = cs0 + cg * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sc[k] = lS[cg * 8 + k]; sh[k] = lQ[cg * 8 + k]; }
+  const int Mo = N * Ho * Wo;
+  const __amdgpu_buffer_rsrc_t rsx = bn_rsrc(x, 2LL * N * H * W * C);
+  const int rows_per_blk = (Mo + gridDim.x - 1) / gridDim.x;
+  const int start = blockIdx.x * rows_per_blk;
+  const int end = min(Mo, start + rows_per_blk);
+  for (int row0 = start + r0; row0 < end; row0 += U * RPI) {
+    bf16x8 v[U][K][K];                // every tap of U pooled rows in flight together
+    int h0[U], w0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = row0 + u * RPI;
+      const int wo = row % Wo, r = row / Wo;
+      const int ho = r % Ho, n = r / Ho;
+      h0[u] = row < end ? ho * S - P : -K - 1;        // a dead row loads no tap
+      w0[u] = wo * S - P;
+#pragma unroll
+      for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          v[u][i][j] = bn_ld16(
+              rsx, (unsigned)(h0[u] + i) < (unsigned)H && (unsigned)(w0[u] + j) < (unsigned)W
+                       ? 2u * (unsigned)(((n * H + h0[u] + i) * W + w0[u] + j) * C + cofs)
+                       : kBnOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = row0 + u * RPI;
+      if (row >= end) break;
+      float best[8];
+      u32 bi[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+#pragma unroll
+      for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          if ((unsigned)(h0[u] + i) < (unsigned)H && (unsigned)(w0[u] + j) < (unsigned)W) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float f = bf2f(f2bf(fmaxf(bn_pre(bf2f(v[u][i][j].v[k]), sc[k], sh[k]), 0.f)));
+              if (f > best[k]) { best[k] = f; bi[k] = (u32)(i * K + j); }
+            }
+          }
+        }
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o.v[k] = f2bf(best[k]);
+        if (!(best[k] > 0.f)) bi[k] = 255;
+      }
+      const long long off = (long long)row * C + cofs;
+      *reinterpret_cast<bf16x8*>(y + off) = o;
+      uint2 packed;
+      packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+      packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+      *reinterpret_cast<uint2*>(idx + off) = packed;
+    }
+  }
+}
+
+// backward reduce pass: s += dz, q += dz * xhat over the un-pooled rows, dz gathered
+template <int K, int S, int P>
+__global__ void __launch_bounds__(256) maxpool_bn_partial_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ dp, const uint8_t* __restrict__ idx,
+    const float* __restrict__ stats, float* __restrict__ part, int N, int H, int W, int C, int Ho,
+    int Wo) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int U = kPoolPartU;
+  const int tpr = C >> 3;
+  const int rpi = 256 / tpr;
+  const int t = threadIdx.x;
+  const int cg = t % tpr, r0 = t / tpr;
+  const int M = N * H * W;
+  const int rows_per_blk = (M + gridDim.x - 1) / gridDim.x;
+  const int start = blockIdx.x * rows_per_blk;
+  const int end = min(M, start + rows_per_blk);
+  const __amdgpu_buffer_rsrc_t rsx = bn_rsrc(x, 2LL * M * C);
+  const __amdgpu_buffer_rsrc_t rsdp = bn_rsrc(dp, 2LL * N * Ho * Wo * C);
+  const __amdgpu_buffer_rsrc_t rsidx = bn_rsrc(idx, (long long)N * Ho * Wo * C);
+  float s[8], q[8], mean[8], inv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s[k] = 0.f;
+    q[k] = 0.f;
+    mean[k] = stats[cg * 8 + k];
+    inv[k] = stats[C + cg * 8 + k];
+  }
+  if (r0 < rpi) {
+    for (int row0 = start + r0; row0 < end; row0 += U * rpi) {
+      PoolGather<K, S, P> pg[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = row0 + u * rpi;
+        pg[u].load(rsx, rsdp, rsidx, row, row < end, H, W, C, Ho, Wo, cg * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (row0 + u * rpi >= end) break;
+        float xv[8], g[8];
+        pg[u].reduce(g, xv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] += g[k] * (xv[k] - mean[k]) * inv[k]; }
+      }
+    }
+  }
+  float* ls = smem;            // [rpi][C]
+  float* lq = smem + rpi * C;  // [rpi][C]
+  if (r0 < rpi) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { ls[r0 * C + cg * 8 + k] = s[k]; lq[r0 * C + cg * 8 + k] = q[k]; }
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) { a += ls[rr * C + c]; b += lq[rr * C + c]; }
+    const int slot = blockIdx.x % kBnSlots;
+    atomicAdd(part + (long long)slot * C + c, a);
+    atomicAdd(part + (long long)(kBnSlots + slot) * C + c, b);
+  }
+}
+
+template <int CS, int K, int S, int P>
+__global__ void __launch_bounds__(256) maxpool_bn_bwd_apply_fold_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ dp, const uint8_t* __restrict__ idx,
+    const float* __restrict__ part, float* __restrict__ zero_buf, const float* __restrict__ gamma,
+    const float* __restrict__ stats, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    u16* __restrict__ dx, int N, int H, int W, int C, int Ho, int Wo) {
+  __shared__ float lS[CS], lQ[CS], lC[CS];
+  const int t = threadIdx.x;
+  const int cs0 = blockIdx.y * CS;
+  const int M = N * H * W;
+  fold_bwd_coefs<CS>(part, zero_buf, gamma, stats, dgamma, dbeta, M, C, cs0, lS, lQ, lC);
+  constexpr int TPR = CS / 8, RPI = 256 / TPR, U = kPoolApplyU;
+  const int cg = t % TPR, r0 = t / TPR;
+  const int cofs = cs0 + cg * 8;
+  float ka[8], kb[8], kc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    ka[k] = lS[cg * 8 + k];
+    kb[k] = lQ[cg * 8 + k];
+    kc[k] = lC[cg * 8 + k];
+  }
+  const __amdgpu_buffer_rsrc_t rsx = bn_rsrc(x, 2LL * M * C);
+  const __amdgpu_buffer_rsrc_t rsdp = bn_rsrc(dp, 2LL * N * Ho * Wo * C);
+  const __amdgpu_buffer_rsrc_t rsidx = bn_rsrc(idx, (long long)N * Ho * Wo * C);
+  const int rows_per_blk = (M + gridDim.x - 1) / gridDim.x;
+  const int start = blockIdx.x * rows_per_blk;
+  const int end = min(M, start + rows_per_blk);
+  for (int row0 = start + r0; row0 < end; row0 += U * RPI) {
+    PoolGather<K, S, P> pg[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = row0 + u * RPI;
+      pg[u].load(rsx, rsdp, rsidx, row, row < end, H, W, C, Ho, Wo, cofs);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = row0 + u * RPI;
+      if (row >= end) break;
+      float xv[8], g[8], o[8];
+      pg[u].reduce(g, xv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = ka[k] * g[k] + kc[k] * xv[k] + kb[k];
+      store8(dx + (long long)row * C + cofs, o);
+    }
+  }
+}
+
+int maxpool_out(int H, int K, int S, int P);   // pool.hip
+
+bool bn_maxpool_supported(int C, int K, int S, int P) {
+  return C % 64 == 0 && C <= 2048 && K == 3 && S == 2 && P == 1;
+}
+
+void launch_bn_relu_maxpool_fold(const u16* x, u16* y, uint8_t* idx, const float* gamma,
+                                 const float* beta, float* running_mean, float* running_var,
+                                 float* stats, float* part, float* zero_buf, int N, int H, int W,
+                                 int C, float momentum, float eps, bool have_partials,
+                                 hipStream_t s) {
+  const long long M = (long long)N * H * W;
+  if (!have_partials) {
+    const int G = bn_num_partials(M, C);
+    const size_t lds = (size_t)(256 / (C / 8)) * C * 2 * sizeof(float);
+    hipLaunchKernelGGL((bn_partial_kernel<0, 0>), dim3(G), dim3(256), lds, s, x, nullptr,
+                       nullptr, nullptr, nullptr, part, M, C);
+  }
+  const int Ho = maxpool_out(H, 3, 2, 1), Wo = maxpool_out(W, 3, 2, 1);
+  const dim3 grid = fold_grid((long long)N * Ho * Wo, C, 64);
+  hipLaunchKernelGGL((bn_relu_maxpool_fold_kernel<64, 3, 2, 1>), grid, dim3(256), 0, s, x, part,
+                     zero_buf, gamma, beta, running_mean, running_var, momentum, eps, stats, y, idx,
+                     N, H, W, C, Ho, Wo);
+}
+
+void launch_maxpool_bn_bwd_fold(const u16* x, const u16* dp, const uint8_t* idx,
+                                const float* gamma, const float* stats, float* dgamma,
+                                float* dbeta, float* part, float* zero_buf, u16* dx, int N, int H,
+                                int W, int C, hipStream_t s) {
+  const long long M = (long long)N * H * W;
+  const int Ho = maxpool_out(H, 3, 2, 1), Wo = maxpool_out(W, 3, 2, 1);
+  const int G = bn_num_partials(M, C);
+  const size_t lds = (size_t)(256 / (C / 8)) * C * 2 * sizeof(float);
+  hipLaunchKernelGGL((maxpool_bn_partial_kernel<3, 2, 1>), dim3(G), dim3(256), lds, s, x, dp, idx,
+                     stats, part, N, H, W, C, Ho, Wo);
+  hipLaunchKernelGGL((maxpool_bn_bwd_apply_fold_kernel<64, 3, 2, 1>), fold_grid(M, C, 64),
+                     dim3(256), 0, s, x, dp, idx, part, zero_buf, gamma, stats, dgamma, dbeta, dx,
+                     N, H, W, C, Ho, Wo);
 }
 
 }  // namespace dmp

@@ -30,6 +30,7 @@ namespace {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr unsigned kOOBs = 0x80000000u;
 constexpr int kSCO = 64, kSK = 256;   // output channels, packed reduction length
@@ -253,6 +254,14 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const u16* __restrict__ x
       s_sq[j][r] = 0.f;
       bj[j][r] = bias != nullptr ? bias[j * 16 + 4 * kg + r] : 0.f;
     }
+  // The D fragments (8 B per lane: a store instruction wrote 16 pixels x 32 B)
+  // go through a wave-private LDS tile and leave as whole 128-B pixel rows,
+  // 16 B per lane, 8 rows per instruction (LDS ops of one wave complete in
+  // order).  DMP_STEM_ROWSTORE=0 at build time: the direct fragment stores.
+#ifndef DMP_STEM_ROWSTORE
+#define DMP_STEM_ROWSTORE 1
+#endif
+  __shared__ __attribute__((aligned(16))) u16 stg[NW][16][kSCO + 8];
   auto epilogue = [&](int k) {
     const int t = tile_of(k);
     const int b = t / tpi, oh0 = (t - b * tpi) * NW;
@@ -276,7 +285,19 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const u16* __restrict__ x
           }
         }
         const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
-        __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, rowoff + 2u * n, 0, 0);
+        if constexpr (DMP_STEM_ROWSTORE)
+          *reinterpret_cast<u32x2_t*>(&stg[wid][l16][n]) = packed;
+        else
+          __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, rowoff + 2u * n, 0, 0);
+      }
+      if constexpr (DMP_STEM_ROWSTORE) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int pr = hh * 8 + (lane >> 3), ck = lane & 7;
+          const u32x4_t v = *reinterpret_cast<const u32x4_t*>(&stg[wid][pr][ck * 8]);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              v, rsY, 2u * (unsigned)((mrow + i * 16 + pr) * kSCO + ck * 8), 0, 0);
+        }
       }
     }
   };
@@ -493,8 +514,13 @@ template <typename K>
 void allow_lds160(K kernel) {
   static bool done = false;
   if (!done) {
+    // the dynamic cap excludes the kernel's static LDS (stem_fwd's store tile)
+    hipFuncAttributes fa{};
+    const int stat = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel)) == hipSuccess
+                         ? (int)fa.sharedSizeBytes
+                         : 0;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - stat);
     done = true;
   }
 }

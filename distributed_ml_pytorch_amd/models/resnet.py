@@ -23,6 +23,7 @@ import torch.nn as nn
 
 from ..ops import layers as L
 from ..ops.eval_fold import conv_bn, fold_enabled
+from ..ops.functional import bn_relu_maxpool, bn_relu_maxpool_ok
 from ..ops.linear import gap_linear, gap_linear_ok
 
 
@@ -169,9 +170,15 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         h = conv_bn(x, self.conv1, self.bn1) if fold_enabled(x, self) else None
+        pooled = False
         if h is None:
-            h = self.bn1(self.conv1(x))
-        if self.pool is not None:
+            h = self.conv1(x)
+            pk = (self.pool.kernel_size, self.pool.stride, self.pool.padding) if self.pool else None
+            if pk is not None and bn_relu_maxpool_ok(h, self.bn1, *pk):
+                h, pooled = bn_relu_maxpool(h, self.bn1, *pk), True   # BN + ReLU + pool fused
+            else:
+                h = self.bn1(h)
+        if self.pool is not None and not pooled:
             h = self.pool(h)
         h = self.layer4(self.layer3(self.layer2(self.layer1(h))))
         if gap_linear_ok(h, self.linear):

@@ -433,6 +433,76 @@ def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0,
     return F.max_pool2d(x, kernel_size, stride, padding)
 
 
+# BatchNorm + ReLU + max pool in one kernel each way (csrc/bn.hip: the pool reads
+# the raw conv output and applies the BN itself; the BN backward gathers its dz
+# from the pooled gradient): the ImageNet ResNet stem.  DMP_BN_POOL_FUSE=0: the
+# unfused BN apply + max pool pair.
+_BN_POOL_FUSE = os.environ.get("DMP_BN_POOL_FUSE", "1") != "0"
+
+
+class _BNReLUPool(Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, momentum, eps, k, s, p, part,
+                slots):
+        x = x.contiguous(memory_format=CL)
+        C = x.shape[1]
+        bslots = slots[1] if slots is not None else None
+        src = part if part is not None else _fresh_slots(
+            slots[0] if slots is not None else None, C, x.device)
+        y, idx, stats = native().bn_relu_maxpool_fwd(
+            x, src, part is not None, gamma, beta, running_mean, running_var, float(momentum),
+            float(eps), bslots, k, s, p)
+        mark_slots(src, True)              # read here, zeroed by the backward apply
+        if bslots is not None:
+            mark_slots(bslots, False)      # zeroed by this apply
+        ctx.fpart, ctx.bslots, ctx.meta = src, bslots, (k, s, p)
+        ctx.gamma, ctx.beta = gamma, beta
+        ctx.save_for_backward(x, idx, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dp):
+        x, idx, stats = ctx.saved_tensors
+        gamma, beta = ctx.gamma, ctx.beta
+        dg_arena, db_arena = _arena_grad(gamma), _arena_grad(beta)
+        need_g = gamma is not None and ctx.needs_input_grad[1]
+        need_b = beta is not None and ctx.needs_input_grad[2]
+        dg = dg_arena if dg_arena is not None else (torch.zeros_like(gamma) if need_g else None)
+        db = db_arena if db_arena is not None else (torch.zeros_like(beta) if need_b else None)
+        bs = _fresh_slots(ctx.bslots, x.shape[1], x.device)
+        k, s, p = ctx.meta
+        dx = native().maxpool_bn_bwd(x, dp, idx, gamma, stats, dg, db, bs, ctx.fpart, k, s, p)
+        mark_slots(bs, True)
+        mark_slots(ctx.fpart, False)
+        ctx.fpart = None
+        if dg_arena is not None or db_arena is not None:
+            _notify(gamma, beta)
+        ret_g = None if (dg_arena is not None or not need_g) else dg
+        ret_b = None if (db_arena is not None or not need_b) else db
+        return dx, ret_g, ret_b, None, None, None, None, None, None, None, None, None
+
+
+def bn_relu_maxpool_ok(x, bn, k: int, s: int, p: int) -> bool:
+    """The fused training path applies: a bf16 GPU NHWC activation feeding a
+    ReLU BatchNorm in batch-statistics mode, then a 3x3/s2/p1 max pool."""
+    return bool(_BN_POOL_FUSE and _BN_FOLD and _BN_BWD_FUSE in ("0", False) and x.is_cuda
+                and x.dtype == torch.bfloat16 and x.dim() == 4 and bn.training
+                and getattr(bn, "relu", False) and 2 * x.numel() < 2 ** 31
+                and native().bn_maxpool_supported(x.shape[1], k, s, p))
+
+
+def bn_relu_maxpool(x, bn, k: int, s: int, p: int):
+    """``max_pool2d(relu(bn(x)), k, s, p)`` in one fused kernel pair (see
+    ``bn_relu_maxpool_ok``); ``bn`` is an ``ops.layers.BatchNorm2d``."""
+    part = getattr(x, "_dmp_bn_part", None)
+    y = _BNReLUPool.apply(
+        x, bn.weight, bn.bias, bn.running_mean if bn.track_running_stats else None,
+        bn.running_var if bn.track_running_stats else None,
+        0.1 if bn.momentum is None else bn.momentum, bn.eps, int(k), int(s), int(p), part,
+        bn._slots(x))
+    return set_nonneg(y)
+
+
 # ----------------------------------------------------------------------- ReLU
 class _ReLU(Function):
     """Standalone ReLU (where no producing GEMM / conv epilogue can take it):

@@ -272,6 +272,68 @@ def test_max_pool(shape, k, st, pd):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 16, 16), (2, 64, 15, 17), (3, 128, 12, 9),
+                                   (2, 64, 112, 112)])
+def test_bn_relu_maxpool_fused(shape, monkeypatch):
+    """Fused BN + ReLU + max pool 3x3/s2/p1 (csrc/bn.hip, the ImageNet stem):
+    pooled output bit-identical to the unfused BN apply + max pool, gradients and
+    running statistics against both the unfused kernels and fp32 PyTorch."""
+    from distributed_ml_pytorch_amd.ops import functional as DF
+    from distributed_ml_pytorch_amd.ops import layers as L
+
+    torch.manual_seed(1)
+    C = shape[1]
+    x0 = _bf(torch.randn(shape, device="cuda") * 2 + 0.3).contiguous(memory_format=CL)
+    dp = _bf(torch.randn(shape[0], C, (shape[2] - 1) // 2 + 1, (shape[3] - 1) // 2 + 1,
+                         device="cuda")).float()
+
+    gw = torch.rand(C) + 0.5
+    gw[::7] *= -1                                  # negative scales: max != scale * max
+    gb = torch.randn(C) * 0.2
+
+    def make():
+        bn = L.BatchNorm2d(C, relu=True).cuda()
+        with torch.no_grad():
+            bn.weight.copy_(gw)
+            bn.bias.copy_(gb)
+        return bn
+
+    bn_f, bn_u = make(), make()
+    assert DF.bn_relu_maxpool_ok(x0, bn_f, 3, 2, 1)
+    xf = x0.clone().requires_grad_(True)
+    yf = DF.bn_relu_maxpool(xf, bn_f, 3, 2, 1)
+    (yf.float() * dp).sum().backward()
+
+    monkeypatch.setattr(DF, "_BN_POOL_FUSE", False)
+    assert not DF.bn_relu_maxpool_ok(x0, bn_u, 3, 2, 1)
+    xu = x0.clone().requires_grad_(True)
+    yu = DF.max_pool2d(bn_u(xu), 3, 2, 1)
+    (yu.float() * dp).sum().backward()
+
+    assert yf.shape == yu.shape and yf.is_contiguous(memory_format=CL)
+    assert torch.equal(yf, yu)
+    torch.testing.assert_close(bn_f.running_mean, bn_u.running_mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(bn_f.running_var, bn_u.running_var, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(xf.grad.float(), xu.grad.float(), rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(bn_f.weight.grad, bn_u.weight.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(bn_f.bias.grad, bn_u.bias.grad, rtol=1e-3, atol=1e-3)
+
+    # fp32 PyTorch reference
+    xr = x0.detach().float().requires_grad_(True)
+    g = make()
+    w = g.weight.detach().float().requires_grad_(True)
+    b = g.bias.detach().float().requires_grad_(True)
+    yr = F.max_pool2d(F.relu(F.batch_norm(xr, None, None, w, b, True, 0.1, 1e-5)), 3, 2, 1)
+    (yr * dp).sum().backward()
+    torch.testing.assert_close(yf.float(), yr, rtol=2e-2, atol=2e-2)
+    def rel(a, r):
+        return float((a.float() - r).norm() / (r.norm() + 1e-12))
+
+    assert rel(xf.grad, xr.grad) < 4e-2      # bf16 dz through a 25k-row BN reduction
+    assert rel(bn_f.weight.grad, w.grad) < 1e-2
+    assert rel(bn_f.bias.grad, b.grad) < 1e-2
+
+
 @pytest.mark.parametrize("mode", ["elem", "nchw", "nhwc"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_dropout_kernel(mode, dtype):

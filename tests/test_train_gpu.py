@@ -225,7 +225,7 @@ def test_rccl_sharded_ps_and_bucketed_allreduce_paths():
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("model", ["resnet18", "vit_tiny", "alexnet"])
+@pytest.mark.parametrize("model", ["resnet18", "vit_tiny", "alexnet", "resnet50"])
 def test_fp32_gpu_mode_is_an_oracle(model):
     """``--dtype fp32`` on the GPU: every op on PyTorch's fp32 kernels (no bf16
     shadow), same model / optimizer / PS.  Its first-step loss and parameters
@@ -247,7 +247,10 @@ def test_fp32_gpu_mode_is_an_oracle(model):
     assert all(v == v for v in l32)
     assert abs(l32[0] - l16[0]) < 0.05 * abs(l32[0]) + 0.02, (l32, l16)
     rel = float((p16 - p32).norm() / p32.norm())
-    assert rel < 1e-2, rel
+    # ResNet-50 from a random init is chaotic: stock autocast-bf16's gradients are
+    # ~1.3 off fp32 there (profiles/grad_parity_resnet50_r2.txt); 4 steps leave
+    # ~3.3 % parameter drift with or without the fused stem (DMP_BN_POOL_FUSE=0/1)
+    assert rel < (5e-2 if model == "resnet50" else 1e-2), rel
 
 
 def test_rccl_world1_device_async_shards_and_bf16_wire():
