@@ -676,10 +676,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fold_kernel(
 
 static int fold_cs(int C) { return C % 64 == 0 ? 64 : C % 32 == 0 ? 32 : C % 16 == 0 ? 16 : 8; }
 
-// row blocks per slice: >= 4 vectors per thread (DMP_BN_FOLD_VPT), at most 2048
-// blocks in all.  The per-block slot reduction is CS x 128 floats from L2; the
-// streaming pass needs the blocks: ResNet-18 bs512 3.77 ms/step unfolded, 4.15
-// at 32 vectors per thread, 3.66 at 8, 3.65 at 4 (profiles/bn_fold_stem3_r2.txt)
+// row blocks per slice: >= 4 vectors per thread (DMP_BN_FOLD_VPT), at most 1024
+// blocks in all (DMP_BN_FOLD_CAP).  The per-block slot reduction is CS x 128
+// floats from L2; the streaming pass needs the blocks: ResNet-18 bs512 3.77
+// ms/step unfolded, 4.15 at 32 vectors per thread, 3.66 at 8, 3.65 at 4
+// (profiles/bn_fold_stem3_r2.txt).  Cap 1024 vs 2048: ResNet-50 bs128 -0.14
+// ms/step, ResNet-18 unchanged; 512 and 4096 slower (profiles/bn_grid_knobs_r4.txt)
 static dim3 fold_grid(long long M, int C, int cs) {
   static const long long vpt = [] {
     const char* e = std::getenv("DMP_BN_FOLD_VPT");
@@ -687,7 +689,7 @@ static dim3 fold_grid(long long M, int C, int cs) {
   }();
   static const long long total = [] {
     const char* e = std::getenv("DMP_BN_FOLD_CAP");
-    return e ? std::max(1, std::atoi(e)) : 2048;
+    return e ? std::max(1, std::atoi(e)) : 1024;
   }();
   const long long nsl = C / cs;
   long long nrb = (M * (cs / 8) + 256 * vpt - 1) / (256 * vpt);
