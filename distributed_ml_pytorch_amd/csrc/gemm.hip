@@ -207,9 +207,12 @@ __device__ __forceinline__ bf16x8 frag(const u16* img, int r, int ks, int lane) 
 //     by which row 1's reads of k-tile t-1 completed (lgkmcnt(0) before it);
 //   * past the last k-tile the DMAs read zeros into slots nobody reads again, so
 //     every wave's vmcnt count stays uniform.
+// OCC > 0: at least OCC waves per SIMD (the register budget that lets two 8-wave
+// blocks share a CU, so one block's prologue / epilogue overlaps the other's MFMAs)
 template <int BM, int BN, int BK, int WM, int WN, int NS, bool AT, bool BT, int EPI, int KG = 1,
-          bool PP = false>
-__global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
+          bool PP = false, int OCC = 0>
+__global__ void __launch_bounds__(64 * WM * WN * KG)
+__attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) {
   constexpr int NWG = WM * WN, NW = NWG * KG;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "wave tiles of 16x16 MFMAs");
@@ -222,7 +225,11 @@ __global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
   constexpr int INS_MIN = SA::PW_MIN + SB::PW_MIN;   // DMAs every wave issues per stage
   static_assert(NS >= 2 && (NS - 2) * INS_MIN < 64, "pipeline depth");
   constexpr bool TRANS_OUT = EPI != EPI_ACC32;   // lane owns 4 consecutive n of one m
-  __shared__ __attribute__((aligned(16))) u16 lds[NS * STAGE];
+  // the two-blocks-per-CU tiles (OCC > 0) have a ring smaller than the padded
+  // epilogue tile: LDS sized for the larger of the two
+  constexpr int EPI_EL = NW * (BM / WM) * (BN / WN + 8);
+  constexpr int LDS_EL = (OCC > 0 && TRANS_OUT && EPI_EL > NS * STAGE) ? EPI_EL : NS * STAGE;
+  __shared__ __attribute__((aligned(16))) u16 lds[LDS_EL];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -359,9 +366,9 @@ __global__ void __launch_bounds__(64 * WM * WN * KG) gemm_kernel(GemmArgs g) {
       constexpr int WROWS = BM / WM, WCOLS = BN / WN, CPR = WCOLS / 8, RPI = 64 / CPR;
       // 16-B row padding when it fits, else (256x256 ring) an XOR swizzle of the
       // 16-B chunks by row & 7 (needs a multiple of 8 chunks per row)
-      constexpr bool SWZ = NW * WROWS * (WCOLS + 8) > NS * STAGE;
+      constexpr bool SWZ = NW * WROWS * (WCOLS + 8) > LDS_EL;
       constexpr int PITCH = SWZ ? WCOLS : WCOLS + 8;
-      static_assert(NW * WROWS * PITCH <= NS * STAGE, "epilogue tile fits in the ring's LDS");
+      static_assert(NW * WROWS * PITCH <= LDS_EL, "epilogue tile fits in the ring's LDS");
       static_assert(!SWZ || CPR % 8 == 0, "swizzled epilogue tile needs 8k chunks per row");
       auto pchunk = [](int row, int c) { return SWZ ? (c ^ (row & 7)) : c; };
       constexpr int NR = (WROWS + RPI - 1) / RPI;   // row segments per lane
@@ -732,7 +739,7 @@ void launch_small(const GemmArgs& g, int splits, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ configs
-struct Cfg { int bm, bn, bk, wm, wn, ns, kg = 1, pp = 0; };
+struct Cfg { int bm, bn, bk, wm, wn, ns, kg = 1, pp = 0, occ = 0; };
 // LDS = ns * (bm + bn) * bk * 2 B.  Tile heights 160 / 192 exist for tile
 // counts: M = 12608 tokens x N = 768 is 150 tiles of 256x256 (59 % of 256 CUs)
 // but 237 of 160x256.  A k-strided (transposed) operand needs a tile side that
@@ -751,6 +758,10 @@ constexpr Cfg kCfgs[] = {
     {256, 256, 32, 2, 4, 4, 1, 1},   // 10: ping-pong k-loop (PP), 128 KiB, 8 waves of 128x64
     {128, 256, 32, 2, 4, 4, 1, 1},   // 11: PP, 96 KiB, 8 waves of 64x64
     {256, 128, 32, 2, 4, 4, 1, 1},   // 12: PP, 96 KiB, 8 waves of 128x32
+    // two 8-wave blocks per CU (<= 128 VGPRs): 13-15
+    {128, 256, 32, 2, 4, 2, 1, 0, 4},   // 13: 48 KiB, 8 waves of 64x64
+    {128, 256, 32, 2, 4, 3, 1, 0, 4},   // 14: 72 KiB, 8 waves of 64x64
+    {256, 128, 32, 4, 2, 2, 1, 0, 4},   // 15: 48 KiB, 8 waves of 64x64
 };
 // (4 waves of 128x128 per 256x256 / 192x256 tile, accumulators in AGPRs: 20-40 %
 // slower than the 8-wave tiles on every ViT shape -- profiles/gemm_vs_hipblaslt_r2.txt)
@@ -771,7 +782,7 @@ void launch_cfg(const GemmArgs& a, int splits, hipStream_t s) {
     const int tiles = ((g.M + c.bm - 1) / c.bm) * g.tiles_n;
     if constexpr (c.kg == 1 || EPI == EPI_ACC32)
       hipLaunchKernelGGL((gemm_kernel<c.bm, c.bn, c.bk, c.wm, c.wn, c.ns, AT, BT, EPI, c.kg,
-                                      c.pp != 0>),
+                                      c.pp != 0, c.occ>),
                          dim3((unsigned)tiles, (unsigned)splits), dim3(64 * c.wm * c.wn * c.kg), 0,
                          s, g);
     else
@@ -795,7 +806,10 @@ void launch_mode(int cfg, const GemmArgs& a, int splits, hipStream_t s) {
     case 9: launch_cfg<9, AT, BT, EPI>(a, splits, s); break;
     case 10: launch_cfg<10, AT, BT, EPI>(a, splits, s); break;
     case 11: launch_cfg<11, AT, BT, EPI>(a, splits, s); break;
-    default: launch_cfg<12, AT, BT, EPI>(a, splits, s); break;
+    case 12: launch_cfg<12, AT, BT, EPI>(a, splits, s); break;
+    case 13: launch_cfg<13, AT, BT, EPI>(a, splits, s); break;
+    case 14: launch_cfg<14, AT, BT, EPI>(a, splits, s); break;
+    default: launch_cfg<15, AT, BT, EPI>(a, splits, s); break;
   }
 }
 
