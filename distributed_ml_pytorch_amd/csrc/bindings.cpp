@@ -1618,20 +1618,21 @@ std::vector<Tensor> bn_relu_maxpool_fwd(Tensor x, Tensor part, bool have_partial
   auto mf = at::MemoryFormat::ChannelsLast;
   auto y = at::empty({N, C, Ho, Wo}, x.options().memory_format(mf));
   auto idx = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(mf));
+  auto xm = at::empty({N, C, Ho, Wo}, x.options().memory_format(mf));
   auto stats = at::empty({4, C}, fopt);
   dmp::launch_bn_relu_maxpool_fold(
       reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
-      idx.data_ptr<uint8_t>(), ptr_or_null<float>(gamma), ptr_or_null<float>(beta),
+      idx.data_ptr<uint8_t>(), reinterpret_cast<uint16_t*>(xm.data_ptr()), ptr_or_null<float>(gamma), ptr_or_null<float>(beta),
       ptr_or_null<float>(running_mean), ptr_or_null<float>(running_var), stats.data_ptr<float>(),
       part.data_ptr<float>(), zb, N, H, W, C, (float)momentum, (float)eps, have_partials,
       cur_stream());
-  return {y, idx, stats};
+  return {y, idx, stats, xm};
 }
 
 // backward of bn_relu_maxpool_fwd: dx of the raw conv output from the pooled
 // gradient; slots = the layer's backward slots (zero on entry), zero_buf = the
 // forward slot sums the forward read
-Tensor maxpool_bn_bwd(Tensor x, Tensor dp, Tensor idx, optional<Tensor> gamma, Tensor stats,
+Tensor maxpool_bn_bwd(Tensor x, Tensor dp, Tensor idx, Tensor xm, optional<Tensor> gamma, Tensor stats,
                       optional<Tensor> dgamma, optional<Tensor> dbeta, Tensor slots,
                       optional<Tensor> zero_buf, int64_t K, int64_t S, int64_t P) {
   check_nhwc_bf16(x, "x");
@@ -1648,6 +1649,8 @@ Tensor maxpool_bn_bwd(Tensor x, Tensor dp, Tensor idx, optional<Tensor> gamma, T
   TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.sizes() == dp.sizes() &&
                   idx.is_contiguous(mf),
               "maxpool_bn_bwd: idx mismatch");
+  check_nhwc_bf16(xm, "xm");
+  TORCH_CHECK(xm.sizes() == dp.sizes(), "maxpool_bn_bwd: xm mismatch");
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * C, "bad stats");
   for (auto* t : {&gamma, &dgamma, &dbeta}) {
     if (t->has_value()) {
@@ -1666,8 +1669,8 @@ Tensor maxpool_bn_bwd(Tensor x, Tensor dp, Tensor idx, optional<Tensor> gamma, T
   auto dx = at::empty_like(x);
   dmp::launch_maxpool_bn_bwd_fold(
       reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(dp.data_ptr()),
-      idx.data_ptr<uint8_t>(), ptr_or_null<float>(gamma), stats.data_ptr<float>(),
-      ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta), part.data_ptr<float>(), zb,
+      idx.data_ptr<uint8_t>(), reinterpret_cast<const uint16_t*>(xm.data_ptr()),
+      ptr_or_null<float>(gamma), stats.data_ptr<float>(), ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta), part.data_ptr<float>(), zb,
       reinterpret_cast<uint16_t*>(dx.data_ptr()), N, H, W, C, cur_stream());
   return dx;
 }
@@ -1750,12 +1753,13 @@ PYBIND11_MODULE(_native, m) {
         },
         "fused BN + ReLU + max pool applies to (C, K, S, P)");
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd,
-        "BN + ReLU + max pool forward, finalize folded in -> (y, idx, stats)", py::arg("x"),
+        "BN + ReLU + max pool forward, finalize folded in -> (y, idx, stats, x at the taps)",
+        py::arg("x"),
         py::arg("part"), py::arg("have_partials"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("zero_buf"), py::arg("K"), py::arg("S"), py::arg("P"));
   m.def("maxpool_bn_bwd", &maxpool_bn_bwd, "backward of bn_relu_maxpool_fwd -> dx", py::arg("x"),
-        py::arg("dp"), py::arg("idx"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
+        py::arg("dp"), py::arg("idx"), py::arg("xm"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("slots"), py::arg("zero_buf"), py::arg("K"), py::arg("S"),
         py::arg("P"));
   m.def("bn_fwd", &bn_fwd, "NHWC batchnorm(+residual)(+relu) forward", py::arg("x"),

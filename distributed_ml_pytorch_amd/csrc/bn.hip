@@ -682,7 +682,7 @@ static int fold_cs(int C) { return C % 64 == 0 ? 64 : C % 32 == 0 ? 32 : C % 16 
 // ms/step unfolded, 4.15 at 32 vectors per thread, 3.66 at 8, 3.65 at 4
 // (profiles/bn_fold_stem3_r2.txt).  Cap 1024 vs 2048: ResNet-50 bs128 -0.14
 // ms/step, ResNet-18 unchanged; 512 and 4096 slower (profiles/bn_grid_knobs_r4.txt)
-static dim3 fold_grid(long long M, int C, int cs) {
+static dim3 fold_grid(long long M, int C, int cs, long long cap_blocks = 0) {
   static const long long vpt = [] {
     const char* e = std::getenv("DMP_BN_FOLD_VPT");
     return e ? std::max(1, std::atoi(e)) : 4;
@@ -693,7 +693,7 @@ static dim3 fold_grid(long long M, int C, int cs) {
   }();
   const long long nsl = C / cs;
   long long nrb = (M * (cs / 8) + 256 * vpt - 1) / (256 * vpt);
-  const long long cap = std::max<long long>(1, total / nsl);
+  const long long cap = std::max<long long>(1, (cap_blocks > 0 ? cap_blocks : total) / nsl);
   nrb = std::max<long long>(1, std::min(nrb, std::min(cap, M)));
   return dim3((unsigned)nrb, (unsigned)nsl);
 }
@@ -785,14 +785,17 @@ void launch_bn_bwd_fold(const u16* x, const u16* dy, const u16* y, const float* 
 //   forward   each pooled output applies the folded scale / shift + ReLU to its
 //             K x K taps of the raw conv output x and keeps the max and its tap;
 //             y never exists.
-//   backward  both BN passes gather dz(h, w) = sum of dp over the windows whose
-//             saved argmax is this tap -- dp and the uint8 taps are 1/4 and 1/8
-//             of x's bytes -- so dy is never written or read.
-// Bit-identical to the unfused ops: the tap values are rounded to bf16 before
-// the compare (the pool saw stored bf16 y), the gathered dz is rounded to bf16
-// (the unfused dy was stored), and a window whose max is 0 records tap 255 (the
-// pool's relu_in rule: relu' = 0 everywhere in it).  The ReLU mask of the BN
-// backward is implied: only a tap with y = max > 0 can receive gradient.
+//   backward  the reduce runs over the pooled windows (dp, taps, xm); the apply
+//             gathers dz(h, w) = sum of dp over the windows whose saved argmax is
+//             this tap -- dp and the uint8 taps are 1/4 and 1/8 of x's bytes --
+//             so dy is never written or read.
+// The forward is bit-identical to the unfused ops: the tap values are rounded to
+// bf16 before the compare (the pool saw stored bf16 y), and a window whose max
+// is 0 records tap 255 (the pool's relu_in rule: relu' = 0 everywhere in it);
+// it also keeps the raw x of every window's winning tap (xm, pooled-sized) for
+// the backward reduce.  The backward apply's gathered dz is rounded to bf16 (the
+// unfused dy was stored).  The ReLU mask of the BN backward is implied: only a
+// tap with y = max > 0 can receive gradient.
 // 32-bit-offset buffer loads (one VGPR per address instead of a 64-bit pointer;
 // an out-of-range offset returns zeros without a memory access): the fused pool
 // kernels keep 10-20 loads per lane in flight
@@ -869,15 +872,15 @@ struct PoolGather {
   }
 };
 
-constexpr int kPoolFwdU = 2, kPoolPartU = 2, kPoolApplyU = 2;   // rows per trip
+constexpr int kPoolFwdU = 2, kPoolApplyU = 2;   // rows per trip
 
 template <int CS, int K, int S, int P>
 __global__ void __launch_bounds__(256) bn_relu_maxpool_fold_kernel(
     const u16* __restrict__ x, const float* __restrict__ part, float* __restrict__ zero_buf,
     const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
-    float* __restrict__ stats, u16* __restrict__ y, uint8_t* __restrict__ idx, int N, int H,
-    int W, int C, int Ho, int Wo) {
+    float* __restrict__ stats, u16* __restrict__ y, uint8_t* __restrict__ idx,
+    u16* __restrict__ xm, int N, int H, int W, int C, int Ho, int Wo) {
   __shared__ float lS[CS], lQ[CS];
   const int t = threadIdx.x;
   const int cs0 = blockIdx.y * CS;
@@ -919,8 +922,9 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_fold_kernel(
       if (row >= end) break;
       float best[8];
       u32 bi[8];
+      bf16x8 bx;                      // the raw x of the winning tap (backward reduce)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+      for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; bx.v[k] = 0; }
 #pragma unroll
       for (int i = 0; i < K; ++i)
 #pragma unroll
@@ -929,7 +933,11 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_fold_kernel(
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
               const float f = bf2f(f2bf(fmaxf(bn_pre(bf2f(v[u][i][j].v[k]), sc[k], sh[k]), 0.f)));
-              if (f > best[k]) { best[k] = f; bi[k] = (u32)(i * K + j); }
+              if (f > best[k]) {
+                best[k] = f;
+                bi[k] = (u32)(i * K + j);
+                bx.v[k] = v[u][i][j].v[k];
+              }
             }
           }
         }
@@ -937,10 +945,14 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_fold_kernel(
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         o.v[k] = f2bf(best[k]);
-        if (!(best[k] > 0.f)) bi[k] = 255;
+        if (!(best[k] > 0.f)) {
+          bi[k] = 255;
+          bx.v[k] = 0;
+        }
       }
       const long long off = (long long)row * C + cofs;
       *reinterpret_cast<bf16x8*>(y + off) = o;
+      *reinterpret_cast<bf16x8*>(xm + off) = bx;
       uint2 packed;
       packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
       packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
@@ -949,25 +961,26 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_fold_kernel(
   }
 }
 
-// backward reduce pass: s += dz, q += dz * xhat over the un-pooled rows, dz gathered
-template <int K, int S, int P>
-__global__ void __launch_bounds__(256) maxpool_bn_partial_kernel(
-    const u16* __restrict__ x, const u16* __restrict__ dp, const uint8_t* __restrict__ idx,
-    const float* __restrict__ stats, float* __restrict__ part, int N, int H, int W, int C, int Ho,
-    int Wo) {
+// backward reduce pass over the POOLED rows: dz is non-zero only at a window's
+// winning tap, so sum dz = sum over windows of dp and sum dz * xhat = sum over
+// windows of dp * xhat(x at the winning tap), the x the forward kept in xm
+// (reads dp, the taps and xm: 1/4 + 1/8 + 1/4 of x's bytes; the gathering form
+// over the un-pooled rows read x whole: ResNet-50 stem 94.0 -> 22.9 us, for
+// 75.5 -> 91.8 us in the forward that writes xm).  Windows sharing a winning tap
+// add their dp unrounded (the unfused path rounded the per-tap sum to bf16
+// first: this reduce is the more exact one).
+__global__ void __launch_bounds__(256) pooled_bn_partial_kernel(
+    const u16* __restrict__ dp, const uint8_t* __restrict__ idx, const u16* __restrict__ xm,
+    const float* __restrict__ stats, float* __restrict__ part, long long Mo, int C) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int U = kPoolPartU;
+  constexpr int U = 4;
   const int tpr = C >> 3;
   const int rpi = 256 / tpr;
   const int t = threadIdx.x;
   const int cg = t % tpr, r0 = t / tpr;
-  const int M = N * H * W;
-  const int rows_per_blk = (M + gridDim.x - 1) / gridDim.x;
-  const int start = blockIdx.x * rows_per_blk;
-  const int end = min(M, start + rows_per_blk);
-  const __amdgpu_buffer_rsrc_t rsx = bn_rsrc(x, 2LL * M * C);
-  const __amdgpu_buffer_rsrc_t rsdp = bn_rsrc(dp, 2LL * N * Ho * Wo * C);
-  const __amdgpu_buffer_rsrc_t rsidx = bn_rsrc(idx, (long long)N * Ho * Wo * C);
+  const long long rows_per_blk = (Mo + gridDim.x - 1) / gridDim.x;
+  const long long start = (long long)blockIdx.x * rows_per_blk;
+  const long long end = min(Mo, start + rows_per_blk);
   float s[8], q[8], mean[8], inv[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -976,22 +989,34 @@ __global__ void __launch_bounds__(256) maxpool_bn_partial_kernel(
     mean[k] = stats[cg * 8 + k];
     inv[k] = stats[C + cg * 8 + k];
   }
+  auto accum = [&](const bf16x8& g, const uint2& iv, const bf16x8& xr) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u32 bi = ((k < 4 ? iv.x : iv.y) >> (8 * (k & 3))) & 0xffu;
+      const float gv = bi != 255u ? bf2f(g.v[k]) : 0.f;
+      s[k] += gv;
+      q[k] += gv * (bf2f(xr.v[k]) - mean[k]) * inv[k];
+    }
+  };
   if (r0 < rpi) {
-    for (int row0 = start + r0; row0 < end; row0 += U * rpi) {
-      PoolGather<K, S, P> pg[U];
+    long long row = start + r0;
+    for (; row + (U - 1) * rpi < end; row += U * rpi) {
+      bf16x8 gr[U], xr[U];
+      uint2 iv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int row = row0 + u * rpi;
-        pg[u].load(rsx, rsdp, rsidx, row, row < end, H, W, C, Ho, Wo, cg * 8);
+        const long long off = (row + u * rpi) * C + cg * 8;
+        gr[u] = *reinterpret_cast<const bf16x8*>(dp + off);
+        iv[u] = *reinterpret_cast<const uint2*>(idx + off);
+        xr[u] = *reinterpret_cast<const bf16x8*>(xm + off);
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (row0 + u * rpi >= end) break;
-        float xv[8], g[8];
-        pg[u].reduce(g, xv);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] += g[k] * (xv[k] - mean[k]) * inv[k]; }
-      }
+      for (int u = 0; u < U; ++u) accum(gr[u], iv[u], xr[u]);
+    }
+    for (; row < end; row += rpi) {
+      const long long off = row * C + cg * 8;
+      accum(*reinterpret_cast<const bf16x8*>(dp + off), *reinterpret_cast<const uint2*>(idx + off),
+            *reinterpret_cast<const bf16x8*>(xm + off));
     }
   }
   float* ls = smem;            // [rpi][C]
@@ -1063,7 +1088,7 @@ bool bn_maxpool_supported(int C, int K, int S, int P) {
   return C % 64 == 0 && C <= 2048 && K == 3 && S == 2 && P == 1;
 }
 
-void launch_bn_relu_maxpool_fold(const u16* x, u16* y, uint8_t* idx, const float* gamma,
+void launch_bn_relu_maxpool_fold(const u16* x, u16* y, uint8_t* idx, u16* xm, const float* gamma,
                                  const float* beta, float* running_mean, float* running_var,
                                  float* stats, float* part, float* zero_buf, int N, int H, int W,
                                  int C, float momentum, float eps, bool have_partials,
@@ -1076,23 +1101,25 @@ void launch_bn_relu_maxpool_fold(const u16* x, u16* y, uint8_t* idx, const float
                        nullptr, nullptr, nullptr, part, M, C);
   }
   const int Ho = maxpool_out(H, 3, 2, 1), Wo = maxpool_out(W, 3, 2, 1);
-  const dim3 grid = fold_grid((long long)N * Ho * Wo, C, 64);
+  // the pool kernels keep 2048 blocks (1024: fwd 75 -> 94, bwd apply 109 -> 116 us)
+  const dim3 grid = fold_grid((long long)N * Ho * Wo, C, 64, 2048);
   hipLaunchKernelGGL((bn_relu_maxpool_fold_kernel<64, 3, 2, 1>), grid, dim3(256), 0, s, x, part,
                      zero_buf, gamma, beta, running_mean, running_var, momentum, eps, stats, y, idx,
-                     N, H, W, C, Ho, Wo);
+                     xm, N, H, W, C, Ho, Wo);
 }
 
 void launch_maxpool_bn_bwd_fold(const u16* x, const u16* dp, const uint8_t* idx,
-                                const float* gamma, const float* stats, float* dgamma,
+                                const u16* xm, const float* gamma, const float* stats, float* dgamma,
                                 float* dbeta, float* part, float* zero_buf, u16* dx, int N, int H,
                                 int W, int C, hipStream_t s) {
   const long long M = (long long)N * H * W;
   const int Ho = maxpool_out(H, 3, 2, 1), Wo = maxpool_out(W, 3, 2, 1);
-  const int G = bn_num_partials(M, C);
+  const long long Mo = (long long)N * Ho * Wo;
+  const int G = bn_num_partials(Mo, C);
   const size_t lds = (size_t)(256 / (C / 8)) * C * 2 * sizeof(float);
-  hipLaunchKernelGGL((maxpool_bn_partial_kernel<3, 2, 1>), dim3(G), dim3(256), lds, s, x, dp, idx,
-                     stats, part, N, H, W, C, Ho, Wo);
-  hipLaunchKernelGGL((maxpool_bn_bwd_apply_fold_kernel<64, 3, 2, 1>), fold_grid(M, C, 64),
+  hipLaunchKernelGGL(pooled_bn_partial_kernel, dim3(G), dim3(256), lds, s, dp, idx, xm, stats,
+                     part, Mo, C);
+  hipLaunchKernelGGL((maxpool_bn_bwd_apply_fold_kernel<64, 3, 2, 1>), fold_grid(M, C, 64, 2048),
                      dim3(256), 0, s, x, dp, idx, part, zero_buf, gamma, stats, dgamma, dbeta, dx,
                      N, H, W, C, Ho, Wo);
 }

@@ -61,13 +61,14 @@ void launch_bn_bwd_fold(const uint16_t* x, const uint16_t* dy, const uint16_t* y
                         int C, bool relu, hipStream_t s, const uint8_t* mask);
 // BN + ReLU + max pool 3x3/s2/p1 fused (ImageNet ResNet stem), folded finalize
 bool bn_maxpool_supported(int C, int K, int S, int P);
-void launch_bn_relu_maxpool_fold(const uint16_t* x, uint16_t* y, uint8_t* idx, const float* gamma,
+void launch_bn_relu_maxpool_fold(const uint16_t* x, uint16_t* y, uint8_t* idx, uint16_t* xm,
+                                 const float* gamma,
                                  const float* beta, float* running_mean, float* running_var,
                                  float* stats, float* part, float* zero_buf, int N, int H, int W,
                                  int C, float momentum, float eps, bool have_partials,
                                  hipStream_t s);
 void launch_maxpool_bn_bwd_fold(const uint16_t* x, const uint16_t* dp, const uint8_t* idx,
-                                const float* gamma, const float* stats, float* dgamma,
+                                const uint16_t* xm, const float* gamma, const float* stats, float* dgamma,
                                 float* dbeta, float* part, float* zero_buf, uint16_t* dx, int N,
                                 int H, int W, int C, hipStream_t s);
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const float* gamma,

@@ -449,7 +449,7 @@ class _BNReLUPool(Function):
         bslots = slots[1] if slots is not None else None
         src = part if part is not None else _fresh_slots(
             slots[0] if slots is not None else None, C, x.device)
-        y, idx, stats = native().bn_relu_maxpool_fwd(
+        y, idx, stats, xm = native().bn_relu_maxpool_fwd(
             x, src, part is not None, gamma, beta, running_mean, running_var, float(momentum),
             float(eps), bslots, k, s, p)
         mark_slots(src, True)              # read here, zeroed by the backward apply
@@ -457,12 +457,12 @@ class _BNReLUPool(Function):
             mark_slots(bslots, False)      # zeroed by this apply
         ctx.fpart, ctx.bslots, ctx.meta = src, bslots, (k, s, p)
         ctx.gamma, ctx.beta = gamma, beta
-        ctx.save_for_backward(x, idx, stats)
+        ctx.save_for_backward(x, idx, stats, xm)
         return y
 
     @staticmethod
     def backward(ctx, dp):
-        x, idx, stats = ctx.saved_tensors
+        x, idx, stats, xm = ctx.saved_tensors
         gamma, beta = ctx.gamma, ctx.beta
         dg_arena, db_arena = _arena_grad(gamma), _arena_grad(beta)
         need_g = gamma is not None and ctx.needs_input_grad[1]
@@ -471,7 +471,7 @@ class _BNReLUPool(Function):
         db = db_arena if db_arena is not None else (torch.zeros_like(beta) if need_b else None)
         bs = _fresh_slots(ctx.bslots, x.shape[1], x.device)
         k, s, p = ctx.meta
-        dx = native().maxpool_bn_bwd(x, dp, idx, gamma, stats, dg, db, bs, ctx.fpart, k, s, p)
+        dx = native().maxpool_bn_bwd(x, dp, idx, xm, gamma, stats, dg, db, bs, ctx.fpart, k, s, p)
         mark_slots(bs, True)
         mark_slots(ctx.fpart, False)
         ctx.fpart = None
