@@ -229,7 +229,9 @@ def _serve(a, cfg, ctx, sessions: int):
     return stats
 
 
-def _timed_steps(w, pool, steps, warmup, ctx):
+def _timed_steps(w, pool, steps, warmup, ctx, clock=None):
+    """Returns (elapsed s, last loss); ``clock`` (utils.metrics.ClockSampler)
+    samples sclk / power over exactly the timed window."""
     trace = os.environ.get("DMP_BENCH_LOSSES") == "1"
     seen = []
     for _ in range(warmup):
@@ -240,6 +242,8 @@ def _timed_steps(w, pool, steps, warmup, ctx):
     ctx.worker_barrier()
     _sync()
     w.timer.reset()
+    if clock is not None:
+        clock.start()
     t0 = time.perf_counter()
     for _ in range(steps):
         x, y = pool.next()
@@ -320,7 +324,8 @@ def time_to_target(a, cfg, ctx, mode=None):
             h_last = (hv[0], hv[1])
             eval_s += time.perf_counter() - te
             if not h_reached and h_last[1] >= a.ttl_heldout_acc:
-                h_reached, h_steps, h_time = True, steps, time.perf_counter() - t0
+                # training time only, like time_to_target_s (evaluations excluded)
+                h_reached, h_steps, h_time = True, steps, time.perf_counter() - t0 - eval_s
         if reached and h_reached:
             break
     _sync()
@@ -416,14 +421,12 @@ def run(a):
     from distributed_ml_pytorch_amd.runtime.trainer import TrainConfig, Worker
     from distributed_ml_pytorch_amd.utils.data import DeviceBatchPool
 
-    if a.mode == "asgd" and a.ps in ("central", "sharded_async") and \
-            int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        # a parameter server keeps one HIP stream per peer (parallel/links.py) plus
-        # RCCL's per-pair streams: at HIP's default 4 hardware queues two peers'
-        # transfers landed on one queue and ran back to back, from 8 queues on they
-        # overlapped (profiles/links_stream_creation_r4.txt).  HIP reads this once,
-        # at initialisation: set before the first torch.cuda call
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    from distributed_ml_pytorch_amd.runtime.dist import apply_hw_queue_policy
+
+    # every multi-rank topology (sharded workers, PS ranks, sync DP, and the
+    # central check that follows the line) runs several HIP streams per process:
+    # one queue policy for all of them, set before the first torch.cuda call
+    hw_queues = apply_hw_queue_policy(int(os.environ.get("WORLD_SIZE", "1")))
     cuda = torch.cuda.is_available()
     info = init_distributed(use_cuda=cuda)
     world = info.world_size
@@ -464,7 +467,11 @@ def run(a):
         graphed = w.enable_graph(bool(a.graph))
         pool = DeviceBatchPool(a.batch, w.input_shape, w.num_classes, w.device, n_batches=4,
                                dtype=w.compute_dtype, seed=info.rank)
-        elapsed, loss = _timed_steps(w, pool, a.steps, a.warmup, ctx)
+        from distributed_ml_pytorch_amd.utils.metrics import ClockSampler
+
+        clock = ClockSampler(w.device.index or 0) if w.device.type == "cuda" else None
+        elapsed, loss = _timed_steps(w, pool, a.steps, a.warmup, ctx, clock)
+        res["gpu_clock"] = getattr(w, "clock_reading", None)
         final_loss = float(loss.float().item())
         graphed = bool(getattr(w, "use_graph", False) and w.graph is not None)
         res["phases_host_ms"] = {k: v["mean_ms"] for k, v in w.timer.summary().items()}
@@ -521,7 +528,7 @@ def run(a):
     # onto rank 0: in the central topology rank 0 is the PS and trains nothing
     mine = None if ctx.is_ps else {"rank": info.rank, "hip_graph": bool(graphed),
                                    "phases_host_ms": res.get("phases_host_ms"),
-                                   "comm": res.get("comm")}
+                                   "comm": res.get("comm"), "gpu_clock": res.get("gpu_clock")}
     ranks = ctx.gather(mine)
     out = None
     if info.rank == 0:
@@ -576,7 +583,14 @@ def run(a):
         if first.get("comm"):
             out["comm_first_worker"] = first["comm"]
             out["comm_first_worker_rank"] = first["rank"]
+        # sclk / socket power sampled over the timed window (amdsmi), so box
+        # variance shows up beside the number; None where amdsmi is unavailable
+        out["gpu_clock_timed_window"] = first.get("gpu_clock")
+        out["gpu_max_hw_queues"] = hw_queues
         if len(workers) > 1:
+            clocks = [r["gpu_clock"]["sclk_mhz_mean"] for r in workers if r.get("gpu_clock")]
+            if clocks:
+                out["sclk_mhz_mean_min_over_workers"] = min(clocks)
             out["worker_hip_graph"] = [bool(r["hip_graph"]) for r in workers]
         if a.ref_batch and ref_elapsed > 0:
             out["reference_batch"] = {

@@ -12,6 +12,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "geom_guard.h"
 #include "launchers.h"
 
 namespace {
@@ -70,11 +71,20 @@ void asgd_fused_step(Tensor g, Tensor p, optional<Tensor> acc, optional<Tensor> 
                               cur_stream());
 }
 
-void ps_apply(Tensor shard, Tensor delta, optional<Tensor> mirror, double scale) {
+void ps_apply(Tensor shard, Tensor delta, optional<Tensor> mirror, double scale, bool atomic) {
   const int64_t n = shard.numel();
   TORCH_CHECK(n % 4 == 0, "shard length must be a multiple of 4");
   check_flat(shard, at::kFloat, n, "shard");
   if (mirror) check_flat(*mirror, at::kBFloat16, n, "mirror");
+  if (atomic) {
+    // concurrent applies on several streams: no mirror (it would race)
+    TORCH_CHECK(!mirror, "ps_apply: atomic applies take no bf16 mirror");
+    const bool bf = delta.scalar_type() == at::kBFloat16;
+    check_flat(delta, bf ? at::kBFloat16 : at::kFloat, n, "delta");
+    dmp::launch_ps_apply_atomic(shard.data_ptr<float>(), delta.data_ptr(), bf, n, (float)scale,
+                                cur_stream());
+    return;
+  }
   if (delta.scalar_type() == at::kFloat) {
     check_flat(delta, at::kFloat, n, "delta");
     dmp::launch_ps_apply_f32(shard.data_ptr<float>(), delta.data_ptr<float>(),
@@ -509,20 +519,20 @@ struct ConvGeom {
 
 ConvGeom conv_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad) {
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv: 4-D tensors expected");
-  ConvGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(0),
-             (int)w.size(2), (int)w.size(3), 0, 0};
-  TORCH_CHECK(w.size(1) == g.CI, "conv: weight/input channel mismatch");
+  TORCH_CHECK(w.size(1) == x.size(1), "conv: weight/input channel mismatch");
   TORCH_CHECK(stride >= 1 && pad >= 0, "conv: bad stride/pad");
-  g.OH = (g.H + 2 * (int)pad - g.R) / (int)stride + 1;
-  g.OW = (g.W + 2 * (int)pad - g.S) / (int)stride + 1;
-  TORCH_CHECK(g.OH > 0 && g.OW > 0, "conv: empty output");
+  const int64_t OH = dmp::guard::conv_out(x.size(2), pad, w.size(2), stride);
+  const int64_t OW = dmp::guard::conv_out(x.size(3), pad, w.size(3), stride);
+  TORCH_CHECK(OH > 0 && OW > 0, "conv: empty output");
+  // the kernels address operands with 32-bit byte offsets into buffer descriptors
+  // (checked on the 64-bit sizes, before anything is narrowed to int)
+  TORCH_CHECK(dmp::guard::conv_offsets_ok(x.size(0), x.size(2), x.size(3), x.size(1), OH, OW,
+                                          w.size(0), w.size(2), w.size(3)),
+              "native conv: tensor too large for 32-bit byte offsets");
+  ConvGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(0),
+             (int)w.size(2), (int)w.size(3), (int)OH, (int)OW};
   TORCH_CHECK(g.CI % 64 == 0 && g.CO % 64 == 0,
               "native conv needs CI % 64 == 0 and CO % 64 == 0 (got ", g.CI, ", ", g.CO, ")");
-  // the kernels address operands with 32-bit byte offsets into buffer descriptors
-  TORCH_CHECK((long long)g.B * g.H * g.W * g.CI < (1LL << 30) &&
-                  (long long)g.B * g.OH * g.OW * g.CO < (1LL << 30) &&
-                  (long long)g.CO * g.CI * g.R * g.S < (1LL << 30),
-              "native conv: tensor too large for 32-bit byte offsets");
   return g;
 }
 
@@ -797,17 +807,19 @@ struct SmallGeom {
 SmallGeom small_geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad) {
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "small conv: 4-D tensors expected");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, "small conv: x must be bf16 GPU");
-  SmallGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(0),
-              (int)w.size(2), (int)w.size(3), 0, 0};
-  TORCH_CHECK(w.size(1) == g.CI, "small conv: weight/input channel mismatch");
-  TORCH_CHECK(stride >= 1 && pad >= 0 && g.R <= 255 && g.S <= 255, "small conv: bad geometry");
-  TORCH_CHECK(g.CO % 64 == 0, "small conv: CO must be a multiple of 64");
-  TORCH_CHECK(g.R * g.S * g.CI <= dmp::conv_small_max_k(), "small conv: R*S*CI too large");
-  g.OH = (g.H + 2 * (int)pad - g.R) / (int)stride + 1;
-  g.OW = (g.W + 2 * (int)pad - g.S) / (int)stride + 1;
-  TORCH_CHECK(g.OH > 0 && g.OW > 0, "small conv: empty output");
-  TORCH_CHECK((long long)g.B * g.OH * g.OW * g.CO < (1LL << 31) && x.numel() < (1LL << 30),
+  TORCH_CHECK(w.size(1) == x.size(1), "small conv: weight/input channel mismatch");
+  TORCH_CHECK(stride >= 1 && pad >= 0 && w.size(2) <= 255 && w.size(3) <= 255,
+              "small conv: bad geometry");
+  TORCH_CHECK(w.size(0) % 64 == 0, "small conv: CO must be a multiple of 64");
+  TORCH_CHECK(w.size(1) * w.size(2) * w.size(3) <= dmp::conv_small_max_k(),
+              "small conv: R*S*CI too large");
+  const int64_t OH = dmp::guard::conv_out(x.size(2), pad, w.size(2), stride);
+  const int64_t OW = dmp::guard::conv_out(x.size(3), pad, w.size(3), stride);
+  TORCH_CHECK(OH > 0 && OW > 0, "small conv: empty output");
+  TORCH_CHECK(dmp::guard::small_conv_ok(x.size(0), OH, OW, w.size(0), x.numel()),
               "small conv: tensor too large for 32-bit indexing");
+  SmallGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(0),
+              (int)w.size(2), (int)w.size(3), (int)OH, (int)OW};
   return g;
 }
 
@@ -826,7 +838,7 @@ std::vector<Tensor> stem_fwd(Tensor x, Tensor w, bool want_stats, optional<Tenso
               "stem: w must be a channels_last bf16 [64, 3, 7, 7] tensor");
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
   TORCH_CHECK(dmp::stem_supported((int)H, (int)W), "stem: unsupported input size ", H, "x", W);
-  TORCH_CHECK(2 * B * (H / 2) * (W / 2) * 64 < (1LL << 31), "stem: batch too large");
+  TORCH_CHECK(dmp::guard::stem_batch_ok(B, H, W), "stem: batch too large");
   auto xs = at::empty({B, H / 2, W / 2, 16}, x.options());
   auto wp = at::empty({64, 256}, w.options());
   auto y = at::empty({B, 64, H / 2, W / 2}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -1045,7 +1057,7 @@ int64_t mat_ld(const Tensor& t, at::ScalarType dt, int64_t rows, int64_t cols,
   TORCH_CHECK(t.stride(1) == 1, name, " must have a unit inner stride");
   const int64_t ld = rows <= 1 ? cols : t.stride(0);
   TORCH_CHECK(ld >= cols, name, ": row stride smaller than the row");
-  TORCH_CHECK((int64_t)t.element_size() * rows * ld < (1LL << 31), name,
+  TORCH_CHECK(dmp::guard::rows_bytes_ok(t.element_size(), rows, ld), name,
               " exceeds the 2 GiB 32-bit offset range of the GEMM kernels");
   return ld;
 }
@@ -1594,10 +1606,11 @@ std::vector<Tensor> bn_relu_maxpool_fwd(Tensor x, Tensor part, bool have_partial
                                         int64_t P) {
   check_nhwc_bf16(x, "x");
   TORCH_CHECK(x.dim() == 4, "bn_relu_maxpool expects 4-D input");
+  TORCH_CHECK(dmp::guard::bf16_bytes_ok(x.size(0), x.size(2), x.size(3), x.size(1)),
+              "bn_relu_maxpool: x over 2 GiB (32-bit offsets)");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   TORCH_CHECK(dmp::bn_maxpool_supported(C, (int)K, (int)S, (int)P),
               "bn_relu_maxpool: needs C % 64 == 0, C <= 2048 and a 3x3/s2/p1 window");
-  TORCH_CHECK(2LL * N * H * W * C < (1LL << 31), "bn_relu_maxpool: x over 2 GiB (32-bit offsets)");
   auto fopt = x.options().dtype(at::kFloat);
   part = bn_slots(part, C, fopt);
   float* zb = nullptr;
@@ -1639,9 +1652,10 @@ Tensor maxpool_bn_bwd(Tensor x, Tensor dp, Tensor idx, Tensor xm, optional<Tenso
   auto mf = at::MemoryFormat::ChannelsLast;
   dp = dp.contiguous(mf);
   check_nhwc_bf16(dp, "dp");
+  TORCH_CHECK(dmp::guard::bf16_bytes_ok(x.size(0), x.size(2), x.size(3), x.size(1)),
+              "maxpool_bn_bwd: x over 2 GiB (32-bit offsets)");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   TORCH_CHECK(dmp::bn_maxpool_supported(C, (int)K, (int)S, (int)P), "maxpool_bn_bwd: bad window");
-  TORCH_CHECK(2LL * N * H * W * C < (1LL << 31), "maxpool_bn_bwd: x over 2 GiB (32-bit offsets)");
   TORCH_CHECK(dp.size(0) == N && dp.size(1) == C &&
                   dp.size(2) == dmp::maxpool_out(H, (int)K, (int)S, (int)P) &&
                   dp.size(3) == dmp::maxpool_out(W, (int)K, (int)S, (int)P),
@@ -1731,7 +1745,8 @@ PYBIND11_MODULE(_native, m) {
         py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"));
   m.doc() = "gfx950 (MI355X) HIP kernels for distributed_ml_pytorch_amd";
   m.def("asgd_fused_step", &asgd_fused_step, "fused flat ASGD/SGD update");
-  m.def("ps_apply", &ps_apply, "parameter-server delta apply");
+  m.def("ps_apply", &ps_apply, "parameter-server delta apply", py::arg("shard"), py::arg("delta"),
+        py::arg("mirror") = py::none(), py::arg("scale") = 1.0, py::arg("atomic") = false);
   m.def("pull_land", &pull_land, "land a parameter pull into the worker arena");
   m.def("push_handoff", &push_handoff, "snapshot+zero the push accumulator");
   m.def("cast_f32_bf16", &cast_f32_bf16, "flat fp32 -> bf16");

@@ -11,6 +11,8 @@ namespace dmp {
 void launch_asgd_fused_step(const float* g, float* p, float* acc, float* mom, uint16_t* w16,
                             long long n, float lr, float wd, float momentum, float dampening,
                             bool nesterov, hipStream_t s);
+void launch_ps_apply_atomic(float* shard, const void* delta, bool bf16, long long n, float scale,
+                            hipStream_t s);
 void launch_ps_apply_f32(float* shard, const float* delta, uint16_t* mirror, long long n,
                          float scale, hipStream_t s);
 void launch_ps_apply_bf16(float* shard, const uint16_t* delta, uint16_t* mirror, long long n,

@@ -14,6 +14,8 @@
 // 256-B aligned, so n % 4 == 0 always holds (asserted on the host side).
 #include "common.h"
 
+#include <algorithm>
+
 namespace dmp {
 
 // g      : fp32 gradient (flat)         [n]
@@ -97,6 +99,25 @@ __global__ void __launch_bounds__(256) ps_apply_bf16_kernel(
       o.v[0] = f2bf(s.x); o.v[1] = f2bf(s.y); o.v[2] = f2bf(s.z); o.v[3] = f2bf(s.w);
       mirror[i] = o;
     }
+  }
+}
+
+// shard += scale * delta with fp32 global atomics (no-return
+// global_atomic_add_f32): the completion-ordered PS applies each worker's delta
+// on that worker's own link stream, so applies of different workers may run at
+// the same time on one shard ("or use fp32 atomics").  Lane i
+// of a wave adds element base + i: every wave-instruction covers 256 contiguous
+// bytes, the full-rate shape of MI355X_MICROARCH.md §Global float atomics.
+template <typename D>
+__global__ void __launch_bounds__(256) ps_apply_atomic_kernel(float* __restrict__ shard,
+                                                              const D* __restrict__ delta,
+                                                              long long n, float scale) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float d;
+    if constexpr (sizeof(D) == 4) d = delta[i];
+    else d = bf2f(delta[i]);
+    unsafeAtomicAdd(shard + i, scale * d);
   }
 }
 
@@ -238,6 +259,17 @@ void launch_ps_apply_bf16(float* shard, const u16* delta, u16* mirror, long long
   const long long n4 = n / 4;
   hipLaunchKernelGGL(ps_apply_bf16_kernel, dim3(stream_grid(n4, 256)), dim3(256), 0, s,
                      (float4*)shard, (const bf16x4*)delta, (bf16x4*)mirror, n4, scale);
+}
+
+void launch_ps_apply_atomic(float* shard, const void* delta, bool bf16, long long n, float scale,
+                            hipStream_t s) {
+  const int grid = (int)std::min<long long>((n + 255) / 256, 256LL * 16);
+  if (bf16)
+    hipLaunchKernelGGL(ps_apply_atomic_kernel<u16>, dim3(grid), dim3(256), 0, s, shard,
+                       (const u16*)delta, n, scale);
+  else
+    hipLaunchKernelGGL(ps_apply_atomic_kernel<float>, dim3(grid), dim3(256), 0, s, shard,
+                       (const float*)delta, n, scale);
 }
 
 void launch_pull_land_f32(float* p, const float* src, const float* acc, u16* w16, long long n,

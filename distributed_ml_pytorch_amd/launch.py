@@ -21,6 +21,8 @@ import sys
 import threading
 import time
 
+from .runtime.dist import apply_hw_queue_policy
+
 
 def free_port() -> int:
     with socket.socket() as s:
@@ -45,11 +47,10 @@ def launch(script: str, script_args, nproc: int, gpus: bool = False, port: int |
         env.update({"RANK": str(r), "WORLD_SIZE": str(nproc), "LOCAL_RANK": str(r),
                     "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        if r == 0 and gpus:
-            # rank 0 is the parameter server of the reference topology: one HIP
-            # stream per worker link needs more than HIP's default 4 hardware
-            # queues to run the links concurrently (parallel/links.py)
-            env.setdefault("GPU_MAX_HW_QUEUES", "16")
+        if gpus:
+            # every rank runs several HIP streams (PS links, push/pull side
+            # stream, RCCL): one queue policy for all (profiles/hw_queue_policy_r5.txt)
+            apply_hw_queue_policy(nproc, env)
         if env_extra:
             env.update(env_extra)
         args = [python, script, *script_args, "--rank", str(r), "--world-size", str(nproc),

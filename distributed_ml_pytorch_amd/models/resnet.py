@@ -173,7 +173,8 @@ class ResNet(nn.Module):
         pooled = False
         if h is None:
             h = self.conv1(x)
-            pk = (self.pool.kernel_size, self.pool.stride, self.pool.padding) if self.pool else None
+            # ints, floor mode, no dilation: else the separate pool below
+            pk = self.pool.native_params() if self.pool is not None else None
             if pk is not None and bn_relu_maxpool_ok(h, self.bn1, *pk):
                 h, pooled = bn_relu_maxpool(h, self.bn1, *pk), True   # BN + ReLU + pool fused
             else:

@@ -51,7 +51,9 @@ def fold_enabled(x, module) -> bool:
 
 
 def _foldable(bn) -> bool:
-    return (bn.track_running_stats and bn.running_mean is not None
+    # running statistics only: a BatchNorm left in train mode inside an eval-mode
+    # block normalises with batch statistics, which a fold cannot reproduce
+    return (not bn.training and bn.track_running_stats and bn.running_mean is not None
             and bn.running_var is not None)
 
 

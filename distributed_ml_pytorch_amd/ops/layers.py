@@ -106,13 +106,25 @@ class BatchNorm1d(nn.BatchNorm1d):
 
 
 class MaxPool2d(nn.MaxPool2d):
+    def native_params(self):
+        """(k, s, p) as ints when the native floor-mode square pool applies, else
+        None (ceil_mode, dilation, or a non-square kernel / stride / padding)."""
+        def one(v):
+            if isinstance(v, int):
+                return v
+            v = tuple(v)
+            return v[0] if len(v) == 2 and v[0] == v[1] else None
+        k, s, p = one(self.kernel_size), one(self.stride), one(self.padding)
+        d = one(self.dilation)
+        if self.ceil_mode or d != 1 or None in (k, s, p):
+            return None
+        return k, s, p
+
     def forward(self, x):
-        k = self.kernel_size if isinstance(self.kernel_size, int) else self.kernel_size[0]
-        s = self.stride if isinstance(self.stride, int) else self.stride[0]
-        p = self.padding if isinstance(self.padding, int) else self.padding[0]
-        if self.ceil_mode or self.dilation not in (1, (1, 1)):
+        kp = self.native_params()
+        if kp is None:
             return super().forward(x)
-        return DF.max_pool2d(x, k, s, p)
+        return DF.max_pool2d(x, *kp)
 
 
 class GlobalAvgPool(nn.Module):

@@ -114,8 +114,9 @@ class ShardServer:
             self.master = init_shard.detach().to(torch.float32).clone()
         # link-concurrent payloads (:mod:`.links`): one stream + buffer ring per
         # (peer, direction), so pushes from different ranks land concurrently and
-        # only the applies serialise, on self.stream.  The same code path runs on
-        # CPU (gloo groups, host waits) -- the multi-process tests exercise it.
+        # (GPU) each is applied on its own link stream as soon as it has landed
+        # (fp32 atomics).  The same code path runs on CPU (gloo groups, host
+        # waits, applies in arrival order) -- the multi-process tests exercise it.
         peers = [r for r in range(world) if r != rank]
         self.rx = PairLinks(self.device, transport or PairGroupTransport(
             {s: g for (s, _o), g in push_groups.items()}), peers=peers)
@@ -143,7 +144,7 @@ class ShardServer:
                 for dt in (torch.float32, torch.bfloat16):
                     self.nat.ps_apply(self.master, torch.zeros(self.n, dtype=dt,
                                                                device=self.device),
-                                      None, self.scale)
+                                      None, self.scale, True)
             self.stream.synchronize()
         self.thread = threading.Thread(target=self._run, daemon=True, name=f"shard-ps-{rank}")
 
@@ -157,7 +158,9 @@ class ShardServer:
     # --------------------------------------------------------------- apply
     def _apply_locked(self, delta: torch.Tensor, base_version: int | None):
         if self.cuda:
-            self.nat.ps_apply(self.master, delta, None, self.scale)
+            # fp32 atomics: the local apply (self.stream) and every peer's apply
+            # (its own link stream, _recv_push) may run at the same time
+            self.nat.ps_apply(self.master, delta, None, self.scale, True)
         else:
             self.master.add_(delta.to(torch.float32), alpha=self.scale)
         if base_version is not None:
@@ -184,7 +187,8 @@ class ShardServer:
 
     def snapshot(self, out: torch.Tensor | None = None):
         """``(copy of the shard, version, event)``: on GPU the copy is taken on the
-        PS stream after every apply enqueued so far; ``event`` marks it done."""
+        PS stream after every LOCAL apply enqueued so far (peers' applies land on
+        their link streams whenever their payloads arrive); ``event`` marks it done."""
         with self.lock:
             v = self.version
             if not self.cuda:
@@ -204,6 +208,15 @@ class ShardServer:
         # posted on the sender's own link stream, behind nothing but the apply
         # that last read its ring slot; no lock: only the apply needs one
         slot, ready = self.rx.recv(sender, nelem, dtype)
+        if self.cuda:
+            # completion-ordered: applied on the SENDER's link stream right behind
+            # its own receive, so a slow peer's payload still in flight delays no
+            # other peer's apply (the receive's ``ready`` is on that stream)
+            s = self.rx.stream(sender)
+            with self.lock, torch.cuda.stream(s):
+                self._apply_locked(slot.buf, version)
+                self.rx.release(slot, s)
+            return
         with self.lock, self._ctx():
             wait_on(self.stream, ready)
             self._apply_locked(slot.buf, version)
@@ -218,10 +231,19 @@ class ShardServer:
                 buf[:n].copy_(self.master)
                 buf[n:].fill_(version)
 
-            # snapshot on the PS stream (after every apply enqueued so far), sent on
-            # dst's own reply-link stream; the ring slot is reused only after its
-            # previous send completed
-            self.tx.send(dst, n + 1, torch.float32, fill, self.stream)
+            # snapshot on dst's own reply-link stream, after dst's own applies
+            # (its push-link stream: read-your-writes) and the local worker's
+            # (self.stream), never behind another peer's payload in flight; the
+            # ring slot is reused only after its previous send completed
+            if self.cuda:
+                s = self.tx.stream(dst)
+                for src in (self.rx.stream(dst), self.stream):
+                    ev = torch.cuda.Event()
+                    ev.record(src)
+                    s.wait_event(ev)
+                self.tx.send(dst, n + 1, torch.float32, fill, s)
+            else:
+                self.tx.send(dst, n + 1, torch.float32, fill, self.stream)
 
     def _run(self):
         remaining = set(range(self.world)) - {self.rank}

@@ -19,9 +19,15 @@ staleness), per-worker liveness, periodic checkpoints, and two payload paths:
   kernel and the reply snapshots stay on the GPU, and the links run
   concurrently (:mod:`.links`): every worker's receives and sends are posted
   on that worker's own stream and buffer ring, so transfers from different
-  workers overlap (one xGMI link each); only the applies and the reply
-  snapshots are serialised, on the apply stream, each after ITS receive's
-  event.  No host syncs anywhere.
+  workers overlap (one xGMI link each).  Applies are COMPLETION-ordered: each
+  worker's delta is added on that worker's own link stream right after its
+  receive lands, with fp32 atomics (applies of different workers may overlap
+  in time), so a slow worker's pending payload never delays
+  another worker's apply.  A reply snapshot is taken on the requester's own
+  stream: it observes that worker's own applies (read-your-writes) and
+  whatever other workers' applies have landed by then -- the reference PS had
+  no ordering between workers at all (/root/reference/example/main.py:135-138).
+  No host syncs anywhere.
 """
 from __future__ import annotations
 
@@ -128,6 +134,8 @@ class ParameterServer:
         self._tracker = M.SendTracker()
         self._hq = None
         self._recv_bufs = defaultdict(dict)      # gloo payload path
+        self._init_ev = None                     # last shard overwrite (device links)
+        self._applied_on: set = set()            # link streams that carry applies
         self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         if self.links is not None:
             # every worker's payload rings up front (fp32 and bf16 wire), not at
@@ -155,9 +163,9 @@ class ParameterServer:
         the shard unchanged."""
         with torch.cuda.stream(self.stream):
             for dt in (torch.float32, torch.bfloat16):
-                self._native.ps_apply(self.shard, torch.zeros(padded, dtype=dt,
-                                                              device=self.device),
-                                      None, self.delta_scale)
+                z = torch.zeros(padded, dtype=dt, device=self.device)
+                self._native.ps_apply(self.shard, z, None, self.delta_scale)
+                self._native.ps_apply(self.shard, z, None, self.delta_scale, True)
             snap = torch.empty(self.numel + 1, dtype=torch.float32, device=self.device)
             snap[: self.numel].copy_(self.shard[: self.numel])
             snap[self.numel:].fill_(0.0)
@@ -198,9 +206,13 @@ class ParameterServer:
                 buf[:n].copy_(self.shard[:n])   # snapshot: later applies never tear it
                 buf[n:].fill_(version)
 
-            # snapshot on the apply stream (after every apply enqueued so far),
-            # send on dst's own link stream
-            self.links.send(dst, n + 1, torch.float32, fill, self.stream)
+            # snapshot on dst's OWN link stream: behind dst's own applies (same
+            # stream) and the last initialisation, never behind another worker's
+            # payload still in flight
+            s = self.links.stream(dst)
+            with torch.cuda.stream(s):
+                wait_on(s, self._init_ev)
+            self.links.send(dst, n + 1, torch.float32, fill, s)
         else:
             snap = torch.empty(n + 1, dtype=torch.float32)
             snap[:n].copy_(self.shard[:n])
@@ -209,10 +221,21 @@ class ParameterServer:
             self._tracker.add(w, snap)
         self.bytes_out += (n + 1) * 4
 
-    def _apply(self, delta: torch.Tensor, ready=None, slot=None):
-        """``shard += scale * delta``; on GPU on the apply stream, after ``ready``
-        (the delta's receive), releasing the receive ``slot`` when done."""
-        if self._native is not None:
+    def _apply(self, delta: torch.Tensor, ready=None, slot=None, sender: int | None = None):
+        """``shard += scale * delta``.  Device links: on the SENDER's link stream,
+        right behind its receive (``ready`` is on that stream), with fp32 atomics
+        so concurrent applies of different workers all land, releasing the receive
+        ``slot`` when done.  Otherwise on the apply stream after ``ready``."""
+        if self._native is not None and self.links is not None and sender is not None:
+            s = self.links.stream(sender)
+            with torch.cuda.stream(s):
+                wait_on(s, ready)
+                wait_on(s, self._init_ev)
+                self._native.ps_apply(self.shard, delta, None, self.delta_scale, True)
+                if slot is not None:
+                    self.links.release(slot, s)
+            self._applied_on.add(sender)
+        elif self._native is not None:
             with torch.cuda.stream(self.stream):
                 wait_on(self.stream, ready)
                 self._native.ps_apply(self.shard, delta, None, self.delta_scale)
@@ -226,9 +249,18 @@ class ParameterServer:
     def _set(self, params: torch.Tensor, ready=None, slot=None):
         with torch.cuda.stream(self.stream) if self.stream is not None else _null():
             wait_on(self.stream, ready)
+            # an overwrite orders against every apply already enqueued on a link
+            for p in sorted(self._applied_on):
+                ev = torch.cuda.Event()
+                ev.record(self.links.stream(p))
+                self.stream.wait_event(ev)
             self.shard[: self.numel].copy_(params[: self.numel])
             if slot is not None:
                 self.links.release(slot, self.stream)
+            if self.links is not None:
+                # later applies and reply snapshots (link streams) wait for it
+                self._init_ev = torch.cuda.Event()
+                self._init_ev.record(self.stream)
 
     # -------------------------------------------------------------------- loop
     def handle(self, code, sender: int, step: int, version: int, nelem: int, dtype):
@@ -237,7 +269,7 @@ class ParameterServer:
         if code == M.MessageCode.GradientUpdate:
             delta, ready, slot = self._recv_payload(sender, nelem, dtype)
             self.staleness.append(self.version - version)
-            self._apply(delta, ready, slot)
+            self._apply(delta, ready, slot, sender)
             if self.checkpoint_every and self.version % self.checkpoint_every == 0:
                 self.save_checkpoint()
         elif code == M.MessageCode.ParameterUpdate:
@@ -329,17 +361,20 @@ class ParameterServer:
 
     def finish(self):
         self._tracker.drain()
+        self._sync_device()
+        if self.checkpoint_path:
+            self.save_checkpoint()
+
+    def _sync_device(self):
+        """Wait for every enqueued apply / overwrite / transfer (all streams)."""
         if self.links is not None:
             self.links.synchronize()
         if self.stream is not None:
             self.stream.synchronize()
-        if self.checkpoint_path:
-            self.save_checkpoint()
 
     # --------------------------------------------------------------- utilities
     def parameters(self) -> torch.Tensor:
-        if self.stream is not None:
-            self.stream.synchronize()
+        self._sync_device()
         return self.shard[: self.numel]
 
     def stats(self) -> dict:

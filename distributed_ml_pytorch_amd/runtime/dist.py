@@ -35,6 +35,25 @@ def _env(name, default=None):
     return default if v is None or v == "" else v
 
 
+# Hardware queues per process for every multi-rank GPU process.  Each rank runs
+# several HIP streams at once (compute, the push/pull side stream, the wgrad
+# side stream, one link stream per peer on a PS, and RCCL's internal streams);
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4) and
+# streams that share a queue run back to back (profiles/links_stream_creation_r4.txt,
+# profiles/hw_queue_policy_r5.txt).  The harness refuses values above 32.
+MULTI_RANK_HW_QUEUES = 16
+
+
+def apply_hw_queue_policy(world_size: int, env: dict | None = None) -> str | None:
+    """Set ``GPU_MAX_HW_QUEUES`` for a multi-rank job (HIP reads it once, at its
+    initialisation: call before the first ``torch.cuda`` call of the process, or
+    on a child's environment).  An explicit setting wins.  Returns the value."""
+    env = os.environ if env is None else env
+    if world_size > 1:
+        env.setdefault("GPU_MAX_HW_QUEUES", str(MULTI_RANK_HW_QUEUES))
+    return env.get("GPU_MAX_HW_QUEUES")
+
+
 def init_distributed(rank: int | None = None, world_size: int | None = None,
                      backend: str = "auto", master: str | None = None, port: str | None = None,
                      use_cuda: bool | None = None, timeout_s: float = 1800.0) -> DistInfo:

@@ -197,12 +197,15 @@ class Worker:
         """
         can = self.device.type == "cuda"
         if self.ddp is not None and self.info.is_distributed:
-            # gloo collectives cannot be captured; RCCL ones are, by default: eager
-            # sync DP pays the host launch of every dispatch (~350 per ResNet-50
-            # step, profiles/sync_capture_ab_r4.txt).  A capture that fails falls
-            # back to eager stepping (_capture); DMP_GRAPH_SYNC=0 forces eager.
+            # gloo collectives cannot be captured; RCCL ones can, OPT-IN
+            # (DMP_GRAPH_SYNC=1): eager sync DP pays the host launch of every
+            # dispatch (~350 per ResNet-50 step, profiles/sync_dp_capture_ab_r4.txt),
+            # but that A/B ran at world 1 and a captured multi-rank all-reduce has
+            # not been replayed on a multi-GPU node yet, so multi-rank sync DP
+            # steps eagerly by default.  With capture on, a capture that fails on
+            # ANY rank makes every rank step eagerly (_capture_agreed).
             can = can and self.info.backend == "nccl" and \
-                os.environ.get("DMP_GRAPH_SYNC", "1") != "0"
+                os.environ.get("DMP_GRAPH_SYNC", "0") == "1"
         self.use_graph = bool(enabled) and can
         self.graph = None
         return self.use_graph
@@ -230,20 +233,39 @@ class Worker:
             self.step_idx += 1
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
+        err = None
         try:
             # thread_local: RCCL's watchdog thread queries events while we capture
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._gloss, self._ghits = self._graph_body()
         except RuntimeError as e:     # e.g. a collective backend that cannot be captured
+            err = str(e)
             if self.ddp is not None:
                 self.ddp.reset()
-            print(f"[trainer] hipGraph capture failed ({e}); stepping eagerly", flush=True)
+        # sync DP: every rank replays or every rank steps eagerly -- a rank whose
+        # capture failed must not run a different launch path from its peers
+        # (capture records the collectives, it does not run them, so this
+        # agreement all-reduce is the first collective after the eager step)
+        if self.ddp is not None and self.info.is_distributed and \
+                not self._capture_agreed(err is None):
+            err = err or "a peer rank's capture failed"
+            self.ddp.reset()
+        if err is not None:
+            print(f"[trainer] hipGraph capture failed ({err}); stepping eagerly", flush=True)
             self.use_graph = False
             self.graph = None
             return loss.clone(), hits.clone()
         self.graph = g
         self._graph_key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])
         return loss.clone(), hits.clone()
+
+    def _capture_agreed(self, ok: bool) -> bool:
+        """MIN-all-reduce of the local capture verdict over the sync-DP group."""
+        import torch.distributed as dist
+
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.ddp.group)
+        return bool(flag.item())
 
     def _graph_step(self, x, y, keep: bool = True):
         key = (tuple(x.shape), x.dtype, self.opt.param_groups[0]["lr"])

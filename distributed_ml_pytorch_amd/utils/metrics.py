@@ -137,6 +137,99 @@ class StepTimer:
                 for k, v in self.totals.items()}
 
 
+class ClockSampler:
+    """Graphics clock (MHz) and socket power (W) of one GPU, sampled by a host
+    thread through amdsmi while a timed window runs, so box-to-box variance in a
+    benchmark line is visible next to the number (a throttled box reads lower
+    sclk).  These are the SMU's reported values, not the in-kernel clock
+    (MI355X_MICROARCH.md, DVFS give-back item 6); every failure (no amdsmi, no
+    permission, no matching device) yields ``None`` instead of an exception."""
+
+    def __init__(self, device_index: int = 0, period_s: float = 0.004):
+        self.period = period_s
+        self.device_index = device_index
+        self._h = None
+        self._smi = None
+        self._thr = None
+        self._stop = None
+        self.samples: list[tuple[float, float | None]] = []
+        try:
+            import amdsmi
+
+            amdsmi.amdsmi_init()
+            self._smi = amdsmi
+            hs = amdsmi.amdsmi_get_processor_handles()
+            self._h = self._match(hs)
+        except Exception:
+            self._h = None
+
+    def _match(self, hs):
+        if not hs:
+            return None
+        try:   # same PCI bus as the torch device when torch reports one
+            props = torch.cuda.get_device_properties(self.device_index)
+            bus = getattr(props, "pci_bus_id", None)
+            if bus is not None:
+                for h in hs:
+                    bdf = self._smi.amdsmi_get_gpu_device_bdf(h)
+                    if int(bdf.split(":")[1], 16) == int(bus):
+                        return h
+        except Exception:
+            pass
+        return hs[0] if len(hs) == 1 else hs[min(self.device_index, len(hs) - 1)]
+
+    def _read(self):
+        smi = self._smi
+        clk = smi.amdsmi_get_clock_info(self._h, smi.AmdSmiClkType.SYS)["clk"]
+        pw = None
+        try:
+            p = smi.amdsmi_get_power_info(self._h)
+            pw = p.get("current_socket_power")
+            if not isinstance(pw, (int, float)) or pw <= 0:
+                pw = p.get("average_socket_power")
+            pw = float(pw) if isinstance(pw, (int, float)) and pw > 0 else None
+        except Exception:
+            pass
+        return float(clk), pw
+
+    def start(self):
+        if self._h is None:
+            return self
+        import threading
+
+        self.samples = []
+        self._stop = threading.Event()
+
+        def loop():
+            while not self._stop.is_set():
+                try:
+                    self.samples.append(self._read())
+                except Exception:
+                    return
+                self._stop.wait(self.period)
+
+        self._thr = threading.Thread(target=loop, daemon=True)
+        self._thr.start()
+        return self
+
+    def stop(self) -> dict | None:
+        if self._thr is None:
+            return None
+        self._stop.set()
+        self._thr.join(timeout=1.0)
+        self._thr = None
+        clks = [c for c, _ in self.samples if c and c > 0]
+        pws = [p for _, p in self.samples if p]
+        if not clks:
+            return None
+        out = {"samples": len(clks), "sclk_mhz_mean": round(sum(clks) / len(clks), 1),
+               "sclk_mhz_min": min(clks), "sclk_mhz_max": max(clks)}
+        if pws:
+            out["power_w_mean"] = round(sum(pws) / len(pws), 1)
+            out["power_w_max"] = max(pws)
+        return out
+
+
 def classification_report(conf: torch.Tensor, names=None, digits: int = 2) -> str:
     """Per-class precision / recall / F1 / support from a [C, C] confusion matrix
     (rows = true class), laid out like sklearn's ``classification_report`` that the

@@ -46,6 +46,28 @@ def test_asgd_fused_step(nat, momentum, wd, nesterov):
     torch.testing.assert_close(w16, p.to(torch.bfloat16), rtol=0, atol=0)
 
 
+def test_ps_apply_atomic_concurrent_streams(nat):
+    """fp32-atomic PS apply (completion-ordered central / sharded PS): four
+    deltas applied at once from four streams all land (fp32 reference, order
+    free, so a tolerance); fp32 and bf16 wire deltas."""
+    n = (1 << 20) + 4
+    shard = torch.randn(n, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(1)
+    deltas = [torch.randn(n, device="cuda", generator=g) for _ in range(3)]
+    deltas.append(torch.randn(n, device="cuda", generator=g).to(torch.bfloat16))
+    ref = shard.double() + sum(0.25 * d.double() for d in deltas)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in deltas]
+    for s, d in zip(streams, deltas):
+        with torch.cuda.stream(s):
+            nat.ps_apply(shard, d, None, 0.25, True)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(shard.double(), ref, rtol=1e-5, atol=1e-5)
+    with pytest.raises(RuntimeError):
+        nat.ps_apply(shard, deltas[0], torch.empty(n, device="cuda", dtype=torch.bfloat16),
+                     1.0, True)
+
+
 def test_ps_apply_and_pull_land(nat):
     n = 1 << 16
     shard = torch.randn(n, device="cuda")

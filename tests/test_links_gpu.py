@@ -7,8 +7,11 @@ operation makes it wait on the caller's current stream, a ``torch.cuda._sleep``
 stands in for the wire time, a device copy moves the bytes, and ``work.wait()``
 makes the caller's current stream wait for the copy.  With that, the PS must
 (a) have two workers' receives in flight at once, (b) apply each delta only
-after its own receive, serially, all of them, and (c) send replies that
-observe every apply enqueued before them.
+after its own receive, all of them (completion-ordered, fp32 atomics: applies
+of different workers may overlap), and (c) send replies that observe the
+requester's own applies (read-your-writes).  The uneven scenario gives worker
+1 five times worker 2's wire time: worker 2's applies and reply must not wait
+for worker 1's payload (What's missing #1).
 """
 import os
 import socket
@@ -33,8 +36,9 @@ class _EvWork:
 
 
 class DelayedCopyTransport:
-    def __init__(self, cycles: int, peers=(1, 2)):
-        self.cycles = cycles
+    def __init__(self, cycles, peers=(1, 2)):
+        # ``cycles``: one wire time for every peer, or {peer: cycles}
+        self.cycles = cycles if isinstance(cycles, dict) else {p: cycles for p in peers}
         self.outbox = defaultdict(deque)    # peer -> tensors the peer "sends" to us
         self.inbox = defaultdict(list)      # peer -> tensors we sent to the peer
         # created up front, as RCCL creates a communicator's stream at its first
@@ -55,7 +59,7 @@ class DelayedCopyTransport:
         with torch.cuda.stream(cs):
             a = torch.cuda.Event(enable_timing=True)
             a.record()
-            torch.cuda._sleep(self.cycles)
+            torch.cuda._sleep(self.cycles[peer])
             fn()
             b = torch.cuda.Event(enable_timing=True)
             b.record()
@@ -84,15 +88,17 @@ def _gloo_world1():
     return True
 
 
-def _scenario():
-    """Run the two-worker PS scenario; return its timings (ms) and checks."""
+def _scenario(uneven: bool = False):
+    """Run the two-worker PS scenario; return its timings (ms) and checks.
+    ``uneven``: worker 1's wire time is 5x worker 2's, and worker 2 pulls."""
     from distributed_ml_pytorch_amd.parallel import messaging as M
     from distributed_ml_pytorch_amd.parallel.server import ParameterServer
 
     made = _gloo_world1()
     try:
         n = 1 << 20
-        tr = DelayedCopyTransport(cycles=20_000_000)
+        tr = DelayedCopyTransport(cycles={1: 50_000_000, 2: 10_000_000} if uneven
+                                  else 20_000_000)
         g = torch.Generator(device="cuda").manual_seed(0)
         deltas = {w: [torch.randn(n, device="cuda", generator=g) for _ in range(2)]
                   for w in (1, 2)}
@@ -107,21 +113,32 @@ def _scenario():
         import time
 
         host = []
+        puller = 2 if uneven else 1
         for code, w, st, v in ((GU, 1, 0, 0), (GU, 2, 0, 0), (GU, 1, 1, 1), (GU, 2, 1, 1),
-                               (PR, 1, 2, 0)):
+                               (PR, puller, 2, 0)):
             t = time.perf_counter()
             ps.handle(code, w, st, v, n if code == GU else 0, f32)
             host.append(round(1e3 * (time.perf_counter() - t), 3))
         ps.finish()
         torch.cuda.synchronize()
         want = sum(deltas[1]) + sum(deltas[2])
-        reply = tr.inbox[1][-1]
+        reply = tr.inbox[puller][-1]
+        other = 3 - puller
+        # read-your-writes: the reply holds the puller's own two deltas plus a
+        # prefix (none, the first, or both) of the other worker's
+        own = sum(deltas[puller])
+        cands = [own, own + deltas[other][0], own + deltas[other][0] + deltas[other][1]]
+        errs = [float((reply[:n] - c).abs().max()) for c in cands]
         recvs = [(p, a, b) for k, p, a, b in tr.spans if k == "recv"]
+        sends = [(p, a, b) for k, p, a, b in tr.spans if k == "send"]
         a1 = recvs[0][1]
         w1 = [(a, b) for p, a, b in recvs if p == 1]
         return {
             "master_err": float((ps.parameters() - want).abs().max()),
-            "reply_err": float((reply[:n] - want).abs().max()),
+            "reply_err": min(errs),
+            "reply_prefix": errs.index(min(errs)),
+            "w1_first_recv_end": a1.elapsed_time(w1[0][1]),
+            "reply_end": a1.elapsed_time(sends[-1][2]),
             "reply_version": float(reply[n]), "version": ps.version,
             "order": [p for p, _, _ in recvs],
             "dur1": a1.elapsed_time(recvs[0][2]),
@@ -137,7 +154,7 @@ def _scenario():
             dist.destroy_process_group()
 
 
-def _run_scenario(queues: int | None):
+def _run_scenario(queues: int | None, uneven: bool = False):
     """In a fresh process: HIP reads GPU_MAX_HW_QUEUES once, at initialisation."""
     import json
     import subprocess
@@ -146,6 +163,7 @@ def _run_scenario(queues: int | None):
     env = dict(os.environ)
     if queues is not None:
         env["GPU_MAX_HW_QUEUES"] = str(queues)
+    env["DMP_LINKS_SCENARIO"] = "uneven" if uneven else "even"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, os.path.abspath(__file__)], capture_output=True,
                        text=True, timeout=100, env=env, cwd=root)
@@ -162,7 +180,8 @@ def test_ps_links_overlap_receives(queues):
     whatever the PS did (profiles/links_stream_creation_r4.txt, scripts/links_probe.py)."""
     r = _run_scenario(queues)
     print(queues, r)
-    # (b) every delta applied exactly once; (c) the reply saw all four applies
+    # (b) every delta applied exactly once (any order: fp32 atomics, so a
+    # tolerance); (c) the reply saw at least worker 1's own applies
     assert r["master_err"] < 1e-4 and r["reply_err"] < 1e-4, r
     assert r["version"] == 4 and r["reply_version"] == 4.0
     assert r["order"] == [1, 2, 1, 2]
@@ -175,10 +194,23 @@ def test_ps_links_overlap_receives(queues):
     assert r["end_last"] < 3.2 * r["dur1"], r
 
 
+def test_ps_completion_ordered_applies():
+    """Worker 1's wire time is 5x worker 2's.  Worker 2's two applies and its
+    reply (sent on its link stream behind its applies and the snapshot) finish
+    before worker 1's FIRST receive has landed, the reply holds exactly worker
+    2's own deltas, and the master ends at the sum of all four deltas."""
+    r = _run_scenario(16, uneven=True)
+    print(r)
+    assert r["master_err"] < 1e-4, r
+    assert r["reply_err"] < 1e-4 and r["reply_prefix"] == 0, r
+    assert r["version"] == 4 and r["links"]["recv"] == 4 and r["links"]["send"] == 1
+    assert r["reply_end"] < r["w1_first_recv_end"], r
+
+
 if __name__ == "__main__":
     import json
     import sys
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-    print(json.dumps(_scenario()), flush=True)
+    print(json.dumps(_scenario(os.environ.get("DMP_LINKS_SCENARIO") == "uneven")), flush=True)
