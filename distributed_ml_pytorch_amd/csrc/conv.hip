@@ -1214,9 +1214,18 @@ struct HaloPGeom {
   // pass it would replace (profiles/bn_consumer_fusion_r3.txt).
   int xform;
   float xs, xh, xlo;
+  // 8-wave blocks: waves 4-7 (the SIMD partners of waves 0-3) run each tile as
+  // compute(k) -> epilogue(k) instead of epilogue(k-1) -> compute(k), so one
+  // wave's epilogue VALU and stores overlap its partner's MFMAs instead of both
+  // waves of a SIMD storing at once after the tile barrier (MI355X_MICROARCH.md,
+  // "Two waves per SIMD" item 9: split roles by wave number >= 4)
+  int stagger;
 };
 
 constexpr int kHpAPW = 12;   // max halo DMA pieces per wave per tile
+// 8-wave blocks need at most 8 (BM 256 on 32 x 32 / 64 x 64 maps: 6 / 7): the
+// smaller bound frees 8 VGPRs of slot offsets in the register-capped kernel
+constexpr int hp_apw_max(int nw) { return nw == 8 ? 8 : kHpAPW; }
 
 __device__ __forceinline__ void wait_vm_n(int n) {
   switch (n) {
@@ -1238,6 +1247,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   constexpr int BK = 64, BN = 64, RPI = 8;
   constexpr int TM = BM / NW / 16, TN = BN / 16, KS = BK / 32, NSTEP = 9 * KS;
   constexpr int W_EL = 9 * BN * BK;
+  constexpr int APWMAX = hp_apw_max(NW);
   extern __shared__ __attribute__((aligned(16))) u16 lds_p[];
   const int APW = hg.APW;
   // NS = 2 drains the ring every tile (vmcnt(0)), so waves may issue unequal
@@ -1276,11 +1286,11 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   }
   // halo DMA slots: staged row -> element offset from the tile's first pixel +
   // {valid, image in tile, source row - h0}
-  int x_off[kHpAPW];
-  unsigned x_inf[kHpAPW];
+  int x_off[APWMAX];
+  unsigned x_inf[APWMAX];
   const int per_img = (TH + 2) * W2;
 #pragma unroll
-  for (int j = 0; j < kHpAPW; ++j) {
+  for (int j = 0; j < APWMAX; ++j) {
     x_off[j] = 0;
     x_inf[j] = 0;
     if (j < APW) {
@@ -1300,7 +1310,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     const int m0 = t * BM;
     const int b0 = m0 / img, h0 = (m0 - b0 * img) / W;
 #pragma unroll
-    for (int j = 0; j < kHpAPW; ++j) {
+    for (int j = 0; j < APWMAX; ++j) {
       if (j < APW && (NS != 2 || wid + j * NW < hg.AINS)) {
         const unsigned inf = x_inf[j];
         const int tb = (int)((inf >> 16) & 0x7fff), dh = (int)((inf >> 8) & 255) - 64;
@@ -1320,7 +1330,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   }
   const int rb = lane & 15;
   f32x4 acc[TM][TN];
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf, f32x4 (&dst)[TM][TN]) {
     const u16* As = Hs + buf * STAGE;
     // fragments prefetched PD steps ahead (PD = 2 when a step has <= 8 MFMAs:
     // one step's MFMAs alone do not cover an LDS read round trip at 1 wave/SIMD)
@@ -1352,7 +1362,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = mfma16(bw[st % NB][j], af[st % NB][i], acc[i][j]);
+          dst[i][j] = mfma16(bw[st % NB][j], af[st % NB][i], dst[i][j]);
       if (st + PD < NSTEP) {
 #pragma unroll
         for (int k = 0; k < TM + TN && k < TM * TN; ++k) {
@@ -1404,7 +1414,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   // this wave's DMA pieces per stage (issued after the addend loads)
   int dma_pw = 0;
 #pragma unroll
-  for (int j = 0; j < kHpAPW; ++j)
+  for (int j = 0; j < APWMAX; ++j)
     if (j < APW && (NS != 2 || wid + j * NW < hg.AINS)) ++dma_pw;
   // the store of one 16 x 16 fragment (i, j) of tile k from accumulators `src`
   auto epi_one = [&](int k, f32x4 (&src)[TM][TN], int i, int j) {
@@ -1466,7 +1476,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     const int m0 = t * BM;
     const int b0 = m0 / img, h0 = (m0 - b0 * img) / W;
 #pragma unroll
-    for (int j = 0; j < kHpAPW; ++j) {
+    for (int j = 0; j < APWMAX; ++j) {
       if (j < APW && (NS != 2 || wid + j * NW < hg.AINS)) {
         const unsigned inf = x_inf[j];
         const int tb = (int)((inf >> 16) & 0x7fff), dh = (int)((inf >> 8) & 255) - 64;
@@ -1482,30 +1492,56 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
       }
     }
   };
-  for (int k = 0; k < nt; ++k) {
-    if (NS == 2) wait_vm<0>();
-    else wait_vm_n(vm_wait);            // tile k (and, at k = 0, the weights) landed ...
-    if (!FLIP && hg.xform) xform_tile(k);
-    __builtin_amdgcn_s_barrier();       // ... for every wave; slot (k-1) % NS is free
-    asm volatile("" ::: "memory");
-    if (k > 0 && add_in) aload(k - 1);
-    if (DMP_ABLATE != 2) stage((k + NS - 1) % NS, k + NS - 1);
-    if (DMP_ABLATE == 3) {
+  // waves 4-7 of an 8-wave block: each tile's own stores right after its MFMAs
+  const bool late = NS == 2 && NW == 8 && DMP_ABLATE == 0 && hg.stagger && !add_in &&
+                    !hg.xform && wid >= 4;
+  if (late) {
+    for (int k = 0; k < nt; ++k) {
+      // tile k landed; the TM*TN youngest ops (tile k-1's stores, issued after
+      // tile k's DMA) may still be in flight (vmcnt retires in issue order)
+      if (k >= 1) wait_vm<TM * TN>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      stage((k + 1) % 2, k + 1);
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
-    } else if (k > 0) {
-      epilogue(k - 1, false);
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      compute(k % 2, acc);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) epi_one(k, acc, i, j);
     }
+  } else {
+    for (int k = 0; k < nt; ++k) {
+      if (NS == 2) wait_vm<0>();
+      else wait_vm_n(vm_wait);            // tile k (and, at k = 0, the weights) landed ...
+      if (!FLIP && hg.xform) xform_tile(k);
+      __builtin_amdgcn_s_barrier();       // ... for every wave; slot (k-1) % NS is free
+      asm volatile("" ::: "memory");
+      if (k > 0 && add_in) aload(k - 1);
+      if (DMP_ABLATE != 2) stage((k + NS - 1) % NS, k + NS - 1);
+      if (DMP_ABLATE == 3) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (DMP_ABLATE != 1) compute(DMP_ABLATE == 2 ? 0 : k % NS);
+          for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+      } else if (k > 0) {
+        epilogue(k - 1, false);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (DMP_ABLATE != 1) compute(DMP_ABLATE == 2 ? 0 : k % NS, acc);
+    }
+    if (add_in) aload(nt - 1);
+    if (DMP_ABLATE != 3) epilogue(nt - 1, true);
   }
-  if (add_in) aload(nt - 1);
-  if (DMP_ABLATE != 3) epilogue(nt - 1, true);
   if (STATS) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -1771,7 +1807,7 @@ static bool halop_geom(int cfg, int B, int H, int W, int C, int R, int S, int st
   h.HROWS = h.TB * (h.TH + 2) * (W + 2);
   h.AINS = (h.HROWS + 7) / 8;
   h.APW = (h.AINS + nw - 1) / nw;
-  if (h.APW > kHpAPW || (ns - 2) * h.APW > 24) return false;
+  if (h.APW > hp_apw_max(nw) || (ns - 2) * h.APW > 24) return false;
   const long long P = (long long)B * img;
   if (2LL * P * 64 >= (1LL << 31)) return false;
   h.ntiles = (int)((P + bm - 1) / bm);
@@ -1863,6 +1899,11 @@ static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
       return e && e[0] == '1' ? 1 : 0;
     }();
     pg.xform = xform_env;
+    static const int stagger_env = [] {
+      const char* e = getenv("DMP_HALO64P_STAGGER");
+      return e && e[0] == '1' ? 1 : 0;
+    }();
+    pg.stagger = stagger_env;
     pg.xs = 1.f;
     pg.xh = 0.f;
     pg.xlo = -INFINITY;
