@@ -1153,11 +1153,25 @@ void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
     const int sp = dmp::gemm_effective_splits((int)K, (int)std::max<int64_t>(1, splits));
     if (sp > 1) ws = at::empty({(int64_t)sp * M * N}, c.options().dtype(at::kFloat));
   }
+  // fwd / dgrad remainder split-K: per-call fp32 piece workspace + zeroed tickets
+  // (caching-allocator memory: safe inside a captured graph)
+  Tensor skw, skc;
+  if (mode != 2 && cfg >= 0 && splits > 1) {
+    long long wf = 0;
+    int nc = 0;
+    dmp::gemm_sk_sizes((int)cfg, (int)M, (int)N, (int)K, (int)splits, &wf, &nc);
+    if (wf > 0 && nc > 0) {
+      skw = at::empty({(int64_t)wf}, c.options().dtype(at::kFloat));
+      skc = at::zeros({(int64_t)nc}, c.options().dtype(at::kInt));
+    }
+  }
   dmp::launch_gemm((int)mode, (int)epi, (int)cfg, reinterpret_cast<const uint16_t*>(a.data_ptr()),
                    (int)lda, reinterpret_cast<const uint16_t*>(b.data_ptr()), (int)ldb,
                    c.data_ptr(), (int)ldc, c2p, biasp, auxp, dbp, (int)M, (int)N, (int)K,
                    (int)std::max<int64_t>(1, splits), cur_stream(), relu, partp,
-                   ws.defined() ? ws.data_ptr<float>() : nullptr);
+                   ws.defined() ? ws.data_ptr<float>() : nullptr,
+                   skw.defined() ? skw.data_ptr<float>() : nullptr,
+                   skc.defined() ? skc.data_ptr<int>() : nullptr);
 }
 
 std::vector<std::vector<int64_t>> gemm_configs() {
@@ -1745,6 +1759,14 @@ PYBIND11_MODULE(_native, m) {
         py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"));
   m.doc() = "gfx950 (MI355X) HIP kernels for distributed_ml_pytorch_amd";
   m.def("asgd_fused_step", &asgd_fused_step, "fused flat ASGD/SGD update");
+  m.def("gemm_sk_pieces",
+        [](int64_t cfg, int64_t M, int64_t N, int64_t K, int64_t splits) {
+          long long wf = 0;
+          int nc = 0;
+          dmp::gemm_sk_sizes((int)cfg, (int)M, (int)N, (int)K, (int)splits, &wf, &nc);
+          return nc > 0 ? wf / std::max<long long>(1, nc) : 0LL;
+        },
+        "fwd / dgrad remainder split-K: fp32 workspace floats per split tile (0 = no split)");
   m.def("ps_apply", &ps_apply, "parameter-server delta apply", py::arg("shard"), py::arg("delta"),
         py::arg("mirror") = py::none(), py::arg("scale") = 1.0, py::arg("atomic") = false);
   m.def("pull_land", &pull_land, "land a parameter pull into the worker arena");

@@ -72,6 +72,15 @@ struct GemmArgs {
                       // stored bf16 outputs (a 1x1 conv feeding a BatchNorm)
   float* slab;        // EPI_ACC32 split-K: per-split fp32 partials [splits][M][N] written
                       // with plain stores, summed into C by gemm_slab_reduce_kernel
+  // remainder split-K of the bf16-output passes (fwd / dgrad): blocks
+  // [0, sk_full) own whole tiles; the T - sk_full tiles of the last, partial
+  // round are cut into sk_split k-pieces of sk_kchunk reduction rows, one block
+  // each (launched last, so the short pieces fill the final round).  Every piece
+  // publishes its fp32 accumulators to sk_ws; the last to arrive (ticket in
+  // sk_cnt[tile], zeroed per call) adds the others and runs the epilogue.
+  int sk_full, sk_split, sk_kchunk;
+  float* sk_ws;
+  int* sk_cnt;
 };
 
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -238,14 +247,20 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
 
   // XCD-aware bijective remap of the tile id: blocks sharing an XCD take
   // consecutive tiles (neighbouring N tiles of one M panel)
-  const int G = gridDim.x, bid = blockIdx.x;
+  const int bid = blockIdx.x;
+  // remainder split-K piece (see GemmArgs): tile sk_full + rt, k-piece `piece`
+  const bool sk = TRANS_OUT && g.sk_split > 1 && bid >= g.sk_full;
+  const int rt = sk ? (bid - g.sk_full) / g.sk_split : 0;
+  const int piece = sk ? bid - g.sk_full - rt * g.sk_split : 0;
+  const int G = TRANS_OUT && g.sk_split > 1 ? g.sk_full : gridDim.x;   // whole-tile blocks
   const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = sk ? g.sk_full + rt
+                      : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int tm = tile / g.tiles_n;
   const int m0 = tm * BM, n0 = (tile - tm * g.tiles_n) * BN;
-  const int kbase = blockIdx.y * g.k_chunk;
-  const int kend = min(g.K, kbase + g.k_chunk) - kbase;
-  if (kend <= 0) return;
+  const int kbase = sk ? piece * g.sk_kchunk : blockIdx.y * g.k_chunk;
+  const int kend = min(g.K, kbase + (sk ? g.sk_kchunk : g.k_chunk)) - kbase;
+  if (kend <= 0) return;   // (the host sizes pieces so that none is empty)
   const int KT = (kend + BKS - 1) / BKS;
 
   SA sa;
@@ -309,7 +324,7 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
       for (int j = 0; j < TN; ++j) {
         const int n = n0 + rb + j * 16 + 4 * (lane >> 4);
         f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-        if (EPI != EPI_DGELU && EPI != EPI_DRELU && g.bias != nullptr && n < g.N) {
+        if (EPI != EPI_DGELU && EPI != EPI_DRELU && g.bias != nullptr && n < g.N && piece == 0) {
           const uint2 raw = *reinterpret_cast<const uint2*>(g.bias + n);
           bv = f32x4{__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
                      __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
@@ -588,6 +603,50 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
       accb[i] += *reinterpret_cast<const f32x4*>(park + ((wq * PT + TM * TN + i) * 64 + lane) * 4);
     }
   }
+  if constexpr (TRANS_OUT) {
+    if (sk) {
+      // publish this piece's fp32 accumulators in the lane-native layout (16 B per
+      // lane and fragment: whole lines), then take a ticket; the last piece to
+      // arrive adds the others' (agent-scope release / acquire: the pieces of a
+      // tile may run on any XCD, MI355X_MICROARCH.md "Workgroup dispatch")
+      constexpr int FR = TM * TN * 256;   // floats per wave
+      const int S = g.sk_split;
+      float* mine = g.sk_ws + ((long long)(rt * S + piece) * NW + wid) * FR;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          *reinterpret_cast<f32x4*>(mine + (i * TN + j) * 256 + lane * 4) = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // every wave's stores done; every wave past its last ring read
+      int* flag = reinterpret_cast<int*>(lds);
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(g.sk_cnt + rt, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == S - 1;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+      }
+      __syncthreads();
+      const bool last = *flag != 0;
+      __syncthreads();   // the flag is read before the epilogue reuses the LDS
+      if (!last) return;
+      for (int p = 0; p < S; ++p) {
+        if (p == piece) continue;
+        const float* other = g.sk_ws + ((long long)(rt * S + p) * NW + wid) * FR;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] += *reinterpret_cast<const f32x4*>(other + (i * TN + j) * 256 + lane * 4);
+      }
+    }
+  }
   epilogue(m0, n0);
 }
 
@@ -771,6 +830,48 @@ constexpr bool cfg_ok(const Cfg& c, bool at, bool bt) {
   return (!at || c.bm % 128 == 0) && (!bt || c.bn % 128 == 0) && (c.kg == 1 || (at && bt));
 }
 
+// blocks of a config resident per CU (LDS, and the 256-VGPR 8-wave tiles)
+constexpr int cfg_blocks_per_cu(const Cfg& c) {
+  const int lds = c.ns * (c.bm + c.bn) * c.bk * 2;
+  const int by_lds = (160 * 1024) / (lds > 0 ? lds : 1);
+  const int by_regs = (c.occ > 0 || c.wm * c.wn * c.kg <= 4) ? 2 : 1;
+  return by_lds < by_regs ? (by_lds < 1 ? 1 : by_lds) : by_regs;
+}
+
+int num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+// remainder split-K plan of a fwd / dgrad launch (GemmArgs sk_*): the whole
+// rounds as usual, the last round's `rem` tiles in `sp` k-pieces (fewer than
+// requested when the round has no room or K is short; sp = 1: no split)
+struct SkPlan { int full = 0, rem = 0, sp = 1, kchunk = 0; };
+SkPlan sk_plan(const Cfg& c, int M, int N, int K, int want) {
+  SkPlan p;
+  if (want <= 1) return p;
+  const int tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
+  const int slots = num_cus() * cfg_blocks_per_cu(c);
+  const int rem = tiles % slots;
+  const int kt = (K + c.bk - 1) / c.bk;
+  int sp = rem > 0 ? std::min(std::min(want, slots / rem), kt) : 1;
+  if (sp <= 1) return p;
+  const int kchunk = (kt + sp - 1) / sp * c.bk;
+  sp = (K + kchunk - 1) / kchunk;   // no empty piece
+  if (sp <= 1) return p;
+  p.full = tiles - rem;
+  p.rem = rem;
+  p.sp = sp;
+  p.kchunk = kchunk;
+  return p;
+}
+
 template <int C, bool AT, bool BT, int EPI>
 void launch_cfg(const GemmArgs& a, int splits, hipStream_t s) {
   constexpr Cfg c = kCfgs[C];
@@ -780,10 +881,23 @@ void launch_cfg(const GemmArgs& a, int splits, hipStream_t s) {
     GemmArgs g = a;
     g.tiles_n = (g.N + c.bn - 1) / c.bn;
     const int tiles = ((g.M + c.bm - 1) / c.bm) * g.tiles_n;
+    int grid_x = tiles, grid_y = splits;
+    if (EPI != EPI_ACC32 && g.sk_split > 1) {
+      const SkPlan p = sk_plan(c, g.M, g.N, g.K, g.sk_split);
+      g.sk_split = p.sp;
+      if (p.sp > 1) {
+        g.sk_full = p.full;
+        g.sk_kchunk = p.kchunk;
+        grid_x = p.full + p.rem * p.sp;
+      }
+      grid_y = 1;
+    } else {
+      g.sk_split = 1;
+    }
     if constexpr (c.kg == 1 || EPI == EPI_ACC32)
       hipLaunchKernelGGL((gemm_kernel<c.bm, c.bn, c.bk, c.wm, c.wn, c.ns, AT, BT, EPI, c.kg,
                                       c.pp != 0, c.occ>),
-                         dim3((unsigned)tiles, (unsigned)splits), dim3(64 * c.wm * c.wn * c.kg), 0,
+                         dim3((unsigned)grid_x, (unsigned)grid_y), dim3(64 * c.wm * c.wn * c.kg), 0,
                          s, g);
     else
       throw std::runtime_error("gemm: k-group configs are weight-gradient only");
@@ -837,12 +951,18 @@ void gemm_config_info(int cfg, int* info) {
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
-                 hipStream_t s, bool relu, float* part, float* slab) {
+                 hipStream_t s, bool relu, float* part, float* slab, float* sk_ws, int* sk_cnt) {
   GemmArgs g{};
   g.relu = relu ? 1 : 0;
   g.part = part;
   g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.aux = aux; g.dbias = dbias;
   g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  // fwd / dgrad: `splits` > 1 asks for the remainder split-K (needs sk_ws / sk_cnt)
+  if (mode != 2 && splits > 1 && cfg >= 0 && sk_ws != nullptr && sk_cnt != nullptr) {
+    g.sk_split = splits;
+    g.sk_ws = sk_ws;
+    g.sk_cnt = sk_cnt;
+  }
   if (splits < 1 || mode != 2) splits = 1;   // split-K only for the fp32-accumulating pass
   g.k_chunk = ((K + splits - 1) / splits + 63) / 64 * 64;   // whole k-tiles of any BK
   splits = (K + g.k_chunk - 1) / g.k_chunk;
@@ -864,6 +984,18 @@ void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const u
                          slab, reinterpret_cast<float*>(c), M, N, ldc, splits);
     }
   }
+}
+
+void gemm_sk_sizes(int cfg, int M, int N, int K, int splits, long long* ws_floats, int* counters) {
+  *ws_floats = 0;
+  *counters = 0;
+  if (cfg < 0 || cfg >= kNumCfgs || splits <= 1) return;
+  const Cfg& c = kCfgs[cfg];
+  if (c.kg != 1) return;
+  const SkPlan p = sk_plan(c, M, N, K, splits);
+  if (p.sp <= 1) return;
+  *ws_floats = (long long)p.rem * p.sp * c.bm * c.bn;
+  *counters = p.rem;
 }
 
 // effective split count launch_gemm uses for (K, requested splits) in mode 2

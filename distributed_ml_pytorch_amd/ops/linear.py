@@ -116,6 +116,17 @@ def _wgrad_splits(M: int, N: int, K: int, bm: int, bn: int):
     return out
 
 
+# opt-in (DMP_GEMM_SK=1): measured slower than the unsplit tiles on every ViT-B/16
+# fwd / dgrad shape -- the pieces' fp32 publish + combine costs more than the
+# partial round it recovers (profiles/gemm_remainder_splitk_r5.txt)
+_SK_SPLITS = (2, 4) if os.environ.get("DMP_GEMM_SK", "0") == "1" else ()
+
+
+def _sk_splits(cfg: int, M: int, N: int, K: int, s: int) -> bool:
+    """The fwd / dgrad remainder split-K plan of ``cfg`` splits at ``s``."""
+    return native().gemm_sk_pieces(cfg, M, N, K, s) > 0
+
+
 def _small_splits(mode: int, K: int) -> int:
     """Split-K of the any-shape kernel in wgrad mode: its blocks cover only a
     64x64 output tile, so a long reduction (a conv's B*OH*OW pixels) must be
@@ -148,6 +159,9 @@ def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bo
             cands += [_enc(cid, s, True) for s in _wgrad_splits(M, N, K, bm, bn) if s > 1]
         else:
             cands.append(_enc(cid, 1))
+            # remainder split-K (csrc/gemm.hip GemmArgs sk_*): the tiles of a last,
+            # partial round in k-pieces -- only where the plan actually splits
+            cands += [_enc(cid, s) for s in _SK_SPLITS if _sk_splits(cid, M, N, K, s)]
     if M * N * K < (1 << 22):
         cands += [_enc(_SMALL, s) for s in _small_split_options(mode, K)]
     if _GEMM_MODE == "auto" and plain and mode in (0, 1):

@@ -165,3 +165,77 @@ def test_gemm_persistent_many_tiles(mode):
         else:
             native().gemm(1, 0, cfg, a, w, out)
         assert _rel(out, ref) < 1e-2, cfg
+
+
+def _sk_shape(cfg, K, N, want=2):
+    """An M whose tile count leaves a last partial round that the remainder
+    split-K plan of ``cfg`` actually splits (depends on the CU count)."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    info = {c[0]: c for c in native().gemm_configs()}[cfg]
+    bm = info[1]
+    for tiles_m in range(8, 400):
+        M = tiles_m * bm - 37          # a row tail in the last M tile too
+        if native().gemm_sk_pieces(cfg, M, N, K, want) > 0:
+            return M
+    return None
+
+
+@pytest.mark.parametrize("mode,epi", [(0, "bias_addend"), (0, "gelu"), (1, "plain"),
+                                      (1, "dgelu"), (1, "drelu")])
+def test_gemm_remainder_split_k(mode, epi):
+    """fwd / dgrad with the last partial round's tiles split along K (csrc/gemm.hip
+    GemmArgs sk_*): every piece publishes fp32 partials, the last arriver adds them
+    and runs the epilogue -- against fp32 PyTorch and against the unsplit launch.
+    The bias / addend / GELU epilogues must be applied exactly once."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    torch.manual_seed(5)
+    dev = "cuda"
+    K, N = 520, 512
+    tried = 0
+    for cfg in [c for c in _cfgs(mode) if c >= 0]:
+        for want in (2, 4):
+            M = _sk_shape(cfg, K, N, want)
+            if M is None:
+                continue
+            tried += 1
+            b = torch.randn(N, device=dev).to(torch.bfloat16)
+            if mode == 0:
+                x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+                w = (torch.randn(N, K, device=dev) + 0.01 * torch.arange(N, device=dev)[:, None]
+                     ).to(torch.bfloat16)
+                r = torch.randn(M, N, device=dev).to(torch.bfloat16)
+                ref = x.float() @ w.float().t() + b.float()
+                y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+                y1 = torch.empty_like(y)
+                if epi == "bias_addend":
+                    native().gemm(0, 0, cfg, x, w, y, bias=b, aux=r, splits=want)
+                    native().gemm(0, 0, cfg, x, w, y1, bias=b, aux=r)
+                    assert _rel(y, ref + r.float()) < 1e-2, (cfg, want)
+                else:
+                    g = torch.empty_like(y)
+                    native().gemm(0, 1, cfg, x, w, y, c2=g, bias=b, splits=want)
+                    native().gemm(0, 1, cfg, x, w, y1, c2=torch.empty_like(y), bias=b)
+                    assert _rel(y, ref) < 1e-2 and _rel(g, _gelu(y.float())) < 1e-2, (cfg, want)
+                assert _rel(y, y1) < 4e-3, (cfg, want)
+            else:
+                dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+                w = (torch.randn(N, K, device=dev) + 0.01 * torch.arange(K, device=dev)[None, :]
+                     ).to(torch.bfloat16)
+                h = torch.randn(M, K, device=dev).to(torch.bfloat16)
+                ref = dy.float() @ w.float()
+                e, aux = 0, None
+                if epi == "dgelu":
+                    hr = h.float().requires_grad_(True)
+                    _gelu(hr).backward(ref)
+                    ref, e, aux = hr.grad, 2, h
+                elif epi == "drelu":
+                    ref, e, aux = ref * (h.float() > 0), 4, h
+                dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+                dx1 = torch.empty_like(dx)
+                native().gemm(1, e, cfg, dy, w, dx, aux=aux, splits=want)
+                native().gemm(1, e, cfg, dy, w, dx1, aux=aux)
+                assert _rel(dx, ref) < 1.5e-2, (cfg, want)
+                assert _rel(dx, dx1) < 4e-3, (cfg, want)
+    assert tried > 0
