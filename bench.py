@@ -252,10 +252,13 @@ def _timed_steps(w, pool, steps, warmup, ctx, clock=None):
             seen.append(loss)
     _sync()
     ctx.worker_barrier()
+    elapsed = time.perf_counter() - t0
+    if clock is not None:     # stopped outside the timed window
+        w.clock_reading = clock.stop()
     if trace:
         print("[trace] losses " + " ".join(f"{float(v.float()):.3g}" for v in seen)
               + f" |p| {w.param_norm():.4f}", file=sys.stderr, flush=True)
-    return time.perf_counter() - t0, loss
+    return elapsed, loss
 
 
 def time_to_target(a, cfg, ctx, mode=None):

@@ -1320,13 +1320,23 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     }
   };
 
-  int hrow[TM];
+  // per-lane LDS element offsets of every A fragment read at k-step 0, one per
+  // (fragment, tap): tile-invariant, computed ONCE.  (Recomputing row -> swizzled
+  // address per read was ~1.5 VALU per MFMA of this VALU-issue-heavy kernel:
+  // profiles/pmc_r5.txt.)  k-step 1 is the same offset with 16-B chunk bit 2
+  // flipped: (4 + g) ^ t == 4 ^ (g ^ t) for the BK = 64 swizzle, i.e. element ^ 32.
+  int aoff[TM][9];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int ml = wid * (BM / NW) + i * 16 + (lane & 15);
     const int tb = ml / (TH * W), r2 = ml - tb * TH * W;
     const int th = r2 / W, tw = r2 - th * W;
-    hrow[i] = (tb * (TH + 2) + th) * W2 + tw;
+    const int hrow = (tb * (TH + 2) + th) * W2 + tw;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int row = hrow + (t / 3) * W2 + (t % 3);
+      aoff[i][t] = row * BK + swz<BK>(row, lane >> 4) * 8;
+    }
   }
   const int rb = lane & 15;
   f32x4 acc[TM][TN];
@@ -1336,17 +1346,14 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     // one step's MFMAs alone do not cover an LDS read round trip at 1 wave/SIMD)
     constexpr int PD = (TM * TN <= 8 && NW == 4) ? 2 : 1, NB = PD + 1;
     bf16x8 af[NB][TM], bw[NB][TN];
+    static_assert(BK == 64 && KS == 2, "tap table: k-step 1 = element offset ^ 32");
     auto load = [&](int st, int slot) {
       if (DMP_ABLATE == 4 && st >= PD) return;
       const int t = st / KS, ks = st % KS;
-      const int rowoff = (t / 3) * W2 + (t % 3);
       const int wt = FLIP ? 8 - t : t;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = hrow[i] + rowoff;
-        af[slot][i] = *reinterpret_cast<const bf16x8*>(
-            As + row * BK + swz<BK>(row, ks * 4 + (lane >> 4)) * 8);
-      }
+      for (int i = 0; i < TM; ++i)
+        af[slot][i] = *reinterpret_cast<const bf16x8*>(As + (ks ? aoff[i][t] ^ 32 : aoff[i][t]));
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         bw[slot][j] = *reinterpret_cast<const bf16x8*>(
@@ -1377,12 +1384,18 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   };
 
   typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+  // conv bias: forward without BN statistics only (the eval-mode BN fold);
+  // the training forward (STATS) feeds a BatchNorm and has none -- the
+  // launcher routes a biased STATS conv elsewhere -- which frees 16 VGPRs of
+  // this register-capped kernel for the tap address table below
+  constexpr bool HAS_BIAS = !FLIP && !STATS;
   float bj[TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + j * 16 + 4 * (lane >> 4);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bj[j][r] = (!FLIP && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
+    for (int r = 0; r < 4; ++r)
+      bj[j][r] = (HAS_BIAS && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
   }
   float s_sum[TN][4], s_sq[TN][4];
 #pragma unroll
@@ -1434,7 +1447,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
     u16 hv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float t = src[i][j][r] + bj[j][r] + av[r];
+      float t = src[i][j][r] + (HAS_BIAS ? bj[j][r] : 0.f) + av[r];
       if (!FLIP && a.relu) t = fmaxf(t, 0.f);
       hv[r] = f2bf(t);
       if (STATS) {
@@ -1888,6 +1901,10 @@ static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
     // deferred epilogue runs with the next tile's DMA in flight): take the 4-wave
     // halo tile for those dgrads instead (a residual addend is fused: loaded ahead
     // of the DMA, see conv_halo64p_kernel)
+    // the persistent kernel's statistics forward carries no conv bias (HAS_BIAS)
+    if (!FLIP && STATS && a.bias != nullptr)
+      return launch_halo<FLIP, STATS>(a, kHaloBase + 9, s) ||
+             launch_halo<FLIP, STATS>(a, kHaloBase + 5, s);
     if (FLIP && (STATS || (a.addend != nullptr && a.addend_sub)))
       return launch_halo<FLIP, STATS>(a, kHaloBase + 9, s) ||
              launch_halo<FLIP, STATS>(a, kHaloBase + 5, s);

@@ -1,0 +1,128 @@
+#!/usr/bin/env python
+"""Same-process A/B of conv kernels between two source revisions.
+
+``python scripts/conv_ab.py build <git-rev>`` (CPU): compiles conv.hip +
+conv_wgrad.hip + csrc/ablate/ablate_entry.hip of the working tree and of
+``<git-rev>`` into ``distributed_ml_pytorch_amd/_ablate/ab_{new,old}.so``
+(ctypes entry points, never part of the extension).
+``python scripts/conv_ab.py run [cfg ...]`` (GPU): times fwd / dgrad of the
+ResNet-18 bs512 3x3 layers with both libraries in interleaved rounds in ONE
+process (median of 5 rounds x 20 calls) and checks that the two produce
+bit-identical outputs.  Default cfgs: the committed tuner picks per layer."""
+import ctypes
+import json
+import os
+import shutil
+import statistics
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "distributed_ml_pytorch_amd" / "csrc"
+LIBDIR = ROOT / "distributed_ml_pytorch_amd" / "_ablate"
+SRCS = ["conv.hip", "conv_wgrad.hip"]
+
+
+def _compile(srcdir: Path, out: Path):
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "-std=c++17", "--offload-arch=gfx950",
+           "-shared", "-DDMP_ABLATE=0", "-I", str(srcdir),
+           *[str(srcdir / s) for s in SRCS], str(srcdir / "ablate" / "ablate_entry.hip"),
+           "-Wl,--no-undefined", "-o", str(out)]
+    return subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+
+
+def build(rev: str):
+    LIBDIR.mkdir(exist_ok=True)
+    tmp = Path(tempfile.mkdtemp(prefix="conv_ab_"))
+    (tmp / "ablate").mkdir()
+    for f in CSRC.glob("*.h"):
+        rel = f"distributed_ml_pytorch_amd/csrc/{f.name}"
+        txt = subprocess.run(["git", "show", f"{rev}:{rel}"], cwd=ROOT, capture_output=True)
+        (tmp / f.name).write_bytes(txt.stdout if txt.returncode == 0 else f.read_bytes())
+    for s in SRCS + ["ablate/ablate_entry.hip"]:
+        rel = f"distributed_ml_pytorch_amd/csrc/{s}"
+        txt = subprocess.run(["git", "show", f"{rev}:{rel}"], cwd=ROOT, capture_output=True,
+                             check=True)
+        (tmp / s).write_bytes(txt.stdout)
+    procs = [_compile(CSRC, LIBDIR / "ab_new.so"), _compile(tmp, LIBDIR / "ab_old.so")]
+    for p in procs:
+        _, err = p.communicate()
+        if p.returncode:
+            raise SystemExit(err.decode()[-3000:])
+    shutil.rmtree(tmp)
+    print("built", LIBDIR / "ab_new.so", LIBDIR / "ab_old.so", f"(old = {rev})")
+
+
+def run(cfgs_arg):
+    sys.path.insert(0, str(ROOT))
+    import torch
+
+    libs = {k: ctypes.CDLL(str(LIBDIR / f"ab_{k}.so")) for k in ("old", "new")}
+    for lib in libs.values():
+        lib.abl_conv_fwd.restype = ctypes.c_int
+        lib.abl_conv_dgrad.restype = ctypes.c_int
+    tune = json.load(open(ROOT / "tuning" / "mi355x_tune_cache.json"))
+    P = ctypes.c_void_p
+    stream = P(torch.cuda.current_stream().cuda_stream)
+    CL = torch.channels_last
+    layers = [("s1 64ch 32x32", 512, 64, 32, 32, 64), ("s2 128ch 16x16", 512, 128, 16, 16, 128),
+              ("s3 256ch 8x8", 512, 256, 8, 8, 256), ("s4 512ch 4x4", 512, 512, 4, 4, 512)]
+    print(f"{'layer':16s} {'pass':5s} {'cfg':>5s} {'old us':>8s} {'new us':>8s} {'delta':>7s}  bitwise")
+    for name, B, CI, H, W, CO in layers:
+        g = torch.Generator(device="cuda").manual_seed(0)
+        x = torch.randn(B, CI, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+            memory_format=CL)
+        w = (0.05 * torch.randn(CO, CI, 3, 3, device="cuda", generator=g)).to(
+            torch.bfloat16).contiguous(memory_format=CL)
+        wt = w.permute(1, 2, 3, 0).contiguous()      # [CI][R][S][CO]
+        dy = torch.randn(B, CO, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+            memory_format=CL)
+        part = torch.zeros(2 * 64 * CO + 4, device="cuda")
+        for op in ("fwd", "dgrad"):
+            key = json.dumps([op, B, CI, H, W, CO, 3, 3, 1, 1]) if op == "fwd" else \
+                json.dumps([op, B, CO, H, W, CI, H, W, 3, 3, 1, 1])
+            cfgs = [int(c) for c in cfgs_arg] or ([tune[key]] if key in tune else [])
+            for cfg in cfgs:
+                outs, times = {}, {k: [] for k in libs}
+                for k, lib in libs.items():
+                    out = torch.empty(B, CO if op == "fwd" else CI, H, W, device="cuda",
+                                      dtype=torch.bfloat16).contiguous(memory_format=CL)
+                    outs[k] = out
+
+                def call(k):
+                    if op == "fwd":
+                        part.zero_()
+                        return libs[k].abl_conv_fwd(P(x.data_ptr()), P(w.data_ptr()),
+                                                    P(outs[k].data_ptr()), P(part.data_ptr()), B,
+                                                    H, W, CI, H, W, CO, 3, 3, 1, 1, cfg, stream)
+                    return libs[k].abl_conv_dgrad(P(dy.data_ptr()), P(wt.data_ptr()),
+                                                  P(outs[k].data_ptr()), B, H, W, CI, H, W, CO, 3,
+                                                  3, 1, 1, cfg, stream)
+                for k in libs:
+                    assert call(k) == 0, (k, op, cfg)
+                torch.cuda.synchronize()
+                same = torch.equal(outs["old"], outs["new"])
+                for _ in range(5):
+                    for k in libs:
+                        a = torch.cuda.Event(enable_timing=True)
+                        b = torch.cuda.Event(enable_timing=True)
+                        a.record()
+                        for _ in range(20):
+                            call(k)
+                        b.record()
+                        b.synchronize()
+                        times[k].append(a.elapsed_time(b) / 20 * 1e3)
+                to, tn = statistics.median(times["old"]), statistics.median(times["new"])
+                print(f"{name:16s} {op:5s} {cfg:5d} {to:8.1f} {tn:8.1f} {100 * (tn / to - 1):+6.1f}%  "
+                      f"{'yes' if same else 'NO'}", flush=True)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "build":
+        build(sys.argv[2])
+    elif len(sys.argv) > 1 and sys.argv[1] == "run":
+        run(sys.argv[2:])
+    else:
+        raise SystemExit(__doc__)

@@ -29,8 +29,11 @@ def main(paths):
                       f"LDS/MFMA = {vals.get('SQ_INSTS_LDS', 0) / max(vals['SQ_INSTS_MFMA'], 1):.2f}")
             if "TCC_HIT_sum" in vals and "TCC_MISS_sum" in vals:
                 print(f"    L2 hit rate = {vals['TCC_HIT_sum'] / max(vals['TCC_HIT_sum'] + vals['TCC_MISS_sum'], 1):.3f}")
-            if "SQ_BUSY_CYCLES" in vals and "SQ_WAVE_CYCLES" in vals and "SQ_WAVES" in vals:
-                pass
+            if "SQ_WAVE_CYCLES" in vals and "SQ_WAIT_ANY" in vals:
+                wc = max(vals["SQ_WAVE_CYCLES"], 1)
+                print(f"    of wave cycles: waiting (vmcnt/lgkmcnt/barrier) {vals['SQ_WAIT_ANY'] / wc:.3f}"
+                      f"  issue-stalled {vals.get('SQ_WAIT_INST_ANY', 0) / wc:.3f}"
+                      f"  issuing {vals.get('SQ_ACTIVE_INST_ANY', 0) / wc:.3f}")
             if "SQ_LDS_BANK_CONFLICT" in vals and "SQ_LDS_IDX_ACTIVE" in vals:
                 print(f"    LDS bank conflict / active = {vals['SQ_LDS_BANK_CONFLICT'] / max(vals['SQ_LDS_IDX_ACTIVE'], 1):.3f}")
 
