@@ -659,7 +659,8 @@ void zero_(Tensor t) {
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
                   int64_t cfg, optional<Tensor> wt_pre, optional<Tensor> addend,
                   optional<Tensor> bn_x, optional<Tensor> bn_mask, optional<Tensor> bn_stats,
-                  optional<Tensor> bn_part, int64_t bn_relu, bool addend_sub) {
+                  optional<Tensor> bn_part, int64_t bn_relu, bool addend_sub,
+                  optional<Tensor> addend_mask) {
   dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc_bf16(dy, "dy");
   check_gpu(w, "w");
@@ -704,6 +705,15 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
     }
     add_ptr = reinterpret_cast<const uint16_t*>(add_t.data_ptr());
   }
+  // deferred ReLU mask of the addend (the residual BN backward's dres not written)
+  const uint8_t* amask = nullptr;
+  if (addend_mask.has_value() && addend_mask->defined()) {
+    TORCH_CHECK(add_ptr != nullptr, "dgrad: addend_mask without an addend");
+    TORCH_CHECK(addend_mask->is_cuda() && addend_mask->scalar_type() == at::kByte &&
+                    addend_mask->is_contiguous() && addend_mask->numel() == add_t.numel() / 8,
+                "dgrad: addend_mask must be the addend's contiguous uint8 [pixels, C/8] bit mask");
+    amask = addend_mask->data_ptr<uint8_t>();
+  }
   // fused backward of the BatchNorm(+ReLU) that produced the conv input (bn_relu >= 0)
   dmp::BnBwdFuse bnf{};
   const bool fuse = bn_relu >= 0;
@@ -737,7 +747,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
                          reinterpret_cast<const uint16_t*>(wt.data_ptr()),
                          reinterpret_cast<uint16_t*>(dx.data_ptr()), B, g.H, g.W, g.CI, g.OH,
                          g.OW, g.CO, g.R, g.S, (int)stride, (int)pad, (int)cfg, cur_stream(),
-                         add_ptr, fuse ? &bnf : nullptr, add_ptr != nullptr && addend_sub);
+                         add_ptr, fuse ? &bnf : nullptr, add_ptr != nullptr && addend_sub,
+                         amask);
   return dx;
 }
 
@@ -1718,7 +1729,8 @@ PYBIND11_MODULE(_native, m) {
         py::arg("cfg") = -1, py::arg("wt") = py::none(), py::arg("addend") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
         py::arg("bn_stats") = py::none(), py::arg("bn_part") = py::none(),
-        py::arg("bn_relu") = -1, py::arg("addend_sub") = false);
+        py::arg("bn_relu") = -1, py::arg("addend_sub") = false,
+        py::arg("addend_mask") = py::none());
   m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of a channels_last bf16 activation",
         py::arg("x"));
   m.def("add_subsampled2", &add_subsampled2, "dx[:, :, ::2, ::2] += xs in place",

@@ -71,7 +71,13 @@ struct ConvArgs {
   // [B][ceil(H/2)][ceil(W/2)][CI] (a 1x1 / stride-2 shortcut that read x[::2, ::2]):
   // it lands on parity class (0, 0) only, indexed by the class-local row
   int addend_sub;
+  // dgrad: optional 1-bit mask of the addend ([pixels][CI/8] bytes, bn.hip's ReLU
+  // bit mask): addend element e counts only where its bit is set.  The residual
+  // BatchNorm's backward then hands its UNMASKED dY over as the residual gradient
+  // instead of writing dres = dY * relu' (ops/functional.py _BNAct, deferred dres)
+  const uint8_t* addmask;
 };
+
 
 // Data-gradient epilogue fused with the backward of the BatchNorm(+ReLU) whose
 // output the conv consumed (dgrad kernels instantiated with STATS): the kernel
@@ -111,6 +117,25 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t rs, unsigned voff,
   const unsigned m0 = (unsigned)(size_t)(__attribute__((address_space(3))) void*)lds_wave_base;
   asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
                "{m0}"(m0));
+}
+
+// addend channels n..n+3 at byte offset `boff` (= 2 * element offset) of the
+// addend, with the deferred ReLU mask applied when a.addmask is set
+__device__ __forceinline__ void masked_addend4(const ConvArgs& a, __amdgpu_buffer_rsrc_t rsAdd,
+                                               __amdgpu_buffer_rsrc_t rsAm, unsigned boff, bool ok,
+                                               int n, float (&ad)[4]) {
+  typedef unsigned int u32x2_m __attribute__((ext_vector_type(2)));
+  const u32x2_m av = __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? boff : kOOB, 0, 0);
+  ad[0] = __uint_as_float(av.x << 16);
+  ad[1] = __uint_as_float(av.x & 0xffff0000u);
+  ad[2] = __uint_as_float(av.y << 16);
+  ad[3] = __uint_as_float(av.y & 0xffff0000u);
+  if (a.addmask != nullptr) {
+    // byte (element offset / 8); channels n..n+3 are its bits (n & 4) .. +3
+    const unsigned bits = __builtin_amdgcn_raw_buffer_load_b8(rsAm, ok ? boff >> 4 : kOOB, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ad[r] = (bits >> ((n & 4) + r)) & 1u ? ad[r] : 0.f;
+  }
 }
 
 // q = n / d, r = n % d for 0 <= n < 2^24 with a float reciprocal (one
@@ -370,6 +395,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
   const bool add_in = a.addend != nullptr && (MODE == 0 || !a.addend_sub || blockIdx.z == 0);
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsAm = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(add_in && a.addmask ? (const void*)a.addmask : (const void*)a.y), 0,
+      (int)(a.B * a.OH * a.OW * (long long)a.CO / 8), 0x00020000);
   constexpr bool BNB = MODE == 1 && STATS;   // fused BN(+ReLU) backward
   const __amdgpu_buffer_rsrc_t rsBx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(BNB ? a.bnx : a.y), 0, (int)(2LL * a.B * a.OH * a.OW * a.CO), 0x00020000);
@@ -424,12 +452,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
       float ad[4] = {0.f, 0.f, 0.f, 0.f};
       if (add_in) {
         const unsigned aoff = a.addend_sub ? 2u * (unsigned)(m * a.CO) : rowoff;
-        const u32x2_t av =
-            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? aoff + 2u * n : kOOB, 0, 0);
-        ad[0] = __uint_as_float(av.x << 16);
-        ad[1] = __uint_as_float(av.x & 0xffff0000u);
-        ad[2] = __uint_as_float(av.y << 16);
-        ad[3] = __uint_as_float(av.y & 0xffff0000u);
+        masked_addend4(a, rsAdd, rsAm, aoff + 2u * n, ok, n, ad);
       }
       float xb[4] = {0.f, 0.f, 0.f, 0.f}, mk[4] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (BNB) {
@@ -560,6 +583,9 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
                          : (a.addend != nullptr);   // dgrad residual grad / fwd BN-fold residual
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsAm = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(add_in && a.addmask ? (const void*)a.addmask : (const void*)a.y), 0,
+      (int)(Mtot * a.CO / 8), 0x00020000);
   constexpr bool BNB = FLIP && STATS;   // fused BN(+ReLU) backward
   const __amdgpu_buffer_rsrc_t rsBx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(BNB ? a.bnx : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
@@ -611,12 +637,7 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
       float ad[4] = {0.f, 0.f, 0.f, 0.f};
       if (add_in) {
         const unsigned aoff = a.addend_sub ? 2u * (unsigned)(m * a.CO) : rowoff;
-        const u32x2_t av =
-            __builtin_amdgcn_raw_buffer_load_b64(rsAdd, ok ? aoff + 2u * n : kOOB, 0, 0);
-        ad[0] = __uint_as_float(av.x << 16);
-        ad[1] = __uint_as_float(av.x & 0xffff0000u);
-        ad[2] = __uint_as_float(av.y << 16);
-        ad[3] = __uint_as_float(av.y & 0xffff0000u);
+        masked_addend4(a, rsAdd, rsAm, aoff + 2u * n, ok, n, ad);
       }
       float xb[4] = {0.f, 0.f, 0.f, 0.f}, mk[4] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (BNB) {
@@ -755,8 +776,13 @@ __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&ac
       (void*)a.y, 0, (int)(2LL * Mtot * a.CO), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
+  // deferred ReLU mask of the addend (ConvArgs::addmask): one byte = this lane's 8 channels
+  const bool add_mask = add_in && a.addmask != nullptr;
+  const __amdgpu_buffer_rsrc_t rsAm = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(add_mask ? (const void*)a.addmask : (const void*)a.y), 0, (int)(Mtot * a.CO / 8),
+      0x00020000);
   constexpr int NR = (BM + NW * RPI - 1) / (NW * RPI);
-  unsigned off[NR];
+  unsigned off[NR], amb[NR];
   u32x4_t xa[NR];
 #pragma unroll
   for (int q = 0; q < NR; ++q) {
@@ -764,6 +790,9 @@ __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&ac
     const long long m = m0 + ml;
     off[q] = (ml < mv && m < Mtot && nok) ? 2u * (unsigned)(m * a.CO + n) : kOOB;
     if (add_in) xa[q] = __builtin_amdgcn_raw_buffer_load_b128(rsAdd, off[q], 0, 0);
+    amb[q] = add_mask ? __builtin_amdgcn_raw_buffer_load_b8(rsAm, off[q] != kOOB ? off[q] >> 4 : kOOB,
+                                                             0, 0)
+                      : 0xffu;
   }
   float s_sum[8], s_sq[8];
 #pragma unroll
@@ -776,7 +805,7 @@ __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&ac
       const bf16x8 xv = __builtin_bit_cast(bf16x8, xa[q]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float t = bf2f(v.v[e]) + bf2f(xv.v[e]);
+        float t = bf2f(v.v[e]) + ((amb[q] >> e) & 1u ? bf2f(xv.v[e]) : 0.f);
         if (relu) t = fmaxf(t, 0.f);
         v.v[e] = f2bf(t);
       }
@@ -1410,6 +1439,13 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * P * a.CO), 0x00020000);
   u32x2_a ad[TM][TN];
+  // deferred ReLU mask of the addend (ConvArgs::addmask): the 64 bits of the
+  // block's 64 channels of pixel m, one dwordx2 per fragment row i
+  const bool add_mask = add_in && a.addmask != nullptr;
+  const __amdgpu_buffer_rsrc_t rsAm = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(add_mask ? (const void*)a.addmask : (const void*)a.y), 0, (int)((long long)P * a.CO / 8),
+      0x00020000);
+  u32x2_a am[TM];
   auto aload = [&](int k) {
     const int m0 = tile_of(k) * BM;
 #pragma unroll
@@ -1421,6 +1457,13 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
         const unsigned off = (m < P && n < a.CO) ? 2u * (unsigned)(m * a.CO + n) : kOOB;
         asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(ad[i][j]) : "v"(off), "s"(rsAdd)
                      : "memory");
+      }
+      if (add_mask) {   // counted with the addend loads (issued before the next DMA)
+        const unsigned moff = m < P ? (unsigned)((m * a.CO + n0) >> 3) : kOOB;
+        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(am[i]) : "v"(moff), "s"(rsAm)
+                     : "memory");
+      } else {
+        am[i] = u32x2_a{0xffffffffu, 0xffffffffu};
       }
     }
   };
@@ -1443,6 +1486,11 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
       av[1] = __uint_as_float(ad[i][j].x & 0xffff0000u);
       av[2] = __uint_as_float(ad[i][j].y << 16);
       av[3] = __uint_as_float(ad[i][j].y & 0xffff0000u);
+      // mask bits of channels n..n+3: bit (n - n0) of the pixel's 64-bit word
+      const int nb = j * 16 + 4 * (lane >> 4);
+      const unsigned bits = (nb < 32 ? am[i].x >> nb : am[i].y >> (nb - 32)) & 0xfu;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) av[r] = (bits >> r) & 1u ? av[r] : 0.f;
     }
     u16 hv[4];
 #pragma unroll
@@ -1466,9 +1514,11 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
       if (last) wait_vm<0>();
       else wait_vm_n(dma_pw);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(ad[i][j]));
+        asm volatile("" : "+v"(am[i]));
+      }
     }
   };
   auto epilogue = [&](int k, bool last) {
@@ -2050,11 +2100,12 @@ void launch_conv_fwd(const u16* x, const u16* w, u16* y, float* part, int B, int
 void launch_conv_dgrad(const u16* dy, const u16* wt, u16* dx, int B, int H, int W, int CI,
                        int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s, const u16* addend, const BnBwdFuse* bnf,
-                       bool addend_sub) {
+                       bool addend_sub, const uint8_t* addend_mask) {
   const long long rows = (long long)B * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);
   ConvArgs a{dy, wt, dx, nullptr, B, OH, OW, CO, H, W, CI, R, S, stride, pad, rows, nullptr,
              addend};
   a.addend_sub = addend_sub ? 1 : 0;
+  a.addmask = addend ? addend_mask : nullptr;
   if (bnf) {
     a.part = bnf->part;
     a.bnx = bnf->x;

@@ -174,7 +174,8 @@ struct BnBwdFuse {
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int B, int H, int W,
                        int CI, int OH, int OW, int CO, int R, int S, int stride, int pad, int cfg,
                        hipStream_t s, const uint16_t* addend = nullptr,
-                       const BnBwdFuse* bnf = nullptr, bool addend_sub = false);
+                       const BnBwdFuse* bnf = nullptr, bool addend_sub = false,
+                       const uint8_t* addend_mask = nullptr);
 // x_sub = x[:, ::2, ::2, :] (NHWC bf16, C % 8 == 0), [B][ceil(H/2)][ceil(W/2)][C]
 void launch_subsample2(const uint16_t* x, uint16_t* xs, int B, int H, int W, int C,
                        hipStream_t s);

@@ -23,7 +23,7 @@ import torch.nn as nn
 
 from ..ops import layers as L
 from ..ops.eval_fold import conv_bn, fold_enabled
-from ..ops.functional import bn_relu_maxpool, bn_relu_maxpool_ok
+from ..ops.functional import bn_relu_maxpool, bn_relu_maxpool_ok, mark_residual_only
 from ..ops.linear import gap_linear, gap_linear_ok
 
 
@@ -80,7 +80,9 @@ class BasicBlock(nn.Module):
             sc = self.shortcut[1](self.shortcut[0](xa, stride=1))
         else:
             sc = self.shortcut(xa)
-        return self.bn2(self.conv2(h), residual=sc)
+        # sc feeds only bn2: its backward may hand dY over unmasked (deferred
+        # residual mask) to conv1's dgrad epilogue or the shortcut BN
+        return self.bn2(self.conv2(h), residual=mark_residual_only(sc))
 
 
 class Bottleneck(nn.Module):
@@ -127,7 +129,10 @@ class Bottleneck(nn.Module):
             sc = self.shortcut[1](self.shortcut[0](xa, stride=1))
         else:
             sc = self.shortcut(xa)
-        return self.bn3(self.conv3(h), residual=sc)
+        # projection blocks only: the identity alias's consumer here is a 1x1
+        # conv1 on the GEMM route, whose epilogue takes no deferred mask
+        return self.bn3(self.conv3(h),
+                        residual=sc if self.shortcut is None else mark_residual_only(sc))
 
 
 class ResNet(nn.Module):

@@ -31,7 +31,8 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from ._ext import native
-from .functional import is_relu_masked, set_nonneg
+from .functional import (DEFER_RES_STATS, apply_bitmask, deferred_mask, is_relu_masked,
+                         resolve_deferred, set_nonneg)
 from .tuner import TUNER
 
 _NATIVE_ENABLED = True
@@ -306,7 +307,18 @@ class _NativeConv(Function):
     @staticmethod
     def backward(ctx, dy, _dpart, dxa=None):
         if dy is None:
-            return None, None, None, None, None, None, None, None, dxa, None
+            # only the alias output received a gradient: it is x's whole gradient
+            dx = None
+            if dxa is not None and ctx.needs_input_grad[0]:
+                dxa = resolve_deferred(dxa)
+                if ctx.alias_sub:
+                    x = ctx.saved_tensors[0]
+                    dx = torch.zeros(x.shape, dtype=dxa.dtype, device=dxa.device).contiguous(
+                        memory_format=torch.channels_last)
+                    dx[:, :, ::2, ::2] = dxa
+                else:
+                    dx = dxa
+            return dx, None, None, None, None, None, None, None, None, None
         x, w16, y = ctx.saved_tensors
         H, W, stride, pad = ctx.geom
         masked = is_relu_masked(dy)           # the consumer applied relu'(y) already
@@ -315,6 +327,15 @@ class _NativeConv(Function):
             dy = native().relu_bwd(dy, y)
         dx = None
         master = ctx.master
+        # residual gradient handed over unmasked (ops/functional.py deferred
+        # residual mask): the native dgrad epilogue applies the bit mask; every
+        # other use of dxa gets the masked tensor
+        amask = deferred_mask(dxa)
+        if amask is not None and (ctx.alias_sub or not ctx.needs_input_grad[0]
+                                  or _dgrad_cfg(dy, w16, H, W, stride, pad) == _GEMM_ROUTE):
+            dxa, amask = apply_bitmask(dxa, amask), None
+        elif amask is not None:
+            DEFER_RES_STATS["native"] += 1
         sub = ctx.alias_sub and dxa is not None
         sub_after = None          # subsampled alias gradient added after the dgrad
         if sub and not ctx.needs_input_grad[0]:
@@ -340,11 +361,11 @@ class _NativeConv(Function):
                                          bn_mask=(x if bn.relu == 1 else
                                                   bn.mask if bn.relu == 3 else None),
                                          bn_stats=bn.stats, bn_part=bn.part, bn_relu=bn.relu,
-                                         addend_sub=sub)
+                                         addend_sub=sub, addend_mask=amask)
                 bn.fused = (dx, dx._version)
             else:
                 dx = native().conv_dgrad(dy, w16, H, W, stride, pad, cfg, wt, dxa,
-                                         addend_sub=sub)
+                                         addend_sub=sub, addend_mask=amask)
         elif dxa is not None:
             dx = dxa
         if sub_after is not None:
@@ -680,6 +701,9 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
                                             slots if want_stats and not relu else None, b,
                                             alias if alias == "sub" else bool(alias),
                                             bool(relu))
+            if xa is not None:
+                # (the object apply() returned: x handed back is a new view of x)
+                xa._dmp_conv_alias = True   # its gradient may carry a deferred mask
             if part is not None:
                 y._dmp_bn_part = part
             set_nonneg(y, relu)

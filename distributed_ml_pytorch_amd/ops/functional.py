@@ -60,6 +60,63 @@ def is_relu_masked(t) -> bool:
     return t is not None and getattr(t, "_dmp_relu_masked_ver", None) == t._version
 
 
+# ------------------------------------------------ deferred residual-gradient mask
+# The backward of a BatchNorm + residual + ReLU (bn2 of a BasicBlock) owes its
+# residual input dres = dY * relu'(.): an activation-sized write (67 MB at the
+# ResNet-18 bs512 stage 1) that the residual's consumer reads straight back.  When
+# the block marks the residual as consumed ONLY by that BatchNorm
+# (``mark_residual_only``) and it was produced by a consumer that understands the
+# hand-off -- the alias output of a native conv (its dgrad adds the gradient in
+# the epilogue) or a native BatchNorm (its backward reduce / apply mask dY) --
+# the BN backward skips dres and passes dY itself with its 1-bit ReLU mask
+# attached; the consumer applies the mask where it reads the gradient
+# (csrc/conv.hip ConvArgs::addmask, or bn.hip's mode-3 kernels).  Any other
+# path materialises the masked tensor first (``resolve_deferred``).
+_BN_DEFER_RES = os.environ.get("DMP_BN_DEFER_RES", "1") != "0"
+# hand-offs by outcome (diagnostics / tests): made, masked inside a native
+# consumer kernel, materialised by apply_bitmask
+DEFER_RES_STATS = {"deferred": 0, "native": 0, "materialized": 0}
+
+
+def mark_residual_only(t):
+    """Declare that ``t`` is consumed only as a BatchNorm residual (single use)."""
+    if t is not None:
+        t._dmp_residual_only = True
+    return t
+
+
+def defer_tag(t, mask):
+    t._dmp_defer_mask = (mask, t._version)
+    return t
+
+
+def deferred_mask(t):
+    """The ReLU bit mask still owed by gradient ``t`` (None: ``t`` is final)."""
+    tag = getattr(t, "_dmp_defer_mask", None) if t is not None else None
+    if tag is None:
+        return None
+    if tag[1] != t._version:
+        # single use was declared: nothing may accumulate into the hand-off
+        raise RuntimeError("deferred residual gradient was modified in place")
+    return tag[0]
+
+
+def apply_bitmask(t, mask):
+    """``t * bit`` of the [pixels, C/8] uint8 ReLU mask (channels_last NCHW ``t``)."""
+    DEFER_RES_STATS["materialized"] += 1
+    N, C, H, W = t.shape
+    rows = t.permute(0, 2, 3, 1).contiguous().view(-1, 8)
+    shifts = torch.arange(8, dtype=torch.uint8, device=t.device)
+    keep = ((mask.view(-1, 1) >> shifts) & 1).bool()
+    out = torch.where(keep, rows, torch.zeros((), dtype=t.dtype, device=t.device))
+    return out.view(N, H, W, C).permute(0, 3, 1, 2)
+
+
+def resolve_deferred(t):
+    m = deferred_mask(t)
+    return t if m is None else apply_bitmask(t, m)
+
+
 def nonneg(t) -> bool:
     """``t`` is known >= 0 (the output of a fused ReLU, or a dropout of one)."""
     return bool(getattr(t, "_dmp_nonneg", False))
@@ -242,6 +299,9 @@ class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
                 relu, part=None, slots=None):
+        res_handoff = residual is not None and bool(
+            getattr(residual, "_dmp_residual_only", False)
+            and (getattr(residual, "_dmp_bn_out", False) or getattr(residual, "_dmp_conv_alias", False)))
         if x.dim() == 4:
             x = x.contiguous(memory_format=CL)
             if residual is not None:
@@ -289,6 +349,10 @@ class _BNAct(Function):
             y._dmp_bnlink = ctx.link
         ctx.relu = relu
         ctx.has_res = residual is not None
+        # dres handed over unmasked with the bit mask (see deferred residual mask)
+        ctx.defer_res = bool(_BN_DEFER_RES and ctx.fold and res_handoff and mask is not None
+                             and x.dim() == 4)
+        y._dmp_bn_out = True
         ctx.gamma, ctx.beta = gamma, beta
         # the backward re-derives the ReLU mask from x and the folded scale/shift
         # unless a residual entered the forward (then the bit mask, or y)
@@ -300,6 +364,11 @@ class _BNAct(Function):
     def backward(ctx, dy):
         x, y, stats, mask = ctx.saved_tensors
         gamma, beta = ctx.gamma, ctx.beta
+        # a residual hand-off from the BatchNorm this one feeds: ReLU-free folded
+        # passes take the owed mask as their own (mode 3); others materialise it
+        in_mask = deferred_mask(dy)
+        if in_mask is not None and not (ctx.fold and not ctx.relu and not ctx.has_res):
+            dy, in_mask = apply_bitmask(dy, in_mask), None
         dg_arena, db_arena = _arena_grad(gamma), _arena_grad(beta)
         need_g = gamma is not None and ctx.needs_input_grad[1]
         need_b = beta is not None and ctx.needs_input_grad[2]
@@ -323,8 +392,17 @@ class _BNAct(Function):
             else:
                 dy = dy.contiguous()
             bs = _fresh_slots(ctx.bslots, x.shape[1], x.device)
-            dx, dres = native().bn_bwd_fold(x, dy, y, gamma, stats, dg, db, ctx.relu, ctx.has_res,
-                                            bs, mask, ctx.fpart)
+            if in_mask is not None:
+                DEFER_RES_STATS["native"] += 1
+                dx, dres = native().bn_bwd_fold(x, dy, None, gamma, stats, dg, db, True, False,
+                                                bs, in_mask, ctx.fpart)
+            else:
+                dx, dres = native().bn_bwd_fold(x, dy, y, gamma, stats, dg, db, ctx.relu,
+                                                ctx.has_res and not ctx.defer_res, bs, mask,
+                                                ctx.fpart)
+                if ctx.defer_res:
+                    dres = defer_tag(dy, mask)
+                    DEFER_RES_STATS["deferred"] += 1
             mark_slots(bs, True)
             mark_slots(ctx.fpart, False)
             ctx.fpart = None

@@ -756,3 +756,63 @@ def test_stride2_halo_dgrad_configs(B, CI, H, CO):
         assert _rel(dxa, ref + add.float()) < 1e-2, cfg
         dxs = nat.conv_dgrad(dy, w, H, H, 2, 1, cfg, addend=sub, addend_sub=True)
         assert _rel(dxs, ref_sub) < 1e-2, cfg
+
+
+@pytest.mark.parametrize("B,C,H", [(4, 64, 32), (3, 128, 16), (8, 256, 8), (8, 512, 4)])
+def test_dgrad_addend_bitmask(B, C, H):
+    """Deferred residual mask (ops/functional.py): the data-gradient epilogue
+    applying the 1-bit ReLU mask to its addend (ConvArgs::addmask) == the same
+    dgrad with the addend masked beforehand, bitwise, on every tile family that
+    takes an addend: halo tiles (row-staged epilogue), the persistent 64-channel
+    kernel (hand-counted mask loads) and the implicit GEMM."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+    from distributed_ml_pytorch_amd.ops.functional import apply_bitmask
+
+    nat = native()
+    torch.manual_seed(3)
+    dy = torch.randn(B, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(C, C, 3, 3, device="cuda") / (C * 9) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    add = torch.randn_like(dy)
+    mask = torch.randint(0, 256, (B * H * H * C // 8,), device="cuda", dtype=torch.uint8)
+    masked = apply_bitmask(add, mask).contiguous(memory_format=CL)
+    # the torch fallback itself against an explicit bit unpack
+    bits = torch.stack([(mask >> k) & 1 for k in range(8)], 1).view(B, H, H, C).permute(0, 3, 1, 2)
+    assert torch.equal(masked.float(), torch.where(bits.bool(), add.float(), 0.0))
+    cfgs = list(nat.conv_halo_configs(H, H, C, 3, 3, 1, 1)) + [0, 3, -1]
+    for cfg in cfgs:
+        ref = nat.conv_dgrad(dy, w, H, H, 1, 1, cfg, None, masked)
+        got = nat.conv_dgrad(dy, w, H, H, 1, 1, cfg, None, add, addend_mask=mask)
+        assert torch.equal(got, ref), (cfg, (got.float() - ref.float()).abs().max())
+
+
+@pytest.mark.parametrize("stride,cin,planes", [(1, 64, 64), (2, 64, 128)])
+def test_resnet_block_deferred_dres(stride, cin, planes, monkeypatch):
+    """BasicBlock backward with bn2's residual gradient handed over unmasked
+    (identity: into conv1's dgrad epilogue; projection: into the shortcut BN's
+    mode-3 passes) == the materialised-dres path (DMP_BN_DEFER_RES=0), and
+    nothing is materialised on the way."""
+    from distributed_ml_pytorch_amd.models.resnet import BasicBlock
+    from distributed_ml_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(0)
+    blk = BasicBlock(cin, planes, stride).cuda()
+    x0 = torch.randn(8, cin, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    g = torch.randn(8, planes, 16 // stride, 16 // stride, device="cuda")
+    grads = {}
+    for defer in (False, True):
+        monkeypatch.setattr(Fn, "_BN_DEFER_RES", defer)
+        before = dict(Fn.DEFER_RES_STATS)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        (blk(x).float() * g).sum().backward()
+        torch.cuda.synchronize()
+        grads[defer] = [x.grad.float()] + [p.grad.float() for p in blk.parameters()]
+        d = {k: Fn.DEFER_RES_STATS[k] - before[k] for k in before}
+        if defer:
+            assert d["deferred"] == 1 and d["native"] == 1 and d["materialized"] == 0, d
+        else:
+            assert d["deferred"] == 0, d
+    for a, b in zip(grads[False], grads[True]):
+        # fp32 atomics order the BN / wgrad sums differently run to run
+        assert _rel(b, a) < 5e-3, _rel(b, a)

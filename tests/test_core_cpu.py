@@ -334,3 +334,28 @@ def test_stream_layer_norm_cpu_matches_two_consumers():
     ref = x2 * 2.0 + F.layer_norm(x2, (16,), w.detach(), b.detach(), 1e-6) * 3.0
     ref.sum().backward()
     torch.testing.assert_close(x.grad, x2.grad)
+
+
+def test_deferred_residual_mask_helpers():
+    """ops/functional.py deferred residual mask: apply_bitmask unpacks bn.hip's
+    [pixels, C/8] byte mask (bit k of byte e = NHWC element 8e + k), a tag is
+    bound to the tensor's version, and an in-place change is refused."""
+    import pytest
+
+    from distributed_ml_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(0)
+    t = torch.randn(2, 16, 3, 5).contiguous(memory_format=torch.channels_last)
+    keep = torch.rand(2, 3, 5, 16) > 0.5                       # NHWC
+    packed = (keep.view(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(
+        1).to(torch.uint8)
+    out = Fn.apply_bitmask(t, packed)
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(out, torch.where(keep.permute(0, 3, 1, 2), t, torch.zeros(())))
+    assert Fn.deferred_mask(t) is None and Fn.resolve_deferred(t) is t
+    Fn.defer_tag(t, packed)
+    assert Fn.deferred_mask(t) is packed
+    assert torch.equal(Fn.resolve_deferred(t), out)
+    t.add_(1.0)
+    with pytest.raises(RuntimeError):
+        Fn.deferred_mask(t)
