@@ -879,6 +879,19 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   const float rcp_pi = 1.f / (float)per_img, rcp_w2 = 1.f / (float)HW2;
   const float rcp_tw = 1.f / (float)(TH * W), rcp_w = 1.f / (float)W;
 
+  // Halo-image chunk swizzle.  A 16-pixel fragment on an image of width W <= 8
+  // spans 16 / W image rows whose staged rows are W2 = W + 2 apart, not 16
+  // consecutive rows: the row-bit swizzle of swz<32> then maps half of each
+  // ds_read_b128 lane group onto the other half's slots (2 LDS cycles per read
+  // on the 8 x 8 and 4 x 4 ResNet-18 stages, 40 % bank-conflict cycles measured
+  // by PMC).  There the XOR key is the parity of the staged image row (row / W2)
+  // instead -- conflict-free for every fragment and tap of those tiles (checked
+  // exhaustively over the lane groups of gfx950's b128 reads); W >= 16 keeps
+  // swz<32>.  qrow = row / W2 of the staged row.
+  const bool qsw = BK == 32 && W <= 8 && 16 % W == 0;
+  auto hswz = [&](int row, int qrow, int c) {
+    return qsw ? c ^ ((qrow & 1) << 1) : swz<BK>(row, c);
+  };
   // halo DMA slots: lane's row of each 1-KiB piece -> (image, h, w) of the
   // source pixel; positions outside the image (or past the batch) read zeros
   unsigned a_base[kHaloAPW];
@@ -892,7 +905,8 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
     const int b = b0 + tb, h = h0 - 1 + hh, w = ww - 1;
     const bool ok = ins < hg.A_INS && row < hg.HROWS && b < a.B && (unsigned)h < (unsigned)H &&
                     (unsigned)w < (unsigned)W;
-    a_base[j] = ok ? 2u * (unsigned)(((b * H + h) * W + w) * C + swz<BK>(row, lane % CPR) * 8)
+    a_base[j] = ok ? 2u * (unsigned)(((b * H + h) * W + w) * C +
+                                     hswz(row, tb * (TH + 2) + hh, lane % CPR) * 8)
                    : kOOB;
   }
   // weight DMA slots: row = tap * BN + output channel
@@ -934,8 +948,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // halo row of each of the lane's output pixels at tap (0, 0)
-  int hrow[TM];
+  // LDS element offset of each A fragment read, per (fragment, tap), computed
+  // once (k-step 0; BK = 32 has one): the staged row of the lane's output pixel
+  // at tap (0, 0) plus the tap's row / column shift, swizzled (hswz)
+  static_assert(BK == 32, "conv_halo_kernel: one 32-deep k-step per tap");
+  int aoff[TM][9];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     int ml = wm * (BM / WM) + i * 16 + (lane & 15);
@@ -943,7 +960,12 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
     int tb, r2, th, tw;
     small_divmod(ml, TH * W, rcp_tw, tb, r2);
     small_divmod(r2, W, rcp_w, th, tw);
-    hrow[i] = (tb * (TH + 2) + th) * HW2 + tw;
+    const int q0 = tb * (TH + 2) + th, hrow = q0 * HW2 + tw;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int row = hrow + (t / 3) * HW2 + t % 3;
+      aoff[i][t] = row * BK + hswz(row, q0 + t / 3, lane >> 4) * 8;
+    }
   }
   int offB[BK / 32];
   {
@@ -963,14 +985,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
     auto load = [&](int st, int slot) {
       if (DMP_ABLATE == 4 && st >= 2) return;
       const int t = st / KS, ks = st % KS;
-      const int rowoff = (t / 3) * HW2 + (t % 3);
       const int wt = FLIP ? 8 - t : t;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = hrow[i] + rowoff;
-        af[slot][i] = *reinterpret_cast<const bf16x8*>(
-            As + row * BK + swz<BK>(row, ks * 4 + (lane >> 4)) * 8);
-      }
+      for (int i = 0; i < TM; ++i) af[slot][i] = *reinterpret_cast<const bf16x8*>(As + aoff[i][t]);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         bw[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + wt * BN * BK + offB[ks] + j * 16 * BK);
