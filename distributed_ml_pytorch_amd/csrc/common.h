@@ -29,6 +29,18 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 struct alignas(16) bf16x8 { u16 v[8]; };
 struct alignas(8) bf16x4 { u16 v[4]; };
 
+// 512-thread workgroups put two waves on each SIMD; the second-dispatched half
+// (waves 4-7) loses VALU-issue arbitration (priority, then age) on every
+// segment.  One static s_setprio 1 for that half before the main loop, no
+// per-segment flips (MI355X_MICROARCH.md "Two waves per SIMD", item 4).
+// DMP_PRIO_YOUNG=0 at compile time for A/B.
+#ifndef DMP_PRIO_YOUNG
+#define DMP_PRIO_YOUNG 1
+#endif
+__device__ __forceinline__ void prio_young_half(int wid) {
+  if (DMP_PRIO_YOUNG && wid >= 4) __builtin_amdgcn_s_setprio(1);
+}
+
 __device__ __forceinline__ float bf2f(u16 h) {
   return __uint_as_float(((u32)h) << 16);
 }

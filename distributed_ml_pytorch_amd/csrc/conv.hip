@@ -1016,6 +1016,9 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
     }
   };
 
+  // 8-wave tiles: waves 4-7 at priority 1 (s4 fwd / dgrad -1.8 / -2.1 %,
+  // profiles/prio_young_half_r5.txt)
+  if (NW == 8) prio_young_half(wid);
   const int KC = C / BK;
   if constexpr (NS == 2) {
     stage(0, 0);
@@ -1575,6 +1578,8 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   // waves 4-7 of an 8-wave block: each tile's own stores right after its MFMAs
   const bool late = NS == 2 && NW == 8 && DMP_ABLATE == 0 && hg.stagger && !add_in &&
                     !hg.xform && wid >= 4;
+  // (no static priority for waves 4-7 here: s1 dgrad +3 %, fwd +0.4 %,
+  // profiles/prio_young_half_r5.txt -- the stagger already orders the halves)
   if (late) {
     for (int k = 0; k < nt; ++k) {
       // tile k landed; the TM*TN youngest ops (tile k-1's stores, issued after
