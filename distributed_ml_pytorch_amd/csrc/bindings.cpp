@@ -1077,7 +1077,8 @@ int64_t mat_ld(const Tensor& t, at::ScalarType dt, int64_t rows, int64_t cols,
 // mode 1: a [M,K], b [K,N]; mode 2: a [K,M], b [K,N], c fp32 accumulated.
 void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
           optional<Tensor> c2, optional<Tensor> bias, optional<Tensor> aux,
-          optional<Tensor> dbias, int64_t splits, bool relu, optional<Tensor> part, bool slab) {
+          optional<Tensor> dbias, int64_t splits, bool relu, optional<Tensor> part, bool slab,
+          optional<Tensor> auxmask) {
   TORCH_CHECK(!relu || epi == 0, "gemm: relu only with the store epilogue");
   TORCH_CHECK(mode >= 0 && mode <= 2, "gemm: mode must be 0 (fwd), 1 (dgrad) or 2 (wgrad)");
   TORCH_CHECK(c.dim() == 2 && a.dim() == 2 && b.dim() == 2, "gemm: 2-D operands expected");
@@ -1109,6 +1110,17 @@ void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
     TORCH_CHECK(epi == 0 || epi == 2 || epi == 4, "gemm: aux only with epilogues 0 / 2 / 4");
     same_as_c(*aux, "aux");
     auxp = reinterpret_cast<const uint16_t*>(aux->data_ptr());
+  }
+  // deferred ReLU bit mask of the addend (ops/functional.py deferred residual mask)
+  const uint8_t* amp = nullptr;
+  if (auxmask.has_value() && auxmask->defined()) {
+    TORCH_CHECK(auxp != nullptr && epi == 0 && cfg >= 0,
+                "gemm: auxmask needs an addend, the store epilogue and an MFMA tile config");
+    TORCH_CHECK(ldc == N && N % 8 == 0, "gemm: auxmask needs a dense output with N % 8 == 0");
+    TORCH_CHECK(auxmask->is_cuda() && auxmask->scalar_type() == at::kByte &&
+                    auxmask->is_contiguous() && auxmask->numel() == M * N / 8,
+                "gemm: auxmask must be a contiguous uint8 [M * N / 8] GPU tensor");
+    amp = auxmask->data_ptr<uint8_t>();
   }
   TORCH_CHECK(epi != 2 || auxp != nullptr, "gemm: GELU-backward epilogue needs aux = h");
   TORCH_CHECK(epi != 4 || auxp != nullptr, "gemm: ReLU-backward epilogue needs aux = the input");
@@ -1182,7 +1194,7 @@ void gemm(int64_t mode, int64_t epi, int64_t cfg, Tensor a, Tensor b, Tensor c,
                    (int)std::max<int64_t>(1, splits), cur_stream(), relu, partp,
                    ws.defined() ? ws.data_ptr<float>() : nullptr,
                    skw.defined() ? skw.data_ptr<float>() : nullptr,
-                   skc.defined() ? skc.data_ptr<int>() : nullptr);
+                   skc.defined() ? skc.data_ptr<int>() : nullptr, amp);
 }
 
 std::vector<std::vector<int64_t>> gemm_configs() {
@@ -1836,7 +1848,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("mode"), py::arg("epi"), py::arg("cfg"), py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("c2") = py::none(), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("dbias") = py::none(), py::arg("splits") = 1, py::arg("relu") = false,
-        py::arg("part") = py::none(), py::arg("slab") = false);
+        py::arg("part") = py::none(), py::arg("slab") = false, py::arg("auxmask") = py::none());
   m.def("im2col", &im2col, "NHWC patch rows [B*OH*OW, Kp], k = (r, s, ci), zero-padded",
         py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("Kp"));
   m.def("col2im", &col2im, "gather-form inverse of im2col -> channels_last dX", py::arg("dcols"),

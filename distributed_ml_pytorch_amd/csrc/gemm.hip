@@ -62,6 +62,9 @@ struct GemmArgs {
   u16* c2;            // EPI_GELU: gelu(h) [M][ldc]  (h itself goes to c)
   const u16* bias;    // EPI_STORE / EPI_GELU: bf16 [N] (optional)
   const u16* aux;     // EPI_STORE: bf16 addend [M][ldc] (optional); EPI_DGELU: h [M][ldc]
+  const uint8_t* auxmask;   // EPI_STORE: optional 1-bit mask of the addend (bit e of byte
+                            // (m * ldc + n) / 8 keeps element (m, n + e); ldc == N): the
+                            // residual gradient's deferred ReLU mask (ops/functional.py)
   float* dbias;       // EPI_ACC32: fp32 [M] += sum_k A(m, k) (optional)
   int M, N, K;
   int lda, ldb, ldc;
@@ -421,6 +424,19 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
         for (int q = 0; q < (has_aux_slots(EPI) ? NR : 1); ++q)
           xa[q] = __builtin_amdgcn_raw_buffer_load_b128(rsX, o[q], 0, 0);
       }
+      // deferred ReLU mask of the addend: one byte = this lane's 8 columns (the
+      // host allows it only with ldc == N, 16-B row segments)
+      const bool amask = EPI == EPI_STORE && has_aux && g.auxmask != nullptr && !narrow;
+      unsigned mb[EPI == EPI_STORE ? NR : 1];
+      if constexpr (EPI == EPI_STORE) {
+        const __amdgpu_buffer_rsrc_t rsM = __builtin_amdgcn_make_buffer_rsrc(
+            amask ? (void*)g.auxmask : g.c, 0, cbytes / 16, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+          mb[q] = amask ? __builtin_amdgcn_raw_buffer_load_b8(rsM, o[q] != kOOBg ? o[q] >> 4 : kOOBg,
+                                                             0, 0)
+                        : 0xffu;
+      }
       __syncthreads();            // every wave is done reading the ring
       u16* wl = lds + wid * (WROWS * PITCH);
 #pragma unroll
@@ -456,7 +472,7 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
         for (int e = 0; e < 8; ++e) {
           const float a = bf2f(v.v[e]);
           if constexpr (EPI == EPI_STORE) {
-            float t = has_aux ? a + bf2f(xv.v[e]) : a;
+            float t = has_aux ? a + ((mb[q] >> e) & 1u ? bf2f(xv.v[e]) : 0.f) : a;
             if (g.relu) t = fmaxf(t, 0.f);
             out.v[e] = (has_aux || g.relu) ? f2bf(t) : v.v[e];
           } else if constexpr (EPI == EPI_GELU) {
@@ -951,8 +967,10 @@ void gemm_config_info(int cfg, int* info) {
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
-                 hipStream_t s, bool relu, float* part, float* slab, float* sk_ws, int* sk_cnt) {
+                 hipStream_t s, bool relu, float* part, float* slab, float* sk_ws, int* sk_cnt,
+                 const uint8_t* auxmask) {
   GemmArgs g{};
+  g.auxmask = aux != nullptr && epi == EPI_STORE ? auxmask : nullptr;
   g.relu = relu ? 1 : 0;
   g.part = part;
   g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.aux = aux; g.dbias = dbias;

@@ -241,7 +241,8 @@ void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const u
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,
                  hipStream_t s, bool relu = false, float* part = nullptr,
-                 float* slab = nullptr, float* sk_ws = nullptr, int* sk_cnt = nullptr);
+                 float* slab = nullptr, float* sk_ws = nullptr, int* sk_cnt = nullptr,
+                 const uint8_t* auxmask = nullptr);
 // remainder split-K of a fwd / dgrad launch_gemm (splits > 1): fp32 workspace
 // floats and ticket counters it needs for (cfg, M, N, K, splits); 0 = not split
 void gemm_sk_sizes(int cfg, int M, int N, int K, int splits, long long* ws_floats, int* counters);

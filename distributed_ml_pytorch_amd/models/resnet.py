@@ -129,10 +129,9 @@ class Bottleneck(nn.Module):
             sc = self.shortcut[1](self.shortcut[0](xa, stride=1))
         else:
             sc = self.shortcut(xa)
-        # projection blocks only: the identity alias's consumer here is a 1x1
-        # conv1 on the GEMM route, whose epilogue takes no deferred mask
-        return self.bn3(self.conv3(h),
-                        residual=sc if self.shortcut is None else mark_residual_only(sc))
+        # sc feeds only bn3 (deferred residual mask: the identity alias's consumer
+        # is conv1's 1x1 GEMM-route dgrad, whose store epilogue applies the mask)
+        return self.bn3(self.conv3(h), residual=mark_residual_only(sc))
 
 
 class ResNet(nn.Module):

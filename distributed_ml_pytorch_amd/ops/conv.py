@@ -173,14 +173,15 @@ def _gemm1x1_fwd(x, w16, part=None, relu=False):
     return y2.view(B, H, W, CO).permute(0, 3, 1, 2)
 
 
-def _gemm1x1_dgrad(dy, w16, addend=None):
+def _gemm1x1_dgrad(dy, w16, addend=None, addend_mask=None):
     from .linear import gemm
 
     B, CO, H, W = dy.shape
     CI = w16.shape[1]
     dx2 = torch.empty(B * H * W, CI, dtype=dy.dtype, device=dy.device)
     aux = _rows_nhwc(addend) if addend is not None else None
-    gemm(1, 0, _rows_nhwc(dy), w16.reshape(CO, CI), dx2, aux=aux)
+    gemm(1, 0, _rows_nhwc(dy), w16.reshape(CO, CI), dx2, aux=aux,
+         auxmask=addend_mask if aux is not None else None)
     return dx2.view(B, H, W, CI).permute(0, 3, 1, 2)
 
 
@@ -331,8 +332,7 @@ class _NativeConv(Function):
         # residual mask): the native dgrad epilogue applies the bit mask; every
         # other use of dxa gets the masked tensor
         amask = deferred_mask(dxa)
-        if amask is not None and (ctx.alias_sub or not ctx.needs_input_grad[0]
-                                  or _dgrad_cfg(dy, w16, H, W, stride, pad) == _GEMM_ROUTE):
+        if amask is not None and (ctx.alias_sub or not ctx.needs_input_grad[0]):
             dxa, amask = apply_bitmask(dxa, amask), None
         elif amask is not None:
             DEFER_RES_STATS["native"] += 1
@@ -346,7 +346,7 @@ class _NativeConv(Function):
         elif sub and (stride != 2 or _dgrad_cfg(dy, w16, H, W, stride, pad) == _GEMM_ROUTE):
             sub_after, dxa, sub = dxa.contiguous(memory_format=torch.channels_last), None, False
         if ctx.needs_input_grad[0] and _dgrad_cfg(dy, w16, H, W, stride, pad) == _GEMM_ROUTE:
-            dx = _gemm1x1_dgrad(dy, w16, dxa)
+            dx = _gemm1x1_dgrad(dy, w16, dxa, amask)
         elif ctx.needs_input_grad[0]:
             cfg = _dgrad_cfg(dy, w16, H, W, stride, pad)
             wt = None

@@ -112,6 +112,15 @@ def apply_bitmask(t, mask):
     return out.view(N, H, W, C).permute(0, 3, 1, 2)
 
 
+def apply_bitmask_rows(t, mask):
+    """``apply_bitmask`` for a dense row-major [M, N] (N % 8 == 0) operand."""
+    DEFER_RES_STATS["materialized"] += 1
+    rows = t.contiguous().view(-1, 8)
+    shifts = torch.arange(8, dtype=torch.uint8, device=t.device)
+    keep = ((mask.view(-1, 1) >> shifts) & 1).bool()
+    return torch.where(keep, rows, torch.zeros((), dtype=t.dtype, device=t.device)).view(t.shape)
+
+
 def resolve_deferred(t):
     m = deferred_mask(t)
     return t if m is None else apply_bitmask(t, m)

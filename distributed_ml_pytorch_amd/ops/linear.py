@@ -189,12 +189,15 @@ def _blas(mode, a, b, c, bias):
 
 
 def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None, relu=False,
-         part=None):
+         part=None, auxmask=None):
     """C = epilogue(A(m,k) B(n,k)) on the native kernels (see csrc/gemm.hip):
     mode 0 fwd (a [M,K], b [N,K]), 1 dgrad (a [M,K], b [K,N]), 2 wgrad (a [K,M],
     b [K,N], fp32 c accumulated); epi 0 store(+bias,+aux), 1 GELU, 2 x gelu'(aux),
     3 fp32 accumulate (+dbias).  ``part``: BatchNorm slot sums [2][64][N] of the
-    stored outputs (epi 0, MFMA tiles; a 1x1 conv feeding a BatchNorm)."""
+    stored outputs (epi 0, MFMA tiles; a 1x1 conv feeding a BatchNorm).
+    ``auxmask``: 1-bit mask of ``aux`` ([M * N / 8] uint8, bn.hip's ReLU mask
+    layout) applied by the epilogue; materialised first where the picked kernel
+    takes none (library GEMM, any-shape fallback, strided output)."""
     M, N = c.shape
     K = a.shape[0] if mode == 2 else a.shape[1]
     if M == 0 or N == 0:
@@ -231,12 +234,17 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
             pick = TUNER.best(key, run, cands)
             if pick == -1:
                 pick = _default(mode, M, N, K, ok)
+    if auxmask is not None and (pick == _BLAS or _dec(pick)[0] < 0 or epi != 0
+                                or c.stride(0) != N or N % 8):
+        from .functional import apply_bitmask_rows
+
+        aux, auxmask = apply_bitmask_rows(aux, auxmask), None
     if pick == _BLAS:
         _blas(mode, a, b, c, bias)
         return
     cfg, splits = _dec(pick)
     native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits, relu, part,
-                  _dec_slab(pick))
+                  _dec_slab(pick), auxmask)
 
 
 def _rows(t, k):

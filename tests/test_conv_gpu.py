@@ -816,3 +816,35 @@ def test_resnet_block_deferred_dres(stride, cin, planes, monkeypatch):
     for a, b in zip(grads[False], grads[True]):
         # fp32 atomics order the BN / wgrad sums differently run to run
         assert _rel(b, a) < 5e-3, _rel(b, a)
+
+
+@pytest.mark.parametrize("stride,cin,planes", [(1, 256, 64), (2, 256, 128)])
+def test_bottleneck_deferred_dres(stride, cin, planes, monkeypatch):
+    """Bottleneck backward with bn3's residual gradient deferred: identity shortcut ->
+    conv1's 1x1 data gradient (GEMM route or implicit GEMM) masks its addend in the
+    epilogue; projection -> the shortcut BN's mode-3 passes.  Matches the
+    materialised-dres path, nothing materialised."""
+    from distributed_ml_pytorch_amd.models.resnet import Bottleneck
+    from distributed_ml_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(0)
+    blk = Bottleneck(cin, planes, stride).cuda()
+    x0 = torch.randn(4, cin, 14, 14, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    oh = (14 + stride - 1) // stride
+    g = torch.randn(4, planes * 4, oh, oh, device="cuda")
+    grads = {}
+    for defer in (False, True):
+        monkeypatch.setattr(Fn, "_BN_DEFER_RES", defer)
+        before = dict(Fn.DEFER_RES_STATS)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        (blk(x).float() * g).sum().backward()
+        torch.cuda.synchronize()
+        grads[defer] = [x.grad.float()] + [p.grad.float() for p in blk.parameters()]
+        d = {k: Fn.DEFER_RES_STATS[k] - before[k] for k in before}
+        if defer:
+            assert d["deferred"] == 1 and d["native"] == 1 and d["materialized"] == 0, d
+        else:
+            assert d["deferred"] == 0, d
+    for a, b in zip(grads[False], grads[True]):
+        assert _rel(b, a) < 5e-3, _rel(b, a)

@@ -239,3 +239,34 @@ def test_gemm_remainder_split_k(mode, epi):
                 assert _rel(dx, ref) < 1.5e-2, (cfg, want)
                 assert _rel(dx, dx1) < 4e-3, (cfg, want)
     assert tried > 0
+
+
+def test_gemm_store_addend_bitmask():
+    """Store epilogue with a deferred ReLU bit mask on its addend (GemmArgs::auxmask,
+    the residual gradient of a Bottleneck's identity shortcut) == the same GEMM with
+    the addend masked beforehand, bitwise, on every MFMA config; the wrapper
+    materialises the mask for the library / fallback picks."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+    from distributed_ml_pytorch_amd.ops.functional import apply_bitmask_rows
+
+    nat = native()
+    torch.manual_seed(5)
+    M, N, K = 1000, 256, 192
+    dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(K, N, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    aux = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    mask = torch.randint(0, 256, (M * N // 8,), device="cuda", dtype=torch.uint8)
+    masked = apply_bitmask_rows(aux, mask)
+    ref32 = dy.float() @ w.float() + masked.float()
+    ran = 0
+    for c in [c[0] for c in nat.gemm_configs()]:
+        if not nat.gemm_config_ok(1, c):
+            continue
+        ran += 1
+        ref = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        got = torch.empty_like(ref)
+        nat.gemm(1, 0, c, dy, w, ref, aux=masked)
+        nat.gemm(1, 0, c, dy, w, got, aux=aux, auxmask=mask)
+        assert torch.equal(got, ref), c
+        assert (got.float() - ref32).norm() / ref32.norm() < 1e-2
+    assert ran > 0
