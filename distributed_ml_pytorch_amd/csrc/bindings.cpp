@@ -1622,6 +1622,8 @@ std::vector<Tensor> bn_bwd_fold(Tensor x, Tensor dy, optional<Tensor> y, optiona
                 "bn: ReLU bit mask must be a contiguous uint8 [M, C/8] GPU tensor");
     mptr = mask->data_ptr<uint8_t>();
   }
+  // [3][C] coefficient hand-off of the one-pass kernel (bn.hip bn_bwd_onepass_kernel)
+  auto coef = at::empty({3 * C}, fopt);
   dmp::launch_bn_bwd_fold(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                           reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                           have_y ? reinterpret_cast<const uint16_t*>(y->data_ptr()) : nullptr,
@@ -1629,7 +1631,7 @@ std::vector<Tensor> bn_bwd_fold(Tensor x, Tensor dy, optional<Tensor> y, optiona
                           ptr_or_null<float>(dgamma), ptr_or_null<float>(dbeta),
                           part.data_ptr<float>(), zb, reinterpret_cast<uint16_t*>(dx.data_ptr()),
                           want_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr, M,
-                          (int)C, relu, cur_stream(), mptr);
+                          (int)C, relu, cur_stream(), mptr, coef.data_ptr<float>());
   return {dx, want_dres ? dres : Tensor()};
 }
 

@@ -674,6 +674,236 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fold_kernel(
   }
 }
 
+// -------- one-pass backward: reduce -> device-wide hand-off -> apply ----------
+// The folded backward above is two launches per BatchNorm (bn_partial_kernel,
+// then bn_bwd_apply_fold_kernel).  Here ONE launch of G blocks (G <= what the
+// device holds at once: every block must be resident, see the host) does both:
+//   1. each block reduces sum dz / sum dz*xhat over ITS rows [start, end) into
+//      the kBnSlots slot sums (device-scope atomics, memory side);
+//   2. arrival ticket (agent-scope release + atomic add on the slot buffer's
+//      tail word 0); the LAST block to arrive (acquire) folds the slot sums into
+//      the dx coefficients [3][C] (coef), accumulates dgamma / dbeta, then
+//      publishes tail word 1 = 1 (release); the others poll it (acquire);
+//   3. every block applies dx = k1*dz + Cc*x + kb to the SAME rows it reduced --
+//      re-read from L2 / the Infinity Cache a moment after phase 1 streamed them.
+// Tail words reset for the next call: word 0 by the last arriver before it
+// releases, word 1 by the last block to depart (tail word 2 counts departures),
+// so the slot buffer's tail is zero again when the kernel ends.  The poll is
+// bounded (~0.1 s): a grid that could not be co-resident ends with wrong dx
+// instead of hanging the GPU, and sets tail word 3 (a test reads it).
+// Slot hygiene as in the fold kernels: the forward slots (zero_buf) are zeroed
+// here, the backward slots by the next forward apply.
+template <int RELU, bool WRITE_DRES>
+__global__ void __launch_bounds__(256) bn_bwd_onepass_kernel(
+    const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
+    const uint8_t* __restrict__ mask, float* __restrict__ part, float* __restrict__ zero_buf,
+    const float* __restrict__ gamma, const float* __restrict__ stats, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ coef, u16* __restrict__ dx,
+    u16* __restrict__ dres, long long M, int C) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int last_flag;
+  const int tpr = C >> 3, rpi = 256 / tpr;
+  const int t = threadIdx.x, cg = t % tpr, r0 = t / tpr;
+  const int G = gridDim.x;
+  const long long rows_per_blk = (M + G - 1) / G;
+  const long long start = (long long)blockIdx.x * rows_per_blk;
+  const long long end = min(M, start + rows_per_blk);
+  int* tail = reinterpret_cast<int*>(part + 2LL * kBnSlots * C);
+  const int c0 = cg * 8;
+  float msc[8], msh[8];
+  if (RELU == 2) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      msc[k] = r0 < rpi ? stats[2 * C + c0 + k] : 0.f;
+      msh[k] = r0 < rpi ? stats[3 * C + c0 + k] : 0.f;
+    }
+  }
+  // dz of 8 channels from the loaded vectors (ReLU mask by mode)
+  auto dz8 = [&](const bf16x8& xr, const bf16x8& dr, const bf16x8& yr, unsigned mb, float xv[8],
+                 float g[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      xv[k] = bf2f(xr.v[k]);
+      g[k] = bf2f(dr.v[k]);
+      if (RELU == 1) g[k] = bf2f(yr.v[k]) > 0.f ? g[k] : 0.f;
+      if (RELU == 2) {
+        const float yy = fmaxf(bn_pre(xv[k], msc[k], msh[k]), 0.f);
+        g[k] = bf2f(f2bf(yy)) > 0.f ? g[k] : 0.f;
+      }
+    }
+    if (RELU == 3) relu_mask_bits(mb, g);
+  };
+  constexpr int U = 4;
+  auto load_rows = [&](long long row, bf16x8 (&xr)[U], bf16x8 (&dr)[U], bf16x8 (&yr)[U],
+                       unsigned (&mb)[U], int nu) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < nu) {
+        const long long off = (row + u * rpi) * C + c0;
+        xr[u] = *reinterpret_cast<const bf16x8*>(x + off);
+        dr[u] = *reinterpret_cast<const bf16x8*>(dy + off);
+        if (RELU == 1) yr[u] = *reinterpret_cast<const bf16x8*>(y + off);
+        if (RELU == 3) mb[u] = mask[off >> 3];
+      }
+    }
+  };
+  // ---- phase 1: this block's partial sums
+  {
+    float s[8], q[8], mean[8], inv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s[k] = 0.f;
+      q[k] = 0.f;
+      mean[k] = r0 < rpi ? stats[c0 + k] : 0.f;
+      inv[k] = r0 < rpi ? stats[C + c0 + k] : 0.f;
+    }
+    if (r0 < rpi) {
+      for (long long row = start + r0; row < end; row += U * rpi) {
+        const int nu = (int)min<long long>(U, (end - row + rpi - 1) / rpi);
+        bf16x8 xr[U], dr[U], yr[U];
+        unsigned mb[U];
+        load_rows(row, xr, dr, yr, mb, nu);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u < nu) {
+            float xv[8], g[8];
+            dz8(xr[u], dr[u], yr[u], mb[u], xv, g);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              s[k] += g[k];
+              q[k] += g[k] * (xv[k] - mean[k]) * inv[k];
+            }
+          }
+        }
+      }
+    }
+    float* ls = smem;            // [rpi][C]
+    float* lq = smem + rpi * C;  // [rpi][C]
+    if (r0 < rpi) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { ls[r0 * C + c0 + k] = s[k]; lq[r0 * C + c0 + k] = q[k]; }
+    }
+    __syncthreads();
+    const int slot = blockIdx.x % kBnSlots;
+    for (int c = t; c < C; c += 256) {
+      float a = 0.f, b = 0.f;
+      for (int r = 0; r < rpi; ++r) { a += ls[r * C + c]; b += lq[r * C + c]; }
+      atomicAdd(part + (long long)slot * C + c, a);
+      atomicAdd(part + (long long)(kBnSlots + slot) * C + c, b);
+    }
+  }
+  // the forward slots this layer's forward apply consumed: zero (rows spread)
+  if (zero_buf != nullptr)
+    for (long long e = (long long)blockIdx.x * 256 + t; e < 2LL * kBnSlots * C; e += 256LL * G)
+      zero_buf[e] = 0.f;
+  // ---- phase 2: arrival; the last block folds the sums into the coefficients
+  __syncthreads();   // every thread's slot atomics are issued
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int ticket = __hip_atomic_fetch_add(tail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_flag = ticket == G - 1;
+  }
+  __syncthreads();
+  if (last_flag) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const float invM = 1.f / (float)M;
+    for (int c = t; c < C; c += 256) {
+      float db = 0.f, dg = 0.f;
+      // plain loads after the acquire (independent, so they pipeline; atomic
+      // loads here serialised into one round trip each)
+      float a[kBnSlots], b[kBnSlots];
+#pragma unroll
+      for (int sl = 0; sl < kBnSlots; ++sl) {
+        a[sl] = part[(long long)sl * C + c];
+        b[sl] = part[(long long)(kBnSlots + sl) * C + c];
+      }
+#pragma unroll
+      for (int sl = 0; sl < kBnSlots; ++sl) { db += a[sl]; dg += b[sl]; }
+      if (dgamma) dgamma[c] += dg;
+      if (dbeta) dbeta[c] += db;
+      const float mean = stats[c], inv = stats[C + c];
+      const float k1 = (gamma ? gamma[c] : 1.f) * inv;
+      const float Cc = -k1 * inv * dg * invM;
+      coef[c] = k1;
+      coef[C + c] = -k1 * db * invM - Cc * mean;
+      coef[2 * C + c] = Cc;
+    }
+    __syncthreads();
+    if (t == 0) {
+      __hip_atomic_store(tail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(tail + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if (t == 0) {
+    int it = 0;
+    while (__hip_atomic_load(tail + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > (1 << 22)) {   // never co-resident: give up (wrong dx, no hang)
+        __hip_atomic_store(tail + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  float ka[8], kb[8], kc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    ka[k] = r0 < rpi ? coef[c0 + k] : 0.f;
+    kb[k] = r0 < rpi ? coef[C + c0 + k] : 0.f;
+    kc[k] = r0 < rpi ? coef[2 * C + c0 + k] : 0.f;
+  }
+  __syncthreads();   // every thread has its coefficients before the departure below
+  if (t == 0) {      // departure: the last block out re-arms the release flag
+    const int d = __hip_atomic_fetch_add(tail + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == G - 1) {
+      __hip_atomic_store(tail + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(tail + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // ---- phase 3: apply to this block's rows
+  if (r0 < rpi) {
+    for (long long row = start + r0; row < end; row += U * rpi) {
+      const int nu = (int)min<long long>(U, (end - row + rpi - 1) / rpi);
+      bf16x8 xr[U], dr[U], yr[U];
+      unsigned mb[U];
+      load_rows(row, xr, dr, yr, mb, nu);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u < nu) {
+          const long long off = (row + u * rpi) * C + c0;
+          float xv[8], g[8], o[8];
+          dz8(xr[u], dr[u], yr[u], mb[u], xv, g);
+          if (WRITE_DRES) store8(dres + off, g);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = ka[k] * g[k] + kc[k] * xv[k] + kb[k];
+          store8(dx + off, o);
+        }
+      }
+    }
+  }
+}
+
+// blocks of the one-pass backward: 1 per CU (co-resident with room to spare: 256 threads,
+// <= 16 KiB of LDS, 3-4 blocks fit a CU), fewer when the rows run out; 0 = two launches
+static int onepass_blocks(long long M, int C) {
+  static const int mode = [] {
+    const char* e = std::getenv("DMP_BN_BWD_ONEPASS");
+    return e ? std::atoi(e) : 0;   // opt-in until it measures faster in the step
+  }();
+  if (mode == 0 || C % 8 != 0 || C > 2048) return 0;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const long long rpi = 256 / (C / 8);
+  long long g = std::min<long long>(cus, (M + 4 * rpi - 1) / (4 * rpi));
+  return (int)std::max<long long>(1, g);
+}
+
 static int fold_cs(int C) { return C % 64 == 0 ? 64 : C % 32 == 0 ? 32 : C % 16 == 0 ? 16 : 8; }
 
 // row blocks per slice: >= 4 vectors per thread (DMP_BN_FOLD_VPT), at most 1024
@@ -737,11 +967,30 @@ void launch_bn_fwd_fold(const u16* x, const u16* res, u16* y, const float* gamma
 void launch_bn_bwd_fold(const u16* x, const u16* dy, const u16* y, const float* gamma,
                         const float* stats, float* dgamma, float* dbeta, float* part,
                         float* zero_buf, u16* dx, u16* dres, long long M, int C, bool relu,
-                        hipStream_t s, const uint8_t* mask) {
+                        hipStream_t s, const uint8_t* mask, float* coef) {
   const int G = bn_num_partials(M, C);
   const int rpi = 256 / (C / 8);
   const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
   const int mode = !relu ? 0 : (mask ? 3 : (y ? 1 : 2));
+  const int G1 = coef != nullptr ? onepass_blocks(M, C) : 0;
+  if (G1 > 0) {
+#define DMP_BN_ONE(R, D)                                                                       \
+  hipLaunchKernelGGL((bn_bwd_onepass_kernel<R, D>), dim3(G1), dim3(256), lds, s, x, dy, y, mask, \
+                     part, zero_buf, gamma, stats, dgamma, dbeta, coef, dx, dres, M, C)
+    if (dres) {
+      if (mode == 0) DMP_BN_ONE(0, true);
+      else if (mode == 1) DMP_BN_ONE(1, true);
+      else if (mode == 2) DMP_BN_ONE(2, true);
+      else DMP_BN_ONE(3, true);
+    } else {
+      if (mode == 0) DMP_BN_ONE(0, false);
+      else if (mode == 1) DMP_BN_ONE(1, false);
+      else if (mode == 2) DMP_BN_ONE(2, false);
+      else DMP_BN_ONE(3, false);
+    }
+#undef DMP_BN_ONE
+    return;
+  }
 #define DMP_BN_PART(R)                                                                          \
   hipLaunchKernelGGL((bn_partial_kernel<1, R>), dim3(G), dim3(256), lds, s, x, dy, y, mask, stats, \
                      part, M, C)

@@ -60,7 +60,8 @@ void launch_bn_fwd_fold(const uint16_t* x, const uint16_t* res, uint16_t* y, con
 void launch_bn_bwd_fold(const uint16_t* x, const uint16_t* dy, const uint16_t* y,
                         const float* gamma, const float* stats, float* dgamma, float* dbeta,
                         float* part, float* zero_buf, uint16_t* dx, uint16_t* dres, long long M,
-                        int C, bool relu, hipStream_t s, const uint8_t* mask);
+                        int C, bool relu, hipStream_t s, const uint8_t* mask,
+                        float* coef = nullptr);   // [3][C] scratch: one-pass kernel (bn.hip)
 // BN + ReLU + max pool 3x3/s2/p1 fused (ImageNet ResNet stem), folded finalize
 bool bn_maxpool_supported(int C, int K, int S, int P);
 void launch_bn_relu_maxpool_fold(const uint16_t* x, uint16_t* y, uint8_t* idx, uint16_t* xm,

@@ -620,3 +620,59 @@ def test_gap_linear_head_fused(B, C, H, N):
     assert float((dx.float() - xr.grad).norm() / xr.grad.norm()) < 1e-2
     assert float((gw - 0.5 - wr.grad).norm() / wr.grad.norm()) < 1e-2
     assert float((gb - 0.25 - br.grad).norm() / br.grad.norm()) < 1e-2
+
+
+@pytest.mark.parametrize("B,C,H,mode", [(64, 64, 32, 2), (32, 64, 32, 3), (64, 256, 8, 3),
+                                        (16, 512, 4, 0), (3, 80, 7, 2)])
+def test_bn_bwd_onepass(B, C, H, mode):
+    """One-launch BatchNorm backward (bn.hip bn_bwd_onepass_kernel: reduce ->
+    last-arriver coefficient fold -> apply on the same rows) at ResNet-18 sizes,
+    ReLU mask from x (mode 2), from the 1-bit mask (mode 3) or none, vs fp32; the
+    slot buffer's hand-off words are re-armed (zero) after every call and the
+    bounded poll never gave up; dgamma / dbeta accumulate across calls."""
+    from distributed_ml_pytorch_amd.ops._ext import native
+
+    nat = native()
+    torch.manual_seed(B + C)
+    M = B * H * H
+    x = _bf(torch.randn(B, C, H, H, device="cuda") * 1.5 + 0.3).contiguous(memory_format=CL)
+    dy = _bf(torch.randn(B, C, H, H, device="cuda")).contiguous(memory_format=CL)
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.randn(C, device="cuda") * 0.2
+    xf = x.float()
+    mean = xf.mean(dim=(0, 2, 3))
+    var = xf.var(dim=(0, 2, 3), unbiased=False)
+    inv = torch.rsqrt(var + 1e-5)
+    sc, sh = gamma * inv, beta - mean * gamma * inv
+    stats = torch.cat([mean, inv, sc, sh]).contiguous()
+    pre = xf * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)
+    mask = None
+    if mode == 0:
+        on = torch.ones_like(pre, dtype=torch.bool)
+    elif mode == 2:
+        on = _bf(torch.relu(pre)).float() > 0
+    else:
+        on = torch.rand_like(pre) > 0.4
+        bits = on.permute(0, 2, 3, 1).reshape(-1, 8).to(torch.uint8)
+        mask = (bits << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1).to(torch.uint8)
+    dz = torch.where(on, dy.float(), torch.zeros(()))
+    xhat = (xf - mean.view(1, -1, 1, 1)) * inv.view(1, -1, 1, 1)
+    db_ref = dz.sum(dim=(0, 2, 3))
+    dg_ref = (dz * xhat).sum(dim=(0, 2, 3))
+    dx_ref = (gamma * inv).view(1, -1, 1, 1) * (dz - db_ref.view(1, -1, 1, 1) / M
+                                                 - xhat * dg_ref.view(1, -1, 1, 1) / M)
+    slots = torch.zeros(2 * 64 * C + 4, device="cuda")
+    fwd_slots = torch.ones(2 * 64 * C + 4, device="cuda")
+    dgam = torch.zeros(C, device="cuda")
+    dbet = torch.zeros(C, device="cuda")
+    for it in range(3):
+        dx, _ = nat.bn_bwd_fold(x, dy, None, gamma, stats, dgam, dbet, mode != 0, False, slots,
+                                mask, fwd_slots)
+        torch.cuda.synchronize()
+        tail = slots[-4:].view(torch.int32)
+        assert tail.tolist() == [0, 0, 0, 0], tail.tolist()
+        assert torch.count_nonzero(fwd_slots[:-4]) == 0          # forward slots zeroed
+        torch.testing.assert_close(dx.float(), dx_ref, rtol=3e-2, atol=3e-2)
+        torch.testing.assert_close(dbet, (it + 1) * db_ref, rtol=1e-3, atol=1e-2 * (it + 1))
+        torch.testing.assert_close(dgam, (it + 1) * dg_ref, rtol=1e-3, atol=1e-2 * (it + 1))
+        slots[:-4].zero_()    # (the next forward apply re-zeroes these in a model)
