@@ -579,8 +579,11 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
   const long long Mrows = S2 ? (long long)a.B * a.GH * a.GW : Mtot;
   const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.y, 0, (int)(2LL * Mtot * a.CO), 0x00020000);
-  const bool add_in = S2 ? (a.addend != nullptr && (!a.addend_sub || cls == 0))
-                         : (a.addend != nullptr);   // dgrad residual grad / fwd BN-fold residual
+  // the training forward that feeds a BatchNorm (STATS, not FLIP) takes no
+  // bias, ReLU or addend (launch_halo routes such a conv elsewhere): compiled out
+  constexpr bool PLAIN = STATS && !FLIP;
+  const bool add_in = !PLAIN && (S2 ? (a.addend != nullptr && (!a.addend_sub || cls == 0))
+                                    : (a.addend != nullptr));   // dgrad residual grad / fwd BN-fold residual
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * Mtot * a.CO), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsAm = __builtin_amdgcn_make_buffer_rsrc(
@@ -602,7 +605,7 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
     nok[j] = n < a.CO;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      bj[j][r] = (!FLIP && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
+      bj[j][r] = (!FLIP && !PLAIN && a.bias != nullptr && n + r < a.CO) ? a.bias[n + r] : 0.f;
       if constexpr (BNB) {
         const int ch = nok[j] ? n + r : 0;
         bmu[j][r] = a.bnstat[ch];
@@ -659,8 +662,8 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
       float v[4], t[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        t[r] = acc[i][j][r] + bj[j][r] + ad[r];
-        if (!FLIP && a.relu) t[r] = fmaxf(t[r], 0.f);
+        t[r] = PLAIN ? acc[i][j][r] : acc[i][j][r] + bj[j][r] + ad[r];
+        if (!FLIP && !PLAIN && a.relu) t[r] = fmaxf(t[r], 0.f);
         if constexpr (BNB)
           t[r] = bnb_on(a.bnrelu, xb[r], mk[r], bsc[j][r], bsh[j][r]) ? t[r] : 0.f;
       }
@@ -1455,6 +1458,8 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
   // loaded (inline asm, counted by hand) BEFORE the next tile's DMA is issued,
   // so the deferred epilogue waits only for them, never for that DMA
   typedef unsigned int u32x2_a __attribute__((ext_vector_type(2)));
+  // (the statistics forward feeds a BatchNorm: no addend / ReLU, compiled out)
+  constexpr bool PLAIN = STATS && !FLIP;
   const bool add_in = a.addend != nullptr;   // dgrad residual grad / fwd BN-fold residual
   const __amdgpu_buffer_rsrc_t rsAdd = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(add_in ? a.addend : a.y), 0, (int)(2LL * P * a.CO), 0x00020000);
@@ -1516,7 +1521,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float t = src[i][j][r] + (HAS_BIAS ? bj[j][r] : 0.f) + av[r];
-      if (!FLIP && a.relu) t = fmaxf(t, 0.f);
+      if (!FLIP && !PLAIN && a.relu) t = fmaxf(t, 0.f);
       hv[r] = f2bf(t);
       if (STATS) {
         const float v = ok ? bf2f(hv[r]) : 0.f;
@@ -1974,9 +1979,8 @@ static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
     // halo tile for those dgrads instead (a residual addend is fused: loaded ahead
     // of the DMA, see conv_halo64p_kernel)
     // the persistent kernel's statistics forward carries no conv bias (HAS_BIAS)
-    if (!FLIP && STATS && a.bias != nullptr)
-      return launch_halo<FLIP, STATS>(a, kHaloBase + 9, s) ||
-             launch_halo<FLIP, STATS>(a, kHaloBase + 5, s);
+    // (a statistics forward takes no bias / ReLU / addend in these kernels: PLAIN)
+    if (!FLIP && STATS && (a.bias != nullptr || a.relu || a.addend != nullptr)) return false;
     if (FLIP && (STATS || (a.addend != nullptr && a.addend_sub)))
       return launch_halo<FLIP, STATS>(a, kHaloBase + 9, s) ||
              launch_halo<FLIP, STATS>(a, kHaloBase + 5, s);
@@ -2006,6 +2010,9 @@ static bool launch_halo(const ConvArgs& a, int cfg, hipStream_t s) {
     return true;
   }
   if (!halo_geom(cfg, a.GH, a.GW, a.CI, a.R, a.S, a.stride, a.pad, &g, &lds)) return false;
+  // the statistics forward's epilogue has no bias / ReLU / addend (PLAIN in
+  // halo_epilogue): such a conv takes the implicit GEMM instead
+  if (!FLIP && STATS && (a.bias != nullptr || a.relu || a.addend != nullptr)) return false;
   switch (cfg - kHaloBase) {
 #define X(i, BM, BN, BK, WM, WN, NS) \
   case i: launch_halo_t<BM, BN, BK, WM, WN, NS, FLIP, STATS>(a, g, lds, s); return true;
