@@ -71,6 +71,54 @@ def build_defines(old_defs: str, new_defs: str):
     print("built", f"old: {old_defs!r}", f"new: {new_defs!r}")
 
 
+def stride2_wgrad(libs, tune, P, stream):
+    """The stride-2 3x3 weight gradients (first conv of stages 2-4)."""
+    import torch
+
+    CL = torch.channels_last
+    for name, B, CI, H, CO in [("s2 64->128 /2", 512, 64, 32, 128), ("s3 128->256 /2", 512, 128, 16, 256),
+                               ("s4 256->512 /2", 512, 256, 8, 512)]:
+        OH = H // 2
+        key = json.dumps(["wgrad", B, CI, H, H, CO, CI, 3, 3, 2, 1])
+        if key not in tune:
+            continue
+        cfg = tune[key]
+        g = torch.Generator(device="cuda").manual_seed(1)
+        x = torch.randn(B, CI, H, H, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+            memory_format=CL)
+        dy = torch.randn(B, CO, OH, OH, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+            memory_format=CL)
+        n = libs["new"].abl_wgrad_slab_elems(cfg, B, H, H, CI, CO, 3, 3, 2, 1)
+        slab = torch.empty(max(n, 1), device="cuda")
+        outs = {k: torch.zeros(CO, CI, 3, 3, device="cuda").contiguous(memory_format=CL)
+                for k in libs}
+
+        def call(k):
+            outs[k].zero_()
+            return libs[k].abl_conv_wgrad(P(dy.data_ptr()), P(x.data_ptr()), P(outs[k].data_ptr()),
+                                          B, H, H, CI, OH, OH, CO, 3, 3, 2, 1, cfg,
+                                          P(slab.data_ptr() if n > 0 else 0), stream)
+        for k in libs:
+            assert call(k) == 0, (k, cfg)
+        torch.cuda.synchronize()
+        d = float((outs["old"] - outs["new"]).norm() / outs["old"].norm())
+        times = {k: [] for k in libs}
+        for rnd in range(ROUNDS):
+            for k in (("old", "new") if rnd % 2 == 0 else ("new", "old")):
+                a = torch.cuda.Event(enable_timing=True)
+                b = torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(20):
+                    call(k)
+                b.record()
+                b.synchronize()
+                times[k].append(a.elapsed_time(b) / 20 * 1e3)
+        to, tn = statistics.median(times["old"]), statistics.median(times["new"])
+        print(f"{name:16s} {'wgrad':5s} {cfg:5d} {to:8.1f} {tn:8.1f} {100 * (tn / to - 1):+6.1f}%  "
+              f"{'yes' if d < 1e-5 else 'NO':>7s}   min {min(times['old']):6.1f} "
+              f"{min(times['new']):6.1f}", flush=True)
+
+
 def run(cfgs_arg):
     sys.path.insert(0, str(ROOT))
     import torch
@@ -89,6 +137,7 @@ def run(cfgs_arg):
               ("s3 256ch 8x8", 512, 256, 8, 8, 256), ("s4 512ch 4x4", 512, 512, 4, 4, 512)]
     print(f"{'layer':16s} {'pass':5s} {'cfg':>5s} {'old us':>8s} {'new us':>8s} {'delta':>7s}  bitwise"
           f"   (median of {ROUNDS} rounds x 20 calls; min)")
+    stride2_wgrad(libs, tune, P, stream)
     for name, B, CI, H, W, CO in layers:
         g = torch.Generator(device="cuda").manual_seed(0)
         x = torch.randn(B, CI, H, W, device="cuda", generator=g).to(torch.bfloat16).contiguous(
