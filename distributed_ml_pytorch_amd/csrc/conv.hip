@@ -745,8 +745,11 @@ __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&ac
   static_assert(BN % 8 == 0 && 64 % CPR == 0, "row segments of 8 channels");
   typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
   const long long Mtot = (long long)a.B * a.OH * a.OW;
-  const bool add_in = a.addend != nullptr;
-  const bool relu = !FLIP && a.relu;
+  // statistics forward (feeds a BatchNorm): no bias / ReLU / addend, compiled out
+  // (launch_cfg sends such a conv with any of them to the plain epilogue)
+  constexpr bool PLAIN = STATS && !FLIP;
+  const bool add_in = !PLAIN && a.addend != nullptr;
+  const bool relu = !FLIP && !PLAIN && a.relu;
   // phase 1: fp32 epilogue math that needs no addend, bf16, into the block tile
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -754,7 +757,7 @@ __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&ac
     float bj[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      bj[r] = (!FLIP && a.bias != nullptr && n0 + nl + r < a.CO) ? a.bias[n0 + nl + r] : 0.f;
+      bj[r] = (!FLIP && !PLAIN && a.bias != nullptr && n0 + nl + r < a.CO) ? a.bias[n0 + nl + r] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int ml = wm * (BM / WM) + i * 16 + (lane & 15);
@@ -1762,7 +1765,9 @@ static void launch_cfg(const ConvArgs& a, int classes, hipStream_t s) {
   // row-staged epilogue: forward, or a stride-1 data gradient without the fused BN
   // backward (one parity class, output row = dX pixel); otherwise the plain tile
   constexpr bool R = ROWS && (MODE == 0 || !STATS);
-  if (R && (MODE == 0 || (a.stride == 1 && !a.addend_sub)))
+  // (the row epilogue of a statistics forward has no bias / ReLU / addend: PLAIN)
+  const bool plain_ok = !(MODE == 0 && STATS) || (a.bias == nullptr && !a.relu && a.addend == nullptr);
+  if (R && plain_ok && (MODE == 0 || (a.stride == 1 && !a.addend_sub)))
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, WM, WN, MODE, STATS, NS, R>), grid,
                        dim3(64 * WM * WN), 0, s, a);
   else
