@@ -19,8 +19,10 @@ All three passes of a linear layer run on one hand-written gfx950 kernel family:
 Tile shape (and split-K) are picked per (pass, shape) by measurement on first
 use (``ops.tuner``); shapes the 16-B DMA tiles cannot take (a dimension not a
 multiple of 8: 10-class heads, LeNet's 84-wide layer) run the any-shape
-fallback kernel of the same file.  ``DMP_GEMM=auto`` also lets hipBLASLt
-compete for the plain forward / data-gradient GEMMs (default ``native``).
+fallback kernel of the same file.  hipBLASLt competes for the plain forward /
+data-gradient GEMMs (no fused epilogue beyond a bias; ``DMP_GEMM=native`` keeps
+it out): it wins only the ViT-B/16 QKV forward (K = 768, N = 2304: 45 vs 55 us,
+-0.2 ms per ViT step, profiles/vit_qkv_blas_r5.txt).
 """
 from __future__ import annotations
 
@@ -34,8 +36,8 @@ from ._ext import native
 from .functional import _notify, is_relu_masked, mark_relu_masked, nonneg, set_nonneg
 from .tuner import TUNER
 
-_GEMM_MODE = os.environ.get("DMP_GEMM", "native")
-_BLAS = -1000          # candidate id of the library GEMM (DMP_GEMM=auto only)
+_GEMM_MODE = os.environ.get("DMP_GEMM", "auto")
+_BLAS = -1000          # candidate id of the library GEMM (plain fwd / dgrad only)
 _SMALL = -1            # any-shape fallback kernel
 
 
