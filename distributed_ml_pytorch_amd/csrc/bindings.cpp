@@ -1859,6 +1859,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("relu_bwd", &relu_bwd, "ReLU backward from the saved output", py::arg("dy"), py::arg("y"),
         py::arg("out") = py::none());
   m.def("gemm_config_ok", &dmp::gemm_config_ok, "tile config usable in this mode");
+  m.def("gemm_set_xcd_k", &dmp::gemm_set_xcd_k, "split-major XCD deal of wgrad split-K on/off");
   m.def("gemm_configs", &gemm_configs, "[(id, BM, BN, threads, stages, BK)] of the GEMM tiles");
   m.def("attention_fwd", &attention_fwd, "fused MHSA forward on qkv rows -> (out, lse2)");
   m.def("attention_bwd", &attention_bwd, "fused MHSA backward -> dqkv (qkv layout)");

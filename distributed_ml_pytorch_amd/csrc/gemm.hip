@@ -32,6 +32,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace dmp {
@@ -84,6 +85,9 @@ struct GemmArgs {
   int sk_full, sk_split, sk_kchunk;
   float* sk_ws;
   int* sk_cnt;
+  // EPI_ACC32 split-K: deal (split, tile) pairs to the XCDs split-major, so one
+  // XCD's blocks share a k-range (and so the operand panels its L2 holds)
+  int xcd_k;
 };
 
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -256,12 +260,21 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
   const int rt = sk ? (bid - g.sk_full) / g.sk_split : 0;
   const int piece = sk ? bid - g.sk_full - rt * g.sk_split : 0;
   const int G = TRANS_OUT && g.sk_split > 1 ? g.sk_full : gridDim.x;   // whole-tile blocks
-  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
-  const int tile = sk ? g.sk_full + rt
-                      : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  // weight gradient with split-K (g.xcd_k): the same deal over the linear block
+  // id of the whole (tile, split) grid, split-major -- the blocks of one XCD take
+  // consecutive tiles of ONE k-range instead of all k-ranges of fewer tiles, so
+  // the operand panels one XCD's L2 must hold shrink (ViT-B/16 QKV dW: the 128x128
+  // tiles over 4 k-ranges read 8 x the 19 MB input X from beyond L2 otherwise)
+  const bool kdeal = EPI == EPI_ACC32 && g.xcd_k && gridDim.y > 1;
+  const int L = kdeal ? bid + (int)blockIdx.y * G : bid;
+  const int GL = kdeal ? G * (int)gridDim.y : G;
+  const int xcd = L & 7, q8 = GL >> 3, r8 = GL & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  const int ky = kdeal ? lin / G : (int)blockIdx.y;
+  const int tile = sk ? g.sk_full + rt : (kdeal ? lin - ky * G : lin);
   const int tm = tile / g.tiles_n;
   const int m0 = tm * BM, n0 = (tile - tm * g.tiles_n) * BN;
-  const int kbase = sk ? piece * g.sk_kchunk : blockIdx.y * g.k_chunk;
+  const int kbase = sk ? piece * g.sk_kchunk : ky * g.k_chunk;
   const int kend = min(g.K, kbase + (sk ? g.sk_kchunk : g.k_chunk)) - kbase;
   if (kend <= 0) return;   // (the host sizes pieces so that none is empty)
   const int KT = (kend + BKS - 1) / BKS;
@@ -345,7 +358,7 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
       const bool atomic = gridDim.y > 1;
       // split-K into a slab: plain stores (~6 TB/s chip-wide) instead of fp32
       // atomics (~1.3 TB/s of added bytes), reduced by a streaming pass after
-      float* S = g.slab != nullptr ? g.slab + (long long)blockIdx.y * g.M * g.N : nullptr;
+      float* S = g.slab != nullptr ? g.slab + (long long)ky * g.M * g.N : nullptr;
       if (do_bias && (lane & 15) == 0) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -962,6 +975,11 @@ void gemm_config_info(int cfg, int* info) {
   info[4] = c.bk;
 }
 
+namespace {
+int g_xcd_k = -1;   // DMP_GEMM_XCD_K (default 1): split-major XCD deal of wgrad split-K
+}
+void gemm_set_xcd_k(int on) { g_xcd_k = on ? 1 : 0; }
+
 // mode 0: fwd (C = A B^T, EPI 0 or 1), 1: dgrad (A [M][K], B [K][N]; EPI 0 or 2),
 // 2: wgrad (A [K][M], B [K][N]; fp32 accumulate)
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
@@ -970,6 +988,11 @@ void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const u
                  hipStream_t s, bool relu, float* part, float* slab, float* sk_ws, int* sk_cnt,
                  const uint8_t* auxmask) {
   GemmArgs g{};
+  if (g_xcd_k < 0) {
+    const char* e = std::getenv("DMP_GEMM_XCD_K");
+    g_xcd_k = (e == nullptr || e[0] != '0') ? 1 : 0;
+  }
+  g.xcd_k = g_xcd_k;
   g.auxmask = aux != nullptr && epi == EPI_STORE ? auxmask : nullptr;
   g.relu = relu ? 1 : 0;
   g.part = part;

@@ -238,6 +238,8 @@ void launch_bn_fwd_partials(const uint16_t* x, const uint16_t* res, uint16_t* y,
 int gemm_num_configs();
 bool gemm_config_ok(int mode, int cfg);   // tile shape usable for this pass
 void gemm_config_info(int cfg, int* info);   // {BM, BN, threads, stages, BK}
+// split-major XCD deal of the weight-gradient split-K (DMP_GEMM_XCD_K, default on)
+void gemm_set_xcd_k(int on);
 void launch_gemm(int mode, int epi, int cfg, const uint16_t* a, int lda, const uint16_t* b,
                  int ldb, void* c, int ldc, uint16_t* c2, const uint16_t* bias,
                  const uint16_t* aux, float* dbias, int M, int N, int K, int splits,

@@ -92,12 +92,18 @@ def test_gemm_wgrad(M, K, N, splits, slab):
         torch.bfloat16)
     ref_w = dy.float().t() @ x.float()
     ref_b = dy.float().sum(0)
-    for cfg in _cfgs(2):
-        g = torch.full((N, K), 0.25, device=dev)
-        gb = torch.full((N,), -0.5, device=dev)
-        native().gemm(2, 3, cfg, dy, x, g, dbias=gb, splits=splits, slab=slab)
-        assert _rel(g - 0.25, ref_w) < 2e-3, cfg
-        assert _rel(gb + 0.5, ref_b) < 2e-3, cfg
+    # split-K: both block -> (tile, k-range) deals (GemmArgs::xcd_k)
+    try:
+        for xcd_k in ((0, 1) if splits > 1 else (1,)):
+            native().gemm_set_xcd_k(xcd_k)
+            for cfg in _cfgs(2):
+                g = torch.full((N, K), 0.25, device=dev)
+                gb = torch.full((N,), -0.5, device=dev)
+                native().gemm(2, 3, cfg, dy, x, g, dbias=gb, splits=splits, slab=slab)
+                assert _rel(g - 0.25, ref_w) < 2e-3, (cfg, xcd_k)
+                assert _rel(gb + 0.5, ref_b) < 2e-3, (cfg, xcd_k)
+    finally:
+        native().gemm_set_xcd_k(1)
 
 
 def test_gemm_strided_operands():
