@@ -22,8 +22,6 @@
 //   BP   - reduction rows per stage (32 / 64)
 //   NS   - pipeline depth: NS-1 stages of DMA in flight, retired with a
 //          counted s_waitcnt vmcnt(N) before one raw s_barrier per stage.
-#include <cstdlib>
-
 #include "common.h"
 
 #ifndef DMP_ABLATE
@@ -45,6 +43,7 @@ struct WgradArgs {
   int p_chunk;      // rows of P per block (multiple of BP)
   float* dbias;     // optional fp32 [CO] += sum_p dY[p][co] (linear / conv bias grad)
   float* slab;      // halo wgrad, slab mode: per-split partials [splits][CO][R][S][CI]
+  int xcd;          // gather wgrad: XCD-aware deal of the blocks (cfg bit 512)
 };
 
 __device__ __forceinline__ f32x4 mfma16w(const bf16x8& a, const bf16x8& b, f32x4 c) {
@@ -110,9 +109,18 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const int kx0 = blockIdx.x * BNW;            // first column in K = (r, s, ci)
-  const int co0 = blockIdx.y * BMW;
-  const long long p_begin = (long long)blockIdx.z * a.p_chunk;
+  // XCD-aware bijective remap (a.xcd): consecutive logical blocks -- the (k, co)
+  // tiles of one pixel split, which read the same dY / X rows -- land on one XCD
+  // under round-robin dispatch instead of being spread over all eight L2s
+  const int nx = gridDim.x, ny = gridDim.y, G = nx * ny * gridDim.z;
+  const int bid = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int lid = a.xcd ? (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3)
+                        : bid;
+  const int bx = lid % nx, by = (lid / nx) % ny, bz = lid / (nx * ny);
+  const int kx0 = bx * BNW;            // first column in K = (r, s, ci)
+  const int co0 = by * BMW;
+  const long long p_begin = (long long)bz * a.p_chunk;
   const long long p_end = min(a.P, p_begin + a.p_chunk);
   const int GH = a.GH, GW = a.GW, CI = a.CI;
   const int nsteps = (int)((p_end - p_begin + BP - 1) / BP);
@@ -208,7 +216,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   // bias gradient from the dY tiles already staged for the weight gradient:
   // one extra MFMA per fragment with an all-ones B operand (column sums), by
   // the wn == 0 waves of the blocks of the first k tile only
-  const bool do_bias = a.dbias != nullptr && blockIdx.x == 0 && wn == 0;
+  const bool do_bias = a.dbias != nullptr && bx == 0 && wn == 0;
   f32x4 accb[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -854,6 +862,9 @@ void launch_conv_wgrad(const u16* dy, const u16* x, float* dw, int B, int H, int
   chunk = (chunk + bp - 1) / bp * bp;
   splits = (a.P + chunk - 1) / chunk;
   a.p_chunk = (int)chunk;
+  // cfg bit 512: XCD-aware deal (a tuner choice: it wins where one pixel split's
+  // tiles share few operand panels, loses where they span a many-MB working set)
+  a.xcd = (cfg >= 0 && (cfg & 512)) ? 1 : 0;
   const dim3 grid((unsigned)(K / bnw), (unsigned)(CO / bmw), (unsigned)splits);
   if (bmw == 128) {
     if (bnw == 192) launch_wgrad_variant<192, 2, 2, 128>(a, grid, bp, ns, s);

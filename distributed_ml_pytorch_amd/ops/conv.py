@@ -111,16 +111,19 @@ def _igemm_candidates(out_channels: int, fwd: bool = True):
 
 def _wgrad_candidates(K: int, CO: int | None = None):
     """cfg = BNW sel | BP32 << 2 | NS3 << 3 | (min P rows / 512) << 4 | BMW128 << 8
-    (csrc/conv_wgrad.hip); the 128-channel tiles only when ``CO % 128 == 0``."""
+    | XCD << 9 (csrc/conv_wgrad.hip); the 128-channel tiles only when ``CO % 128 == 0``.
+    XCD: the tiles of one pixel split dealt to one XCD (profiles/wgrad_xcd_deal_r5.txt)."""
     cands = []
-    for bm in ((0, 1) if CO is not None and CO % 128 == 0 else (0,)):
-        for sel, bnw in ((1, 64), (2, 128), (3, 192)):
-            if K % bnw:
-                continue
-            for bp32 in (0, 1):
-                for ns3 in (0, 1):
-                    for chunk in (2, 4, 8):          # x512 rows of P per block
-                        cands.append(sel | (bp32 << 2) | (ns3 << 3) | (chunk << 4) | (bm << 8))
+    for xcd in (0, 1):
+        for bm in ((0, 1) if CO is not None and CO % 128 == 0 else (0,)):
+            for sel, bnw in ((1, 64), (2, 128), (3, 192)):
+                if K % bnw:
+                    continue
+                for bp32 in (0, 1):
+                    for ns3 in (0, 1):
+                        for chunk in (2, 4, 8):          # x512 rows of P per block
+                            cands.append(sel | (bp32 << 2) | (ns3 << 3) | (chunk << 4) | (bm << 8)
+                                         | (xcd << 9))
     return cands
 
 
