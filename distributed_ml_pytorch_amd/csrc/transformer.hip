@@ -135,26 +135,46 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) { pg[c][k] = 0.f; pb[c][k] = 0.f; }
   const long long step = (long long)gridDim.x * 4 * RPW;
-  for (long long row = ((long long)blockIdx.x * 4 + wid) * RPW + lane / LR; row - lane / LR < rows;
-       row += step) {
+  // software-pipelined over the wave's rows: the next row group's x / dy / dadd
+  // (and mean / rstd) are in flight while this one is reduced and stored
+  bf16x8 nx[MAXC], ny[MAXC], na[MAXC];
+  float nmean = 0.f, nrstd = 0.f;
+  auto fetch = [&](long long row) {
+    const long long r = row < rows ? row : 0;
+    nmean = mean_in[r];
+    nrstd = rstd_in[r];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      if (c < nc) {
+        const int e0 = (sub + c * LR) * 8;
+        nx[c] = *reinterpret_cast<const bf16x8*>(x + r * D + e0);
+        ny[c] = *reinterpret_cast<const bf16x8*>(dy + r * D + e0);
+        if (dadd) na[c] = *reinterpret_cast<const bf16x8*>(dadd + r * D + e0);
+      }
+    }
+  };
+  long long row = ((long long)blockIdx.x * 4 + wid) * RPW + lane / LR;
+  if (row - lane / LR < rows) fetch(row);
+  for (; row - lane / LR < rows; row += step) {
     const bool ok = row < rows;
     const long long r = ok ? row : 0;
-    const float mean = mean_in[r], rstd = rstd_in[r];
+    const float mean = nmean, rstd = nrstd;
+    bf16x8 cx[MAXC], cy[MAXC], ad[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) { cx[c] = nx[c]; cy[c] = ny[c]; ad[c] = na[c]; }
+    if (row + step - lane / LR < rows) fetch(row + step);
     float xh[MAXC][8], dv[MAXC][8];
-    bf16x8 ad[MAXC];   // residual-stream gradient, raw: issued with x / dy, not after the reductions
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       if (c < nc) {
         const int e0 = (sub + c * LR) * 8;
         float gm[8];
-        ld8(x + r * D + e0, xh[c]);
-        ld8(dy + r * D + e0, dv[c]);
-        if (dadd) ad[c] = *reinterpret_cast<const bf16x8*>(dadd + r * D + e0);
         if (gamma) ld8f(gamma + e0, gm);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          if (!ok) dv[c][k] = 0.f;
+          xh[c][k] = bf2f(cx[c].v[k]);
+          dv[c][k] = ok ? bf2f(cy[c].v[k]) : 0.f;
           xh[c][k] = (xh[c][k] - mean) * rstd;
           const float g = dv[c][k] * (gamma ? gm[k] : 1.f);
           s1 += g;
