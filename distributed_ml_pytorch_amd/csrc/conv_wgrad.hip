@@ -90,6 +90,25 @@ __device__ __forceinline__ int wg_off(int row, int col) {
   return row * ROWE + ((((col >> 4) ^ wg_f<ROWE>(row))) << 4) + (col & 15);
 }
 
+// Halo wgrad X image (128-B rows; staged row = X row hx of image tb of the tile,
+// column c of W2 = W + 2).  A half-wave's tr read touches the tap-shifted rows of
+// pixels {p..p+3} and {p+8..p+11}: stride 1, 4 consecutive columns (alternating
+// row parity) and 8 pixels later (same row at W >= 16, next row at W = 8, next
+// image / two rows at W = 4); stride 2, columns c, c+2, c+4, c+6 (one parity).
+// Keyed on the column and on bit 3 of the pixel-like index (tb * TH + hx) * W + c,
+// every (parity, granule) pair of the 8 rows is distinct at any W -- wg_f<64> of
+// the row NUMBER collides for W2 = 10 / 6 (22 % / 9.5 % LDS bank conflicts on the
+// 8x8 / 4x4 layers, profiles/pmc_r5.txt); stride 2 keeps the unavoidable 2-way
+// (8 rows of one parity over 4 granules).
+#ifndef DMP_WGX_SWZ
+#define DMP_WGX_SWZ 1
+#endif
+template <bool S2>
+__device__ __forceinline__ int wgx_f(int c, int pidx) {
+  if constexpr (S2) return (c >> 1) & 3;
+  else return ((c >> 1) & 1) | (((pidx >> 3) & 1) << 1);
+}
+
 template <int BNW, int WM, int WN, int BP, int NS, int BMW>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   constexpr int NW = 4;
@@ -414,9 +433,10 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
       const int dh = (S2 ? 2 * th : th) - 1 + r0;   // relative to the tile's first X row
       const bool ok = row < hg.XROWS && tb < hg.TB && (unsigned)w < (unsigned)W &&
                       (!whole_img || (unsigned)dh < (unsigned)H);
+      const int fx = DMP_WGX_SWZ ? wgx_f<S2>(w + 1, (tb * TH + th) * W + w + 1) : wg_f<CW>(row);
       if (ok)
         x_rel[j] = 2u * (unsigned)((tb * img + dh * W + w) * C + ci0 +
-                                   (((pch >> 1) ^ wg_f<CW>(row)) * 16) + (pch & 1) * 8);
+                                   (((pch >> 1) ^ fx) * 16) + (pch & 1) * 8);
       x_dh[j] = dh;
       x_tb[j] = tb;
     }
@@ -479,6 +499,7 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
   // staged X row of the lane's reduction rows (pixels pk*32 + 8g + q and +4), tap (0, 0)
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pc = li & 3;
   int xr_lo[BM / 32 / PG], xr_hi[BM / 32 / PG];
+  int xk_lo[BM / 32 / PG], xk_hi[BM / 32 / PG];   // X-image swizzle keys (wgx_f)
 #pragma unroll
   for (int pk = 0; pk < BM / 32 / PG; ++pk) {
 #pragma unroll
@@ -488,12 +509,27 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
       const int tb = pl / (TH * OWd), r2 = pl - tb * TH * OWd;
       const int th = r2 / OWd, tw = r2 - th * OWd;
       const int xr = (tb * THX + th) * W2 + (S2 ? 2 * tw : tw);
-      if (hsel) xr_hi[pk] = xr; else xr_lo[pk] = xr;
+      // swizzle keys of the 3 * TR taps, 2 bits each: column c0 + s, pixel-like
+      // index of image row th + r (stride 2: one staged row per output row, TR = 1)
+      const int c0 = S2 ? 2 * tw : tw, p0 = (tb * TH + th) * W + c0;
+      int xk = 0;
+#pragma unroll
+      for (int r = 0; r < TR; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) xk |= wgx_f<S2>(c0 + s, p0 + r * W + s) << (2 * (r * 3 + s));
+      if (hsel) { xr_hi[pk] = xr; xk_hi[pk] = xk; } else { xr_lo[pk] = xr; xk_lo[pk] = xk; }
     }
   }
   auto tr = [&](const u16* img_, int row, int col) -> s16x4_t {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (__attribute__((address_space(3))) s16x4_t*)(img_ + wg_off<CW>(row, col)));
+  };
+  // X image read of tap (r, s) for the lane's pixel (row xr, key xk)
+  auto trx = [&](const u16* img_, int xr, int xk, int r, int s, int col) -> s16x4_t {
+    const int row = xr + r * W2 + s;
+    const int f = DMP_WGX_SWZ ? (xk >> (2 * (r * 3 + s))) & 3 : wg_f<CW>(row);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(
+        img_ + row * CW + (((col >> 4) ^ f) << 4) + (col & 15)));
   };
 
   f32x4 acc[NT][4];
@@ -523,8 +559,8 @@ __global__ void __launch_bounds__(256 * PG) conv_wgrad_halo_kernel(WgradArgs a, 
       for (int r = 0; r < TR; ++r)
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
-          const s16x4_t lo = tr(Xs, xr_lo[pkl] + r * W2 + s, wc * 16 + 4 * pc);
-          const s16x4_t hi = tr(Xs, xr_hi[pkl] + r * W2 + s, wc * 16 + 4 * pc);
+          const s16x4_t lo = trx(Xs, xr_lo[pkl], xk_lo[pkl], r, s, wc * 16 + 4 * pc);
+          const s16x4_t hi = trx(Xs, xr_hi[pkl], xk_hi[pkl], r, s, wc * 16 + 4 * pc);
           bx[slot][r * 3 + s] =
               __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
