@@ -29,6 +29,8 @@
 // one pixel (8-byte NHWC stores) and the fwd epilogue can reduce per-channel
 // BatchNorm partial sums (no extra pass over Y).  Several tile configurations are
 // compiled; the host side times them per shape on first use (ops/tuner.py).
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -558,6 +560,10 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
 // BM - MV rows read a valid staged row and are dropped by the epilogue.
 struct HaloGeom {
   int TH, TB, HROWS, A_INS, MV;
+  // conv_halo_kernel staging: staged row width W2 (W + 2, or W + 4 with PSW),
+  // rows per image block PI ((TH + 2) * W2 [+ pad]), PSW: swizzle keyed on the
+  // pixel-like index (see conv_halo_kernel)
+  int W2, PI, PSW;
 };
 
 constexpr int kHaloAPW = 8;   // max halo DMA instructions per wave per stage
@@ -875,11 +881,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   const int MV = hg.MV;
   const long long m0 = (long long)blockIdx.x * MV;
   const int n0 = blockIdx.y * BN;
-  const int H = a.GH, W = a.GW, C = a.CI, TH = hg.TH, HW2 = W + 2;
+  const int H = a.GH, W = a.GW, C = a.CI, TH = hg.TH, HW2 = hg.W2;
   const int img = H * W;
   // (32-bit: M * C < 2^31 by the host checks; a 64-bit division is ~100 instructions)
   const int b0 = (int)m0 / img, h0 = ((int)m0 - b0 * img) / W;
-  const int per_img = (TH + 2) * HW2;
+  const int per_img = hg.PI;
   // in-tile index math by float reciprocal (small_divmod): the integer
   // division sequences were ~2/3 of the ~500-VALU per-block prologue
   const float rcp_pi = 1.f / (float)per_img, rcp_w2 = 1.f / (float)HW2;
@@ -894,9 +900,19 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
   // instead -- conflict-free for every fragment and tap of those tiles (checked
   // exhaustively over the lane groups of gfx950's b128 reads); W >= 16 keeps
   // swz<32>.  qrow = row / W2 of the staged row.
+  //
+  // A fragment that wraps an image row at any other width (ImageNet 56 / 28 / 14 /
+  // 7) skips the 2 halo columns, which unbalances the staged rows' 64-B quarters
+  // of a lane group -- no chunk XOR can fix that (24-40 % conflict cycles,
+  // profiles/lds_conflict_census_r5.txt).  There (hg.PSW) the host stages rows
+  // W2 = W + 4 wide with (-2W) mod 4 pad rows per image, so every staged row is
+  // congruent mod 4 to its pixel-like index pidx = (tb * TH + hx) * W + c, which
+  // runs consecutively along every fragment and tap; keyed on pidx, swz<32> then
+  // sees 16 consecutive rows.
   const bool qsw = BK == 32 && W <= 8 && 16 % W == 0;
-  auto hswz = [&](int row, int qrow, int c) {
-    return qsw ? c ^ ((qrow & 1) << 1) : swz<BK>(row, c);
+  const bool psw = BK == 32 && hg.PSW;
+  auto hswz = [&](int row, int qrow, int c, int pidx) {
+    return psw ? swz<BK>(pidx, c) : qsw ? c ^ ((qrow & 1) << 1) : swz<BK>(row, c);
   };
   // halo DMA slots: lane's row of each 1-KiB piece -> (image, h, w) of the
   // source pixel; positions outside the image (or past the batch) read zeros
@@ -909,10 +925,11 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
     small_divmod(row, per_img, rcp_pi, tb, rem);
     small_divmod(rem, HW2, rcp_w2, hh, ww);
     const int b = b0 + tb, h = h0 - 1 + hh, w = ww - 1;
-    const bool ok = ins < hg.A_INS && row < hg.HROWS && b < a.B && (unsigned)h < (unsigned)H &&
-                    (unsigned)w < (unsigned)W;
+    const bool ok = ins < hg.A_INS && row < hg.HROWS && b < a.B && hh < TH + 2 &&
+                    (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
     a_base[j] = ok ? 2u * (unsigned)(((b * H + h) * W + w) * C +
-                                     hswz(row, tb * (TH + 2) + hh, lane % CPR) * 8)
+                                     hswz(row, tb * (TH + 2) + hh, lane % CPR,
+                                          (tb * TH + hh) * W + ww) * 8)
                    : kOOB;
   }
   // weight DMA slots: row = tap * BN + output channel
@@ -966,11 +983,12 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_halo_kernel(ConvArgs a, Hal
     int tb, r2, th, tw;
     small_divmod(ml, TH * W, rcp_tw, tb, r2);
     small_divmod(r2, W, rcp_w, th, tw);
-    const int q0 = tb * (TH + 2) + th, hrow = q0 * HW2 + tw;
+    const int q0 = tb * (TH + 2) + th, hrow = tb * per_img + th * HW2 + tw;
+    const int p0 = (tb * TH + th) * W + tw;   // pixel-like index of tap (0, 0)
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int row = hrow + (t / 3) * HW2 + t % 3;
-      aoff[i][t] = row * BK + hswz(row, q0 + t / 3, lane >> 4) * 8;
+      aoff[i][t] = row * BK + hswz(row, q0 + t / 3, lane >> 4, p0 + (t / 3) * W + t % 3) * 8;
     }
   }
   int offB[BK / 32];
@@ -1867,7 +1885,17 @@ static bool halo_geom(int cfg, int H, int W, int C, int R, int S, int stride, in
     }
   }
   const int rpi = 64 / (bk / 8);
-  h.HROWS = h.TB * (h.TH + 2) * (W + 2);
+  // fragments wrapping image rows (W not a multiple of 16, not the <= 8 widths the
+  // row-parity key covers): the W + 4-wide staging of conv_halo_kernel (PSW)
+  static const bool psw_on = [] {
+    const char* e = std::getenv("DMP_HALO_PSW");
+    return e == nullptr || e[0] != '0';
+  }();
+  h.PSW = psw_on && bk == 32 && W % 16 != 0 && !(W <= 8 && 16 % W == 0);
+  h.W2 = h.PSW ? W + 4 : W + 2;
+  h.PI = (h.TH + 2) * h.W2;
+  if (h.PSW) h.PI += (((h.TH * W - h.PI) % 4) + 4) % 4;   // PI == TH * W (mod 4)
+  h.HROWS = h.TB * h.PI;
   h.A_INS = (h.HROWS + rpi - 1) / rpi;
   if (h.A_INS > kHaloAPW * nw) return false;
   const size_t stage = (size_t)h.A_INS * rpi * bk + (size_t)9 * bn * bk;
