@@ -124,19 +124,25 @@ def _scenario(uneven: bool = False):
         want = sum(deltas[1]) + sum(deltas[2])
         reply = tr.inbox[puller][-1]
         other = 3 - puller
-        # read-your-writes: the reply holds the puller's own two deltas plus a
-        # prefix (none, the first, or both) of the other worker's
+        # read-your-writes: the reply holds the puller's own two deltas plus, per
+        # ELEMENT, a prefix (none, the first, or both) of the other worker's.  The
+        # snapshot runs on the puller's link stream, behind its own applies only
+        # (server.py _reply): an apply of the other worker may be in flight on its
+        # own stream, so the snapshot is Hogwild-consistent per element (elementwise
+        # atomics, that worker's two applies ordered on its stream), not a cut
         own = sum(deltas[puller])
         cands = [own, own + deltas[other][0], own + deltas[other][0] + deltas[other][1]]
-        errs = [float((reply[:n] - c).abs().max()) for c in cands]
+        per_elem = torch.stack([(reply[:n] - c).abs() for c in cands]).min(0).values
+        errs = [float(per_elem.max())] + [float((reply[:n] - c).abs().max()) for c in cands]
         recvs = [(p, a, b) for k, p, a, b in tr.spans if k == "recv"]
         sends = [(p, a, b) for k, p, a, b in tr.spans if k == "send"]
         a1 = recvs[0][1]
         w1 = [(a, b) for p, a, b in recvs if p == 1]
         return {
             "master_err": float((ps.parameters() - want).abs().max()),
-            "reply_err": min(errs),
-            "reply_prefix": errs.index(min(errs)),
+            "reply_err": errs[0],
+            "reply_prefix": errs[1:].index(min(errs[1:])),   # closest whole prefix
+            "reply_err_own": errs[1],                          # own deltas only, exactly
             "w1_first_recv_end": a1.elapsed_time(w1[0][1]),
             "reply_end": a1.elapsed_time(sends[-1][2]),
             "reply_version": float(reply[n]), "version": ps.version,
@@ -202,7 +208,7 @@ def test_ps_completion_ordered_applies():
     r = _run_scenario(16, uneven=True)
     print(r)
     assert r["master_err"] < 1e-4, r
-    assert r["reply_err"] < 1e-4 and r["reply_prefix"] == 0, r
+    assert r["reply_err_own"] < 1e-4 and r["reply_prefix"] == 0, r
     assert r["version"] == 4 and r["links"]["recv"] == 4 and r["links"]["send"] == 1
     assert r["reply_end"] < r["w1_first_recv_end"], r
 
