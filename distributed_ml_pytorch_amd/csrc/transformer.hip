@@ -8,6 +8,8 @@
 // of scores for softmax), bf16 storage, fp32 math.  One wave64 per row: each
 // lane owns 8-element (16 B) chunks lane, lane+64, ... kept in registers
 // between the reduction and the normalisation, so a row is read once.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dmp {
@@ -407,7 +409,15 @@ void launch_layernorm_bwd(const u16* x, const u16* dy, const float* gamma, const
   // the per-block param-grad epilogue (LDS fold + 2*D slot atomics) costs about
   // as much as a row group, so fewer, longer-lived blocks (ViT-B/16 bs64, 25
   // LayerNorms: 1024 blocks 601 us, 1576 blocks 741 us)
-  if (blocks > 512) blocks = 512;   // <= 16 blocks add into each slot row
+  static const int cap = [] {
+    const char* e = std::getenv("DMP_LN_BWD_BLOCKS");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v > 0 ? v : 512;
+  }();
+  // (DMP_LN_BWD_BLOCKS sweeps, ViT-B/16 after the row pipelining: 256 / 512 / 768 /
+  // 1024 blocks 691 / 553 / 673 / 627 us per step; trip-balanced grids of 394 / 526 /
+  // 788 blocks 589 / 727 / 670: two blocks per CU wins, profiles/layernorm_bwd_pipelined_r5.txt)
+  if (blocks > cap) blocks = cap;
   const bool grads = slots != nullptr && (dgamma != nullptr || dbeta != nullptr);
   const size_t lds = grads ? (size_t)8 * D * sizeof(float) : 0;
   DMP_LN_BY_LR(layernorm_bwd_kernel, lr, nc, dim3((unsigned)blocks), lds, x, dy, gamma, mean, rstd,
