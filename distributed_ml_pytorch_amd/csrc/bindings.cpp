@@ -97,6 +97,24 @@ void ps_apply(Tensor shard, Tensor delta, optional<Tensor> mirror, double scale,
   }
 }
 
+// PS applied-count (server.py / async_sharded.py version stamps): ps_count adds
+// `add` to (or, set=True, sets) the int32 counter on the current stream;
+// ps_stamp writes float(counter) into the 1-element fp32 `dst`
+void ps_count(Tensor cnt, int64_t add, bool set) {
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && cnt.numel() == 1,
+              "ps_count: counter must be a 1-element int32 GPU tensor");
+  dmp::launch_ps_count(cnt.data_ptr<int>(), (int)add, set, cur_stream());
+}
+
+void ps_stamp(Tensor cnt, Tensor dst) {
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && cnt.numel() == 1,
+              "ps_stamp: counter must be a 1-element int32 GPU tensor");
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.numel() == 1 &&
+                  dst.device() == cnt.device(),
+              "ps_stamp: dst must be a 1-element fp32 tensor on the counter's device");
+  dmp::launch_ps_stamp(cnt.data_ptr<int>(), dst.data_ptr<float>(), cur_stream());
+}
+
 void pull_land(Tensor p, Tensor src, optional<Tensor> acc, optional<Tensor> w16) {
   const int64_t n = p.numel();
   TORCH_CHECK(n % 4 == 0, "arena length must be a multiple of 4");
@@ -1247,6 +1265,23 @@ std::vector<Tensor> layernorm_fwd(Tensor x, optional<Tensor> gamma, optional<Ten
 }
 
 // ViT token assembly: h [B, N+1, D] = cat(cls, tok) + pos (bf16 operands)
+// [B, D] gradient of the token-`tok` rows -> the [B, N, D] stream gradient
+// (zeros elsewhere), one native pass (models/vit.py class-token head)
+Tensor token_row_scatter(Tensor g, int64_t N, int64_t tok) {
+  check_gpu(g, "g");
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 && g.dim() == 2 && g.is_contiguous(),
+              "token_row_scatter: g must be a contiguous bf16 [B, D] GPU tensor");
+  const int64_t B = g.size(0), D = g.size(1);
+  TORCH_CHECK(D % 8 == 0 && N >= 1 && tok >= 0 && tok < N,
+              "token_row_scatter: D % 8 == 0 and 0 <= tok < N");
+  TORCH_CHECK(B * N * D < (1LL << 40), "token_row_scatter: tensor too large");
+  Tensor out = at::empty({B, N, D}, g.options());
+  dmp::launch_token_row_scatter(reinterpret_cast<const uint16_t*>(g.data_ptr()),
+                                reinterpret_cast<uint16_t*>(out.data_ptr()), (int)B, (int)N,
+                                (int)D, (int)tok, cur_stream());
+  return out;
+}
+
 Tensor vit_embed_fwd(Tensor tok, Tensor cls, Tensor pos) {
   tok = tok.contiguous();
   check_rows_bf16(tok, "tok");
@@ -1795,6 +1830,9 @@ PYBIND11_MODULE(_native, m) {
         "fwd / dgrad remainder split-K: fp32 workspace floats per split tile (0 = no split)");
   m.def("ps_apply", &ps_apply, "parameter-server delta apply", py::arg("shard"), py::arg("delta"),
         py::arg("mirror") = py::none(), py::arg("scale") = 1.0, py::arg("atomic") = false);
+  m.def("ps_count", &ps_count, "bump / set a PS applied-count", py::arg("cnt"),
+        py::arg("add") = 1, py::arg("set") = false);
+  m.def("ps_stamp", &ps_stamp, "copy a PS applied-count into a reply's version element");
   m.def("pull_land", &pull_land, "land a parameter pull into the worker arena");
   m.def("push_handoff", &push_handoff, "snapshot+zero the push accumulator");
   m.def("cast_f32_bf16", &cast_f32_bf16, "flat fp32 -> bf16");
@@ -1833,6 +1871,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("dy"), py::arg("y"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"), py::arg("want_dres"), py::arg("slots") = py::none(),
         py::arg("mask") = py::none());
+  m.def("token_row_scatter", &token_row_scatter, "gradient of a per-sample token-row select");
   m.def("vit_embed_fwd", &vit_embed_fwd, "ViT token assembly cat(cls, tok) + pos");
   m.def("vit_embed_bwd", &vit_embed_bwd, "ViT token assembly backward (dtok + fp32 batch sums)");
   m.def("layernorm_fwd", &layernorm_fwd,

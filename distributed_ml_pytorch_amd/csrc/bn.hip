@@ -838,20 +838,26 @@ __global__ void __launch_bounds__(256) bn_bwd_onepass_kernel(
     int it = 0;
     while (__hip_atomic_load(tail + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
       __builtin_amdgcn_s_sleep(2);
-      if (++it > (1 << 22)) {   // never co-resident: give up (wrong dx, no hang)
+      if (++it > (1 << 22)) {
+        // never co-resident (CUs taken by another stream's kernel): give up rather
+        // than hang, and make it LOUD -- this block's dx becomes NaN (the
+        // divergence watchdog stops the run) instead of silently using stale
+        // coefficients; tail + 3 records it for a host-side check
         __hip_atomic_store(tail + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_flag = -1;
         break;
       }
     }
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const float poison = last_flag == -1 ? __builtin_nanf("") : 0.f;
   float ka[8], kb[8], kc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    ka[k] = r0 < rpi ? coef[c0 + k] : 0.f;
-    kb[k] = r0 < rpi ? coef[C + c0 + k] : 0.f;
-    kc[k] = r0 < rpi ? coef[2 * C + c0 + k] : 0.f;
+    ka[k] = r0 < rpi ? coef[c0 + k] + poison : 0.f;
+    kb[k] = r0 < rpi ? coef[C + c0 + k] + poison : 0.f;
+    kc[k] = r0 < rpi ? coef[2 * C + c0 + k] + poison : 0.f;
   }
   __syncthreads();   // every thread has its coefficients before the departure below
   if (t == 0) {      // departure: the last block out re-arms the release flag

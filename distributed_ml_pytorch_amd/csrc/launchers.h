@@ -17,6 +17,8 @@ void launch_ps_apply_f32(float* shard, const float* delta, uint16_t* mirror, lon
                          float scale, hipStream_t s);
 void launch_ps_apply_bf16(float* shard, const uint16_t* delta, uint16_t* mirror, long long n,
                           float scale, hipStream_t s);
+void launch_ps_count(int* cnt, int add, bool set, hipStream_t s);
+void launch_ps_stamp(int* cnt, float* dst, hipStream_t s);
 void launch_pull_land_f32(float* p, const float* src, const float* acc, uint16_t* w16,
                           long long n, hipStream_t s);
 void launch_pull_land_bf16(float* p, const uint16_t* src, const float* acc, uint16_t* w16,
@@ -118,6 +120,8 @@ void launch_softmax_bwd(const uint16_t* p, const uint16_t* dp, uint16_t* ds, lon
                         float scale, hipStream_t s);
 void launch_vit_embed_fwd(const uint16_t* tok, const uint16_t* cls, const uint16_t* pos,
                           uint16_t* h, int B, int N, int D, hipStream_t s);
+void launch_token_row_scatter(const uint16_t* g, uint16_t* out, int B, int N, int D, int tok,
+                              hipStream_t s);
 void launch_vit_embed_bwd(const uint16_t* dh, uint16_t* dtok, float* dpos, float* dcls, int B,
                           int N, int D, hipStream_t s);
 

@@ -121,6 +121,30 @@ __global__ void __launch_bounds__(256) ps_apply_atomic_kernel(float* __restrict_
   }
 }
 
+// Applied-count of a PS shard: the version a reply is stamped with
+// (parallel/server.py, parallel/async_sharded.py; SURVEY §7.3(3) "a version
+// counter is the basis for staleness-bounded pulls").  ps_count runs on the
+// applying stream right after the apply kernel, so the count only moves once an
+// apply has wholly landed; ps_stamp runs on the replying stream BEFORE the
+// snapshot copy, so a stamp counts only applies the snapshot fully contains
+// (applies still in flight on other link streams may show up in some elements,
+// never in the count).  Both are agent-scope atomics: the counting and reading
+// streams may run on any XCD (MI355X_MICROARCH.md "Workgroup dispatch").
+__global__ void __launch_bounds__(64) ps_count_kernel(int* __restrict__ cnt, int add, int set) {
+  if (threadIdx.x == 0) {
+    if (set) __hip_atomic_exchange(cnt, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_add(cnt, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void __launch_bounds__(64) ps_stamp_kernel(int* __restrict__ cnt,
+                                                      float* __restrict__ dst) {
+  if (threadIdx.x == 0) {
+    const int v = __hip_atomic_fetch_add(cnt, 0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    dst[0] = (float)v;
+  }
+}
+
 // Pull landing: p = src (fp32 or bf16 wire), w16 = bf16(p). Optionally the
 // delta the worker accumulated since the snapshot is re-applied on top
 // (keep_local: p = src + acc), which keeps not-yet-pushed local progress
@@ -263,6 +287,7 @@ void launch_ps_apply_bf16(float* shard, const u16* delta, u16* mirror, long long
 
 void launch_ps_apply_atomic(float* shard, const void* delta, bool bf16, long long n, float scale,
                             hipStream_t s) {
+  if (n <= 0) return;   // an empty shard: nothing to add (a 0-block grid is invalid)
   const int grid = (int)std::min<long long>((n + 255) / 256, 256LL * 16);
   if (bf16)
     hipLaunchKernelGGL(ps_apply_atomic_kernel<u16>, dim3(grid), dim3(256), 0, s, shard,
@@ -270,6 +295,14 @@ void launch_ps_apply_atomic(float* shard, const void* delta, bool bf16, long lon
   else
     hipLaunchKernelGGL(ps_apply_atomic_kernel<float>, dim3(grid), dim3(256), 0, s, shard,
                        (const float*)delta, n, scale);
+}
+
+void launch_ps_count(int* cnt, int add, bool set, hipStream_t s) {
+  hipLaunchKernelGGL(ps_count_kernel, dim3(1), dim3(64), 0, s, cnt, add, set ? 1 : 0);
+}
+
+void launch_ps_stamp(int* cnt, float* dst, hipStream_t s) {
+  hipLaunchKernelGGL(ps_stamp_kernel, dim3(1), dim3(64), 0, s, cnt, dst);
 }
 
 void launch_pull_land_f32(float* p, const float* src, const float* acc, u16* w16, long long n,

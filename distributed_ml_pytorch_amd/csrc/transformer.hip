@@ -541,11 +541,43 @@ __global__ void __launch_bounds__(256) vit_embed_bwd_kernel(const u16* __restric
   }
 }
 
+// Backward of selecting ONE token row per sample (the ViT head reads the class
+// token, models/vit.py): out[b][t][:] = t == tok ? g[b][:] : 0 over the whole
+// [B][N][D] stream gradient in one 16-B-per-lane pass -- instead of ATen's zero
+// fill of the stream gradient plus a strided slice copy (two launches).
+__global__ void __launch_bounds__(256) token_row_scatter_kernel(const u16* __restrict__ g,
+                                                                u16* __restrict__ out, int N,
+                                                                int dv, int tok, long long nvec) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    const long long row = i / dv;
+    const int d8 = (int)(i - row * dv);
+    const long long b = row / N;
+    const int t = (int)(row - b * N);
+    bf16x8 v;
+    if (t == tok) {
+      v = reinterpret_cast<const bf16x8*>(g)[b * dv + d8];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v.v[e] = 0;
+    }
+    reinterpret_cast<bf16x8*>(out)[i] = v;
+  }
+}
+
 void launch_vit_embed_fwd(const u16* tok, const u16* cls, const u16* pos, u16* h, int B, int N,
                           int D, hipStream_t s) {
   const long long nvec = (long long)B * (N + 1) * (D / 8);
   hipLaunchKernelGGL(vit_embed_fwd_kernel, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, tok, cls,
                      pos, h, B, N, D);
+}
+
+void launch_token_row_scatter(const u16* g, u16* out, int B, int N, int D, int tok,
+                              hipStream_t s) {
+  const long long nvec = (long long)B * N * (D / 8);
+  if (nvec <= 0) return;
+  hipLaunchKernelGGL(token_row_scatter_kernel, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, g,
+                     out, N, D / 8, tok, nvec);
 }
 
 void launch_vit_embed_bwd(const u16* dh, u16* dtok, float* dpos, float* dcls, int B, int N, int D,

@@ -81,8 +81,11 @@ class BasicBlock(nn.Module):
         else:
             sc = self.shortcut(xa)
         # sc feeds only bn2: its backward may hand dY over unmasked (deferred
-        # residual mask) to conv1's dgrad epilogue or the shortcut BN
-        return self.bn2(self.conv2(h), residual=mark_residual_only(sc))
+        # residual mask) to conv1's dgrad epilogue or the shortcut BN.  Not when sc
+        # IS x (conv1 off the native path hands x itself back): x also feeds
+        # conv1, autograd would sum the tagged hand-off with conv1's dx and drop
+        # the owed mask
+        return self.bn2(self.conv2(h), residual=sc if sc is x else mark_residual_only(sc))
 
 
 class Bottleneck(nn.Module):
@@ -131,7 +134,7 @@ class Bottleneck(nn.Module):
             sc = self.shortcut(xa)
         # sc feeds only bn3 (deferred residual mask: the identity alias's consumer
         # is conv1's 1x1 GEMM-route dgrad, whose store epilogue applies the mask)
-        return self.bn3(self.conv3(h), residual=mark_residual_only(sc))
+        return self.bn3(self.conv3(h), residual=sc if sc is x else mark_residual_only(sc))
 
 
 class ResNet(nn.Module):

@@ -138,7 +138,8 @@ class VisionTransformer(nn.Module):
             y = self.norm(h)
         else:
             _, y = self.norm.add_forward(h, pending)
-        return self.head(y[:, 0].contiguous())
+        # class token rows read in place by the head GEMM (no gather / zero-fill copies)
+        return self.head(DF.token_row(y, 0))
 
 
 def vit_b16(num_classes: int = 1000, image_size: int = 224) -> VisionTransformer:

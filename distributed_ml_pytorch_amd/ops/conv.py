@@ -31,6 +31,7 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from ._ext import native
+from ._policy import stock_gpu
 from .functional import (DEFER_RES_STATS, apply_bitmask, deferred_mask, is_relu_masked,
                          resolve_deferred, set_nonneg)
 from .tuner import TUNER
@@ -750,6 +751,9 @@ def conv2d(x, w, b, stride, padding, dilation, groups, master=None, want_stats=F
             return (y, x) if alias else y
         if w is None:
             w = master.to(x.dtype)
+    stock_gpu("conv2d", x, reason=f"input {tuple(x.shape)} {x.dtype}, weight "
+              f"{tuple((w if w is not None else master).shape)}, stride {stride}, padding "
+              f"{padding}, groups {groups}")
     y = F.conv2d(x, w, b if b is None or b.dtype == x.dtype else b.to(x.dtype), stride, padding,
                  dilation, groups)
     if relu:

@@ -20,6 +20,7 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from ._ext import native
+from ._policy import stock_gpu
 
 CL = torch.channels_last
 
@@ -451,8 +452,9 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, m
         raise RuntimeError(
             f"batch_norm_act: unsupported bf16 GPU input (C={x.shape[1]}); "
             "the native kernel needs C % 8 == 0 and C <= 2048")
-    # CPU, or an fp32 GPU run (``--dtype fp32``: the framework's own fp32 oracle
-    # mode -- every op on PyTorch's fp32 kernels, same model / optimizer / PS)
+    # CPU, or an fp32 GPU run in the explicit oracle mode (``--deterministic``:
+    # every op on PyTorch's fp32 kernels, same model / optimizer / PS)
+    stock_gpu("batch_norm", x)
     w = weight.to(x.dtype) if weight is not None else None
     b = bias.to(x.dtype) if bias is not None else None
     y = F.batch_norm(x, running_mean, running_var, w, b, training, momentum, eps)
@@ -478,6 +480,7 @@ def global_avg_pool(x):
     """[N,C,H,W] -> [N,C] mean over H,W."""
     if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
         return _GAP.apply(x)
+    stock_gpu("global_avg_pool", x)
     return x.mean(dim=(2, 3))
 
 
@@ -517,6 +520,7 @@ def max_pool2d(x, kernel_size: int, stride: int | None = None, padding: int = 0,
         y = _MaxPool.apply(x, int(kernel_size), int(stride), int(padding), bool(nchw_out),
                            nonneg(x))
         return set_nonneg(y, nonneg(x))
+    stock_gpu("max_pool2d", x)
     return F.max_pool2d(x, kernel_size, stride, padding)
 
 
@@ -610,6 +614,7 @@ class _ReLU(Function):
 def relu(x):
     if x.is_cuda and x.dtype == torch.bfloat16:
         return _ReLU.apply(x)
+    stock_gpu("relu", x)
     return F.relu(x)
 
 
@@ -652,6 +657,7 @@ def dropout(x, p: float, training: bool, channelwise: bool = False, state=None, 
                 x = x.contiguous()
                 mode = 1
         return set_nonneg(_Dropout.apply(x, p, seed, state, mode), nonneg(x))
+    stock_gpu("dropout", x)
     if channelwise:
         return F.dropout2d(x, p, True)
     return F.dropout(x, p, True)
@@ -817,6 +823,7 @@ def layer_norm(x, weight, bias, eps: float, slots=None):
             and (weight is None or weight.dtype == torch.float32)
             and (bias is None or bias.dtype == torch.float32)):
         return _LayerNorm.apply(x, weight, bias, eps, slots)
+    stock_gpu("layer_norm", x)
     w = compute_weight(weight, x.dtype)
     b = compute_weight(bias, x.dtype)
     return F.layer_norm(x, (x.shape[-1],), w, b, eps)
@@ -840,7 +847,34 @@ def gelu(x):
     """tanh-approximate GELU (native bf16 kernel on GPU)."""
     if x.is_cuda and x.dtype == torch.bfloat16 and x.numel() % 8 == 0:
         return _GELU.apply(x)
+    stock_gpu("gelu", x)
     return F.gelu(x, approximate="tanh")
+
+
+# ------------------------------------------------------- token-row select
+class _TokenRow(Function):
+    """``h[:, tok]`` as a strided view (the native GEMM reads its rows in place,
+    row stride N * D: no gather copy); backward = one native pass writing the
+    [B, N, D] stream gradient (zeros but the selected rows) instead of ATen's
+    zero fill + slice copy."""
+
+    @staticmethod
+    def forward(ctx, h, tok):
+        ctx.n, ctx.tok = h.shape[1], int(tok)
+        return h.select(1, int(tok))
+
+    @staticmethod
+    def backward(ctx, g):
+        return native().token_row_scatter(g.contiguous(), ctx.n, ctx.tok), None
+
+
+def token_row(h, tok: int = 0):
+    """Row ``tok`` of every sample of a ``[B, N, D]`` token stream (the ViT class
+    token feeding the head, /root/reference has no ViT: BASELINE.json config #5)."""
+    if h.is_cuda and h.dtype == torch.bfloat16 and h.dim() == 3 and h.shape[-1] % 8 == 0:
+        return _TokenRow.apply(h, tok)
+    stock_gpu("token_row", h)
+    return h[:, tok].contiguous()
 
 
 # ------------------------------------------------------- ViT token assembly
@@ -890,6 +924,7 @@ def vit_embed(tok, cls, pos):
             return _VitEmbed.apply(tok, cls, pos, cls16, pos16)
         return native().vit_embed_fwd(tok, cls16, pos16)
     c = compute_weight(cls, tok.dtype).expand(tok.shape[0], -1, -1)
+    stock_gpu("vit_embed", tok)
     return torch.cat([c, tok], dim=1) + compute_weight(pos, tok.dtype)
 
 
@@ -950,14 +985,17 @@ def attention_qkv(qkv, heads: int):
 
 
 def attention(q, k, v):
-    """softmax(q k^T / sqrt(d)) v over [B, H, N, d] bf16.
+    """softmax(q k^T / sqrt(d)) v over [B, H, N, d]: the geometries the fused
+    kernel does not take (head dim != 64, more than 256 tokens).
 
-    The two batched GEMMs are plain library GEMMs (hipBLASLt via
-    ``torch.matmul``); the scaled row softmax and its backward are native
-    kernels.  At ViT-B/16's 197 tokens the score tensor is small
-    (B*H*197^2 bf16), so it is materialised rather than tiled.
+    The two batched GEMMs are library GEMMs (hipBLASLt via ``torch.matmul``), so
+    on the GPU this runs only in the explicit stock oracle mode (``ops._policy``);
+    the scaled row softmax and its backward are native kernels.
     """
     scale = q.shape[-1] ** -0.5
+    stock_gpu("attention (torch.matmul / SDPA)", q,
+              reason=f"head dim {q.shape[-1]}, {k.shape[-2]} tokens, {q.dtype}: the fused "
+                     "kernel takes head dim 64, <= 256 tokens, bf16")
     if q.is_cuda and q.dtype == torch.bfloat16 and k.shape[-2] <= 1024:
         s = torch.matmul(q, k.transpose(-1, -2))
         p = _ScaledSoftmax.apply(s, scale)

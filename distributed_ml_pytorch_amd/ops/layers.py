@@ -12,6 +12,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import functional as DF
+from ._policy import stock_gpu
 from .conv import (bn_slot_buffer, conv2d as _conv2d, im2col_conv_supported,
                    native_conv_supported, small_conv_supported)
 from .linear import arena_linear_ok, linear as _arena_linear
@@ -56,6 +57,8 @@ class Linear(nn.Linear):
     def forward(self, x, relu: bool = False):
         if arena_linear_ok(x, self.weight, self.bias):
             return _arena_linear(x, self.weight, self.bias, relu)
+        stock_gpu("linear", x, reason=f"input {tuple(x.shape)} {x.dtype}, weight "
+                  f"{tuple(self.weight.shape)} (no bf16 arena shadow)")
         w = DF.compute_weight(self.weight, x.dtype)
         b = DF.compute_weight(self.bias, x.dtype)
         y = F.linear(x, w, b)
@@ -123,6 +126,7 @@ class MaxPool2d(nn.MaxPool2d):
     def forward(self, x):
         kp = self.native_params()
         if kp is None:
+            stock_gpu("max_pool2d", x, reason="ceil_mode / dilation / non-square window")
             return super().forward(x)
         return DF.max_pool2d(x, *kp)
 

@@ -19,10 +19,10 @@ All three passes of a linear layer run on one hand-written gfx950 kernel family:
 Tile shape (and split-K) are picked per (pass, shape) by measurement on first
 use (``ops.tuner``); shapes the 16-B DMA tiles cannot take (a dimension not a
 multiple of 8: 10-class heads, LeNet's 84-wide layer) run the any-shape
-fallback kernel of the same file.  hipBLASLt competes for the plain forward /
-data-gradient GEMMs (no fused epilogue beyond a bias; ``DMP_GEMM=native`` keeps
-it out): it wins only the ViT-B/16 QKV forward (K = 768, N = 2304: 45 vs 55 us,
--0.2 ms per ViT step, profiles/vit_qkv_blas_r5.txt).
+fallback kernel of the same file.  No library GEMM is ever a candidate: every
+Linear pass of every model runs on these kernels (round 6 took the hipBLASLt
+candidate of round 5 back out; the QKV forward it won is tracked
+in profiles/gemm_native_only_r6.txt).
 """
 from __future__ import annotations
 
@@ -36,8 +36,6 @@ from ._ext import native
 from .functional import _notify, is_relu_masked, mark_relu_masked, nonneg, set_nonneg
 from .tuner import TUNER
 
-_GEMM_MODE = os.environ.get("DMP_GEMM", "auto")
-_BLAS = -1000          # candidate id of the library GEMM (plain fwd / dgrad only)
 _SMALL = -1            # any-shape fallback kernel
 
 
@@ -83,7 +81,7 @@ def _mfma_ok(mode: int, M: int, N: int, K: int, *mats) -> bool:
 
 # candidate encoding: (cfg + 1) * 1024 + splits (cfg -1 = any-shape kernel),
 # + _SLAB for a wgrad split-K reduced through a plain-store slab instead of fp32
-# atomics; _BLAS < 0; the tuner's "no pick" is -1
+# atomics; the tuner's "no pick" is -1
 _SLAB = 1 << 20
 
 
@@ -148,7 +146,7 @@ def _small_split_options(mode: int, K: int):
                   {max(1, min(1023, K // r)) for r in (32, 64, 128)})
 
 
-def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bool):
+def _candidates(mode: int, epi: int, M: int, N: int, K: int, ok: bool):
     if not ok:
         return [_enc(_SMALL, s) for s in _small_split_options(mode, K)]
     cands = []
@@ -166,8 +164,6 @@ def _candidates(mode: int, epi: int, M: int, N: int, K: int, plain: bool, ok: bo
             cands += [_enc(cid, s) for s in _SK_SPLITS if _sk_splits(cid, M, N, K, s)]
     if M * N * K < (1 << 22):
         cands += [_enc(_SMALL, s) for s in _small_split_options(mode, K)]
-    if _GEMM_MODE == "auto" and plain and mode in (0, 1):
-        cands.append(_BLAS)
     return cands
 
 
@@ -180,16 +176,6 @@ def _default(mode: int, M: int, N: int, K: int, ok: bool) -> int:
     return _enc(4, 1)
 
 
-def _blas(mode, a, b, c, bias):
-    if mode == 0:
-        if bias is not None:
-            torch.addmm(bias, a, b.t(), out=c)
-        else:
-            torch.mm(a, b.t(), out=c)
-    else:
-        torch.mm(a, b, out=c)
-
-
 def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None, relu=False,
          part=None, auxmask=None):
     """C = epilogue(A(m,k) B(n,k)) on the native kernels (see csrc/gemm.hip):
@@ -199,23 +185,22 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
     stored outputs (epi 0, MFMA tiles; a 1x1 conv feeding a BatchNorm).
     ``auxmask``: 1-bit mask of ``aux`` ([M * N / 8] uint8, bn.hip's ReLU mask
     layout) applied by the epilogue; materialised first where the picked kernel
-    takes none (library GEMM, any-shape fallback, strided output)."""
+    takes none (any-shape fallback, strided output)."""
     M, N = c.shape
     K = a.shape[0] if mode == 2 else a.shape[1]
     if M == 0 or N == 0:
         return
     # outputs / aux of any row stride: the epilogues fall back to element access
     ok = _mfma_ok(mode, M, N, K, a, b)
-    plain = epi == 0 and aux is None and not relu and part is None
     key = ("gemm", mode, epi, M, N, K, bias is not None, aux is not None, dbias is not None,
            bool(relu)) + (("stats",) if part is not None else ())
     pick = TUNER.cache.get(key)
     if pick is None:
-        cands = _candidates(mode, epi, M, N, K, plain, ok)
+        cands = _candidates(mode, epi, M, N, K, ok)
         if part is not None:
             if not ok:
                 raise ValueError("gemm: BN partial sums need MFMA-compatible operands")
-            cands = [e for e in cands if e != _BLAS and _dec(e)[0] >= 0]
+            cands = [e for e in cands if _dec(e)[0] >= 0]
         if len(cands) == 1:
             pick = cands[0]
         else:
@@ -226,24 +211,20 @@ def gemm(mode: int, epi: int, a, b, c, c2=None, bias=None, aux=None, dbias=None,
                 cs, ds = c, dbias
 
             def run(e):
-                if e == _BLAS:
-                    _blas(mode, a, b, cs, bias)
-                else:
-                    cfg_e, split_e = _dec(e)
-                    ps = torch.zeros_like(part) if part is not None else None
-                    native().gemm(mode, epi, cfg_e, a, b, cs, c2, bias, aux, ds, split_e, relu,
-                                  ps, _dec_slab(e))
+                cfg_e, split_e = _dec(e)
+                ps = torch.zeros_like(part) if part is not None else None
+                native().gemm(mode, epi, cfg_e, a, b, cs, c2, bias, aux, ds, split_e, relu,
+                              ps, _dec_slab(e))
             pick = TUNER.best(key, run, cands)
             if pick == -1:
                 pick = _default(mode, M, N, K, ok)
-    if auxmask is not None and (pick == _BLAS or _dec(pick)[0] < 0 or epi != 0
-                                or c.stride(0) != N or N % 8):
+    if auxmask is not None and (_dec(pick)[0] < 0 or epi != 0 or c.stride(0) != N or N % 8):
         from .functional import apply_bitmask_rows
 
         aux, auxmask = apply_bitmask_rows(aux, auxmask), None
-    if pick == _BLAS:
-        _blas(mode, a, b, c, bias)
-        return
+    if pick < 0:
+        raise RuntimeError(f"gemm: tune cache entry {pick} for {key} is not a native kernel "
+                           "(library GEMMs are not candidates)")
     cfg, splits = _dec(pick)
     native().gemm(mode, epi, cfg, a, b, c, c2, bias, aux, dbias, splits, relu, part,
                   _dec_slab(pick), auxmask)

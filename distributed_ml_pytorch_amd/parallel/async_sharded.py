@@ -51,7 +51,7 @@ import torch.distributed as dist
 
 from . import messaging as M
 from .clients import PSClient, _EventWork, _Pending
-from .links import PairGroupTransport, PairLinks, wait_on, warm_stream
+from .links import AppliedCount, PairGroupTransport, PairLinks, wait_on, warm_stream
 
 _LOG = logging.getLogger(__name__)
 
@@ -127,7 +127,9 @@ class ShardServer:
         self.reply_g = reply_groups
         self.scale = scale
         self.lock = threading.Lock()
-        self.version = 0
+        self.version = 0           # applies ENQUEUED (host): staleness of incoming pushes
+        # applies wholly landed (device count on GPU): what a reply is stamped with
+        self.applied = AppliedCount(self.device, self.nat if self.cuda else None)
         self.counts: Counter = Counter()
         self.staleness: list[int] = []
         self.error: BaseException | None = None
@@ -145,6 +147,8 @@ class ShardServer:
                     self.nat.ps_apply(self.master, torch.zeros(self.n, dtype=dt,
                                                                device=self.device),
                                       None, self.scale, True)
+                self.nat.ps_count(self.applied.dev, 0)
+                self.nat.ps_stamp(self.applied.dev, torch.empty(1, device=self.device))
             self.stream.synchronize()
         self.thread = threading.Thread(target=self._run, daemon=True, name=f"shard-ps-{rank}")
 
@@ -163,6 +167,7 @@ class ShardServer:
             self.nat.ps_apply(self.master, delta, None, self.scale, True)
         else:
             self.master.add_(delta.to(torch.float32), alpha=self.scale)
+        self.applied.bump()        # GPU: on the applying stream, counted once landed
         if base_version is not None:
             self.staleness.append(self.version - base_version)
         self.version += 1
@@ -188,13 +193,17 @@ class ShardServer:
     def snapshot(self, out: torch.Tensor | None = None):
         """``(copy of the shard, version, event)``: on GPU the copy is taken on the
         PS stream after every LOCAL apply enqueued so far (peers' applies land on
-        their link streams whenever their payloads arrive); ``event`` marks it done."""
+        their link streams whenever their payloads arrive); ``event`` marks it done.
+        ``version`` counts the applies the copy wholly contains: a host int on CPU,
+        on GPU a 1-element device tensor stamped on the PS stream before the copy
+        (:class:`.links.AppliedCount`)."""
         with self.lock:
-            v = self.version
             if not self.cuda:
                 snap = self.master.clone() if out is None else out.copy_(self.master)
-                return snap, v, None
+                return snap, self.applied.host, None
             with self._ctx():
+                v = torch.empty(1, dtype=torch.float32, device=self.device)
+                self.applied.stamp(v)
                 snap = self.master.clone() if out is None else out.copy_(self.master)
                 ev = torch.cuda.Event()
                 ev.record()
@@ -225,11 +234,9 @@ class ShardServer:
     def _reply(self, dst: int):
         n = self.n
         with self.lock:
-            version = float(self.version)
-
             def fill(buf):
+                self.applied.stamp(buf[n:])    # before the copy: wholly-landed applies
                 buf[:n].copy_(self.master)
-                buf[n:].fill_(version)
 
             # snapshot on dst's own reply-link stream, after dst's own applies
             # (its push-link stream: read-your-writes) and the local worker's
@@ -271,7 +278,8 @@ class ShardServer:
 
     def stats(self) -> dict:
         st = self.staleness
-        return {"shard_version": self.version, "shard_counts": dict(self.counts),
+        return {"shard_version": self.version, "shard_applied": self.applied.value(),
+                "shard_counts": dict(self.counts),
                 "shard_links": dict(self.rx.counts, sends=self.tx.counts["send"],
                                     send_reused=self.tx.counts["reused"]),
                 "shard_staleness_mean": (sum(st) / len(st)) if st else 0.0,
@@ -433,7 +441,8 @@ class AsyncShardedPSClient(PSClient):
         # the landed base version is their MIN on every backend -- on GPU resolved
         # without a host sync once the copies' event has completed
         vsrcs = {lo // self.shard_n: rbuf[hi - lo:] for lo, hi, rbuf, _ in pull.parts}
-        vsrcs[self.rank] = torch.tensor([float(pull.own_version)])
+        ov = pull.own_version
+        vsrcs[self.rank] = ov if torch.is_tensor(ov) else torch.tensor([float(ov)])
         self._note_versions([vsrcs[o] for o in range(self.world)])
         ev = None
         if self.cuda:
@@ -475,7 +484,8 @@ class AsyncShardedPSClient(PSClient):
         if ev is not None:
             ev.synchronize()
         return {"kind": "sharded_async", "rank": self.rank, "world": self.world,
-                "master": snap.detach().cpu(), "shard_version": v}
+                "master": snap.detach().cpu(),
+                "shard_version": int(v.item()) if torch.is_tensor(v) else int(v)}
 
     def load_state_dict(self, sd: dict):
         if sd.get("kind") != "sharded_async":
@@ -486,6 +496,7 @@ class AsyncShardedPSClient(PSClient):
         with self.server.lock:
             with self.server._ctx():
                 self.server.master.copy_(sd["master"].to(self.server.device))
+                self.server.applied.set(int(sd.get("shard_version", 0)))
             self.server.version = int(sd.get("shard_version", 0))
         if self.cuda:
             self.server.stream.synchronize()

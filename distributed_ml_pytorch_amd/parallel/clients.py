@@ -243,19 +243,42 @@ class PSClient:
 
 
 class LocalPSClient(PSClient):
-    """In-process parameter server on the worker's device (single-GPU / tests)."""
+    """In-process parameter server on the worker's device (single-GPU / tests).
+
+    The PS work runs on the side HIP stream, ordered by events exactly as the
+    N > 1 clients order theirs (:class:`ShardedPSClient` push / pull): the
+    compute stream only hands the accumulator off (``push_handoff``); the
+    master's apply and the pull snapshot run on ``side`` behind that event and
+    overlap the next step's forward, and a pulled snapshot lands on the compute
+    stream behind the snapshot's event at the staleness-bounded step boundary.
+    So the 1-GPU headline exercises the same overlap structure as the
+    multi-GPU topologies (BASELINE north star: "param pulls overlapped with
+    forward on a side HIP stream"), and reports its ``push`` / ``pull`` device
+    spans (``comm_times``)."""
 
     def init(self):
         self.master = self.arena.p32.detach().clone()
         self.ps_version = 0
         self.side = torch.cuda.Stream(self.device) if self.cuda else None
+        self._pull_bufs: deque = deque()       # (snapshot buffer, land-done event)
         if self.side is not None:
             warm_stream(self.side)     # bind its queue now, not mid-step
+            # the master copy above was made on the compute stream
+            self.side.wait_stream(torch.cuda.current_stream(self.device))
 
     def push(self, step: int):
         buf = self._handoff()
         if self.cuda:
-            self.nat.ps_apply(self.master, buf, None, 1.0)
+            ev = torch.cuda.Event()
+            ev.record()                          # the hand-off kernel wrote buf
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(ev)
+                with self._timed("push"):
+                    self.nat.ps_apply(self.master, buf, None, 1.0)
+                done = torch.cuda.Event()
+                done.record()
+            # the hand-off slot is refilled two pushes later: after this apply read it
+            self._send_work[self._cur_slot] = _EventWork(done)
         else:
             self.master.add_(buf.to(torch.float32))
         self.ps_version += 1
@@ -263,20 +286,51 @@ class LocalPSClient(PSClient):
         self.bytes_sent += buf.numel() * buf.element_size()
 
     def request_pull(self, step: int):
-        snap = self.master.clone() if self.wire_dtype == torch.float32 else \
-            self.master.to(self.wire_dtype)
-        self.pending.append(_Pending(step, snap, version=self.ps_version))
-        self.bytes_recv += snap.numel() * snap.element_size()
+        if not self.cuda:
+            snap = self.master.clone() if self.wire_dtype == torch.float32 else \
+                self.master.to(self.wire_dtype)
+            self.pending.append(_Pending(step, snap, version=self.ps_version))
+            self.bytes_recv += snap.numel() * snap.element_size()
+            return
+        buf, free_ev = self._pull_bufs.popleft() if len(self._pull_bufs) > self.staleness else \
+            (torch.empty(self.master.numel(), dtype=self.wire_dtype, device=self.device), None)
+        with torch.cuda.stream(self.side):
+            if free_ev is not None:
+                self.side.wait_event(free_ev)   # the land kernel that last read buf is done
+            with self._timed("pull"):
+                buf.copy_(self.master)          # behind every apply enqueued on `side`
+            ev = torch.cuda.Event()
+            ev.record()
+        self.pending.append(_Pending(step, buf, event=ev, version=self.ps_version))
+        self.bytes_recv += buf.numel() * buf.element_size()
+
+    def _land(self, pend):
+        super()._land(pend)
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record()              # side may refill the buffer after the land kernel
+            self._pull_bufs.append((pend.buf, ev))
+
+    def finish(self):
+        super().finish()
+        if self.cuda:
+            self.side.synchronize()
 
     def state_dict(self) -> dict:
+        if self.cuda:
+            self.side.synchronize()
         return {"kind": "local", "master": self.master.detach().cpu(),
                 "ps_version": int(self.ps_version)}
 
     def load_state_dict(self, sd: dict):
         if sd.get("kind") != "local":
             return
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.side)
         with torch.no_grad():
             self.master.copy_(sd["master"].to(self.master.device))
+        if self.cuda:
+            self.side.wait_stream(torch.cuda.current_stream())
         self.ps_version = int(sd["ps_version"])
 
 

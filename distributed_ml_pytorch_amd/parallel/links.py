@@ -89,6 +89,54 @@ def warm_stream(stream):
         torch.zeros(1, device=stream.device)
 
 
+class AppliedCount:
+    """How many applies a PS shard has wholly received -- the version a reply is
+    stamped with (the version is the basis of staleness-bounded
+    pulls; the reference PS had none, /root/reference/asgd/optim/Asynchronous.py:
+    17-18,48-59).
+
+    With device links the applies run on several link streams at once, so a host
+    counter bumped at ENQUEUE time overstates what a snapshot holds (a reply could
+    carry only the requester's own deltas and say "version 4").  On GPU the count
+    is a device int32: :meth:`bump` runs on the applying stream right after the
+    apply kernel (it moves only once that apply has landed), :meth:`stamp` runs on
+    the replying stream BEFORE the snapshot copy (``csrc/optim.hip`` ps_count /
+    ps_stamp, agent-scope atomics).  A stamp therefore counts only applies the
+    snapshot fully contains; applies in flight elsewhere may show up in some
+    elements, never in the count.  On CPU applies are synchronous and the count
+    is a host integer."""
+
+    def __init__(self, device, native=None):
+        self.cuda = device.type == "cuda"
+        self.nat = native
+        self.host = 0
+        self.dev = torch.zeros(1, dtype=torch.int32, device=device) if self.cuda else None
+
+    def bump(self):
+        """One apply has been enqueued on the CURRENT stream (GPU: counted when it lands)."""
+        self.host += 1
+        if self.cuda:
+            self.nat.ps_count(self.dev, 1)
+
+    def set(self, value: int):
+        """The shard was overwritten (init / checkpoint) on the current stream."""
+        self.host = int(value)
+        if self.cuda:
+            self.nat.ps_count(self.dev, int(value), True)
+
+    def stamp(self, dst: torch.Tensor):
+        """Write the count into the 1-element fp32 ``dst`` on the current stream;
+        call it BEFORE the snapshot copy."""
+        if self.cuda:
+            self.nat.ps_stamp(self.dev, dst.reshape(1))
+        else:
+            dst.fill_(float(self.host))
+
+    def value(self) -> int:
+        """Landed count (host sync on GPU: stats / checkpoints only)."""
+        return int(self.dev.item()) if self.cuda else self.host
+
+
 class _Slot:
     __slots__ = ("buf", "free", "work")
 

@@ -43,7 +43,7 @@ import torch.distributed as dist
 
 from . import messaging as M
 from .arena import FlatArena
-from .links import PairGroupTransport, PairLinks, wait_on
+from .links import AppliedCount, PairGroupTransport, PairLinks, wait_on
 
 _LOG = logging.getLogger(__name__)
 
@@ -135,7 +135,9 @@ class ParameterServer:
         self._hq = None
         self._recv_bufs = defaultdict(dict)      # gloo payload path
         self._init_ev = None                     # last shard overwrite (device links)
-        self._applied_on: set = set()            # link streams that carry applies
+        # link streams that read or write the shard (applies AND reply snapshots):
+        # an overwrite (_set) orders behind all of them
+        self._touched_on: set = set()
         self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         if self.links is not None:
             # every worker's payload rings up front (fp32 and bf16 wire), not at
@@ -152,6 +154,9 @@ class ParameterServer:
             self._native = native()
         else:
             self._native = None
+        # applies wholly landed: the version a reply is stamped with (links.AppliedCount);
+        # self.version stays the host's ENQUEUE count (staleness of incoming pushes)
+        self.applied = AppliedCount(self.device, self._native)
         if self.links is not None:
             self._warm_kernels(padded)
 
@@ -167,8 +172,9 @@ class ParameterServer:
                 self._native.ps_apply(self.shard, z, None, self.delta_scale)
                 self._native.ps_apply(self.shard, z, None, self.delta_scale, True)
             snap = torch.empty(self.numel + 1, dtype=torch.float32, device=self.device)
+            self._native.ps_count(self.applied.dev, 0)
+            self._native.ps_stamp(self.applied.dev, snap[self.numel:])
             snap[: self.numel].copy_(self.shard[: self.numel])
-            snap[self.numel:].fill_(0.0)
         torch.cuda.synchronize(self.device)
 
     # -------------------------------------------------------------- payload io
@@ -196,15 +202,14 @@ class ParameterServer:
 
     def _reply(self, dst: int):
         """ParameterUpdate to ``dst``: the shard followed by one fp32 element holding
-        the PS version (number of applied deltas) the snapshot was taken at, so
-        the worker can report its staleness on its next push."""
+        the PS version of the snapshot -- the number of applies it WHOLLY contains
+        (:class:`.links.AppliedCount`: stamped on the device before the copy) --
+        so the worker can report its staleness on its next push."""
         n = self.numel
         if self.links is not None:
-            version = float(self.version)
-
             def fill(buf):
+                self.applied.stamp(buf[n:])     # first: counts only landed applies
                 buf[:n].copy_(self.shard[:n])   # snapshot: later applies never tear it
-                buf[n:].fill_(version)
 
             # snapshot on dst's OWN link stream: behind dst's own applies (same
             # stream) and the last initialisation, never behind another worker's
@@ -212,11 +217,12 @@ class ParameterServer:
             s = self.links.stream(dst)
             with torch.cuda.stream(s):
                 wait_on(s, self._init_ev)
+            self._touched_on.add(dst)
             self.links.send(dst, n + 1, torch.float32, fill, s)
         else:
             snap = torch.empty(n + 1, dtype=torch.float32)
             snap[:n].copy_(self.shard[:n])
-            snap[n] = float(self.version)
+            self.applied.stamp(snap[n:])     # gloo: applies are synchronous
             w = dist.isend(snap, dst, group=self.ctrl, tag=M.TAG_REPLY)
             self._tracker.add(w, snap)
         self.bytes_out += (n + 1) * 4
@@ -232,29 +238,35 @@ class ParameterServer:
                 wait_on(s, ready)
                 wait_on(s, self._init_ev)
                 self._native.ps_apply(self.shard, delta, None, self.delta_scale, True)
+                self.applied.bump()            # counted once this apply has landed
                 if slot is not None:
                     self.links.release(slot, s)
-            self._applied_on.add(sender)
+            self._touched_on.add(sender)
         elif self._native is not None:
             with torch.cuda.stream(self.stream):
                 wait_on(self.stream, ready)
                 self._native.ps_apply(self.shard, delta, None, self.delta_scale)
+                self.applied.bump()
                 if slot is not None:
                     self.links.release(slot, self.stream)
         else:
             self.shard[: self.numel].add_(delta[: self.numel].to(torch.float32),
                                           alpha=self.delta_scale)
+            self.applied.bump()
         self.version += 1
 
-    def _set(self, params: torch.Tensor, ready=None, slot=None):
+    def _set(self, params: torch.Tensor, ready=None, slot=None, version: int | None = None):
         with torch.cuda.stream(self.stream) if self.stream is not None else _null():
             wait_on(self.stream, ready)
-            # an overwrite orders against every apply already enqueued on a link
-            for p in sorted(self._applied_on):
+            # an overwrite orders against every apply AND reply snapshot already
+            # enqueued on a link (a reply in flight must not send a torn shard)
+            for p in sorted(self._touched_on):
                 ev = torch.cuda.Event()
                 ev.record(self.links.stream(p))
                 self.stream.wait_event(ev)
             self.shard[: self.numel].copy_(params[: self.numel])
+            if version is not None:
+                self.applied.set(version)   # the restored shard holds `version` applies
             if slot is not None:
                 self.links.release(slot, self.stream)
             if self.links is not None:
@@ -381,6 +393,7 @@ class ParameterServer:
         st = self.staleness
         return {
             "version": self.version,
+            "applied": self.applied.value(),
             "counts": dict(self.counts),
             "bytes_in": self.bytes_in,
             "bytes_out": self.bytes_out,
@@ -401,7 +414,7 @@ class ParameterServer:
         from ..utils.checkpoint import load_ps_checkpoint
 
         flat, version, _ = load_ps_checkpoint(path)
-        self._set(flat.to(self.device))
+        self._set(flat.to(self.device), version=version)
         self.version = version
         self.initialized = True
 

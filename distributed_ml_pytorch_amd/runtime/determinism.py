@@ -50,6 +50,11 @@ def enable_determinism(cfg):
     torch.use_deterministic_algorithms(True, warn_only=False)
     torch.backends.cudnn.deterministic = True
     torch.backends.cudnn.benchmark = False
+    # the one mode in which GPU ops may run on stock kernels: each (op, reason)
+    # sent there is logged once (ops/_policy.py)
+    from ..ops._policy import allow_stock
+
+    allow_stock(True, "--deterministic (fp32 on PyTorch's deterministic kernels)")
     if cfg.dtype != "fp32":
         _LOG.info("deterministic mode: compute dtype %s -> fp32 (PyTorch deterministic kernels)",
                   cfg.dtype)

@@ -114,6 +114,17 @@ class Worker:
         self.device = info.device if (cfg.cuda and info.device.type == "cuda") else \
             torch.device("cpu")
         self.compute_dtype = _dtype(cfg.dtype) if self.device.type == "cuda" else torch.float32
+        if self.device.type == "cuda" and self.compute_dtype != torch.bfloat16:
+            from ..ops._policy import is_allowed
+
+            if not is_allowed():
+                # the native kernels are bf16-compute (fp32 masters / accumulation);
+                # an fp32 GPU run would train entirely on MIOpen / hipBLASLt / ATen
+                raise ValueError(
+                    f"--dtype {cfg.dtype} on the GPU: every native gfx950 kernel computes "
+                    "in bf16 (fp32 master weights and accumulation), so this would train "
+                    "entirely on stock MIOpen / hipBLASLt / ATen kernels.  Use --dtype bf16, "
+                    "or --deterministic for the explicit fp32 stock-kernel oracle mode.")
         model, shape, nc = build_model(cfg.model, cfg.num_classes)
         self.input_shape, self.num_classes = shape, nc
         self.model = model.to(self.device)

@@ -9,7 +9,10 @@
 // step s+1 issued among step s's MFMAs, like conv.hip).  Variants:
 //   shape 16 : v_mfma_f32_16x16x32_bf16, wave tile (16*TM) x (16*TN)
 //   shape 32 : v_mfma_f32_32x32x16_bf16, wave tile (32*TM) x (32*TN)
-//   lds 0    : register-fed (fragments read once, kept live) -- MFMA pipe + clock only
+//   mode REG : register-fed (fragments read once, kept live) -- MFMA pipe + clock only
+//   mode LDS : both operands' fragments re-read from LDS every step
+//   mode AL  : A re-read from LDS every step, B register-resident across the loop
+//              (round 6: "one operand held in registers")
 // at NW waves per block and BPC blocks per CU.  Random operands throughout
 // (zero data raises the clock: MI355X_MICROARCH.md, DVFS give-back).
 //
@@ -48,7 +51,9 @@ __device__ __forceinline__ s16x8 rd(const char* lds, int row, int chunk) {
   return *reinterpret_cast<const s16x8*>(lds + (row & (kRows - 1)) * kRowBytes + swz(row, chunk) * 16);
 }
 
-template <int SHAPE, int TM, int TN, int NW, bool LDS>
+enum { REG = 0, LDS = 1, AL = 2 };
+
+template <int SHAPE, int TM, int TN, int NW, int MODE>
 __global__ void __launch_bounds__(64 * NW) mfma_loop(const short* __restrict__ src, float* out,
                                                       int nstep, int rowstep) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -86,8 +91,19 @@ __global__ void __launch_bounds__(64 * NW) mfma_loop(const short* __restrict__ s
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int cur = h, nxt = h ^ 1;
-      if (LDS) load(st + h + 1, nxt);
-      else {
+      if (MODE == LDS) {
+        load(st + h + 1, nxt);
+      } else if (MODE == AL) {
+        const int off = ((st + h + 1) % 9) * rowstep;
+#pragma unroll
+        for (int k = 0; k < KSUB; ++k) {
+          const int ch = SHAPE == 16 ? kh + 4 * ((st + h + 1) & 1) : 2 * k + kh + 4 * ((st + h + 1) & 1);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) af[nxt][k][i] = rd(lds, abase + off + i * FR, ch);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bf[0][k][j]));
+        }
+      } else {
 #pragma unroll
         for (int k = 0; k < KSUB; ++k) {
 #pragma unroll
@@ -102,8 +118,8 @@ __global__ void __launch_bounds__(64 * NW) mfma_loop(const short* __restrict__ s
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
-            const bf16x8_t a = __builtin_bit_cast(bf16x8_t, LDS ? af[cur][k][i] : af[0][k][i]);
-            const bf16x8_t b = __builtin_bit_cast(bf16x8_t, LDS ? bf[cur][k][j] : bf[0][k][j]);
+            const bf16x8_t a = __builtin_bit_cast(bf16x8_t, MODE != REG ? af[cur][k][i] : af[0][k][i]);
+            const bf16x8_t b = __builtin_bit_cast(bf16x8_t, MODE == LDS ? bf[cur][k][j] : bf[0][k][j]);
             if constexpr (SHAPE == 16)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc[i][j], 0, 0, 0);
             else
@@ -121,10 +137,10 @@ __global__ void __launch_bounds__(64 * NW) mfma_loop(const short* __restrict__ s
   out[blockIdx.x * 64 * NW + tid] = s;
 }
 
-template <int SHAPE, int TM, int TN, int NW, bool LDS>
+template <int SHAPE, int TM, int TN, int NW, int MODE>
 void run(const char* name, const short* src, float* out, int bpc, int ncu, double clk_ghz) {
   const int nstep = 4096, rowstep = 35;
-  auto k = mfma_loop<SHAPE, TM, TN, NW, LDS>;
+  auto k = mfma_loop<SHAPE, TM, TN, NW, MODE>;
   const size_t lds = kRows * kRowBytes;
   CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int grid = ncu * bpc;
@@ -170,21 +186,32 @@ int main() {
   const double clk = 2.4;
   std::printf("MFMA loop ceiling, %d CUs, random bf16, 4096 32-deep steps per wave\n", ncu);
   // the halo kernels' wave tiles, 16x16x32
-  run<16, 4, 4, 4, true>("16x16x32 64x64 LDS  4 waves", src, out, 1, ncu, clk);
-  run<16, 4, 4, 4, true>("16x16x32 64x64 LDS  4 waves", src, out, 2, ncu, clk);
-  run<16, 2, 4, 8, true>("16x16x32 32x64 LDS  8 waves", src, out, 1, ncu, clk);
-  run<16, 4, 4, 8, true>("16x16x32 64x64 LDS  8 waves", src, out, 1, ncu, clk);
-  run<16, 8, 4, 4, true>("16x16x32 128x64 LDS 4 waves", src, out, 1, ncu, clk);
-  run<16, 4, 4, 4, false>("16x16x32 64x64 REG  4 waves", src, out, 1, ncu, clk);
-  run<16, 4, 4, 8, false>("16x16x32 64x64 REG  8 waves", src, out, 1, ncu, clk);
+  run<16, 4, 4, 4, LDS>("16x16x32 64x64 LDS  4 waves", src, out, 1, ncu, clk);
+  run<16, 4, 4, 4, LDS>("16x16x32 64x64 LDS  4 waves", src, out, 2, ncu, clk);
+  run<16, 2, 4, 8, LDS>("16x16x32 32x64 LDS  8 waves", src, out, 1, ncu, clk);
+  run<16, 4, 4, 8, LDS>("16x16x32 64x64 LDS  8 waves", src, out, 1, ncu, clk);
+  run<16, 8, 4, 4, LDS>("16x16x32 128x64 LDS 4 waves", src, out, 1, ncu, clk);
+  run<16, 4, 4, 4, REG>("16x16x32 64x64 REG  4 waves", src, out, 1, ncu, clk);
+  run<16, 4, 4, 8, REG>("16x16x32 64x64 REG  8 waves", src, out, 1, ncu, clk);
   // the same wave tiles on 32x32x16
-  run<32, 2, 2, 4, true>("32x32x16 64x64 LDS  4 waves", src, out, 1, ncu, clk);
-  run<32, 2, 2, 4, true>("32x32x16 64x64 LDS  4 waves", src, out, 2, ncu, clk);
-  run<32, 1, 2, 8, true>("32x32x16 32x64 LDS  8 waves", src, out, 1, ncu, clk);
-  run<32, 2, 2, 8, true>("32x32x16 64x64 LDS  8 waves", src, out, 1, ncu, clk);
-  run<32, 4, 2, 4, true>("32x32x16 128x64 LDS 4 waves", src, out, 1, ncu, clk);
-  run<32, 2, 2, 4, false>("32x32x16 64x64 REG  4 waves", src, out, 1, ncu, clk);
-  run<32, 2, 2, 8, false>("32x32x16 64x64 REG  8 waves", src, out, 1, ncu, clk);
+  run<32, 2, 2, 4, LDS>("32x32x16 64x64 LDS  4 waves", src, out, 1, ncu, clk);
+  run<32, 2, 2, 4, LDS>("32x32x16 64x64 LDS  4 waves", src, out, 2, ncu, clk);
+  run<32, 1, 2, 8, LDS>("32x32x16 32x64 LDS  8 waves", src, out, 1, ncu, clk);
+  run<32, 2, 2, 8, LDS>("32x32x16 64x64 LDS  8 waves", src, out, 1, ncu, clk);
+  run<32, 4, 2, 4, LDS>("32x32x16 128x64 LDS 4 waves", src, out, 1, ncu, clk);
+  run<32, 2, 2, 4, REG>("32x32x16 64x64 REG  4 waves", src, out, 1, ncu, clk);
+  run<32, 2, 2, 8, REG>("32x32x16 64x64 REG  8 waves", src, out, 1, ncu, clk);
+  // round 6: more reuse per LDS byte: 128x64 / 64x128
+  // wave tiles at two waves per SIMD (8 waves, 128 fp32 accumulators per lane),
+  // and one operand register-resident across the loop
+  run<16, 8, 4, 8, LDS>("16x16x32 128x64 LDS 8 waves", src, out, 1, ncu, clk);
+  run<32, 4, 2, 8, LDS>("32x32x16 128x64 LDS 8 waves", src, out, 1, ncu, clk);
+  run<32, 2, 4, 8, LDS>("32x32x16 64x128 LDS 8 waves", src, out, 1, ncu, clk);
+  run<16, 4, 4, 8, AL>("16x16x32 64x64 A-LDS B-REG 8 waves", src, out, 1, ncu, clk);
+  run<16, 8, 4, 8, AL>("16x16x32 128x64 A-LDS B-REG 8 wv", src, out, 1, ncu, clk);
+  run<32, 2, 2, 8, AL>("32x32x16 64x64 A-LDS B-REG 8 waves", src, out, 1, ncu, clk);
+  run<32, 4, 2, 8, AL>("32x32x16 128x64 A-LDS B-REG 8 wv", src, out, 1, ncu, clk);
+  run<32, 4, 2, 4, AL>("32x32x16 128x64 A-LDS B-REG 4 wv", src, out, 1, ncu, clk);
   CHECK(hipFree(src));
   CHECK(hipFree(out));
   return 0;

@@ -69,6 +69,7 @@ def test_async_sharded_every_push_applied_once():
         st = out[r]["stats"]
         # this shard applied its own 7 pushes in-process + 7 from each other rank
         assert st["shard_version"] == world * steps
+        assert st["shard_applied"] == world * steps
         assert st["shard_counts"]["GradientUpdate"] == (world - 1) * steps
         assert st["shard_counts"]["ParameterRequest"] == (world - 1) * len(range(0, steps, 3))
         assert st["pushes"] == steps
@@ -110,6 +111,7 @@ def test_async_sharded_link_rings_with_a_slow_peer():
         torch.testing.assert_close(got[: want.numel()], want, rtol=1e-5, atol=1e-5)
         st = out[r]["stats"]
         assert st["shard_version"] == world * steps
+        assert st["shard_applied"] == world * steps
         links = st["shard_links"]
         assert links["recv"] == (world - 1) * steps
         assert links["reused"] >= (world - 1) * (steps - 2)     # depth-2 rings

@@ -848,3 +848,37 @@ def test_bottleneck_deferred_dres(stride, cin, planes, monkeypatch):
             assert d["deferred"] == 0, d
     for a, b in zip(grads[False], grads[True]):
         assert _rel(b, a) < 5e-3, _rel(b, a)
+
+
+@pytest.mark.parametrize("kind", ["basic32", "bottleneck256"])
+def test_residual_mark_on_bn_output_input(kind, monkeypatch):
+    """a block whose input is a native BatchNorm output.  For
+    BasicBlock(32, 32) conv1 is off the native path and hands x itself back as the
+    shortcut, which also feeds conv1: the residual must NOT be marked single-use
+    (bn2 would hand its unmasked dY over tagged, autograd would sum it with conv1's
+    dx and drop the mask).  Gradients with the deferred mask == DMP_BN_DEFER_RES=0."""
+    from distributed_ml_pytorch_amd.models.resnet import BasicBlock, Bottleneck
+    from distributed_ml_pytorch_amd.ops import functional as Fn
+    from distributed_ml_pytorch_amd.ops import layers as L
+
+    torch.manual_seed(0)
+    if kind == "basic32":
+        C, blk, hw = 32, BasicBlock(32, 32, 1), 16
+    else:
+        C, blk, hw = 256, Bottleneck(256, 64, 1), 14
+    pre = L.BatchNorm2d(C, relu=True).cuda()
+    blk = blk.cuda()
+    x0 = torch.randn(4, C, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    g = torch.randn(4, C, hw, hw, device="cuda")
+    grads = {}
+    for defer in (False, True):
+        monkeypatch.setattr(Fn, "_BN_DEFER_RES", defer)
+        blk.zero_grad(set_to_none=True)
+        pre.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        (blk(pre(x)).float() * g).sum().backward()
+        torch.cuda.synchronize()
+        grads[defer] = [x.grad.float()] + [p.grad.float() for p in
+                                           list(pre.parameters()) + list(blk.parameters())]
+    for a, b in zip(grads[False], grads[True]):
+        assert _rel(b, a) < 5e-3, _rel(b, a)

@@ -134,6 +134,12 @@ def _scenario(uneven: bool = False):
         cands = [own, own + deltas[other][0], own + deltas[other][0] + deltas[other][1]]
         per_elem = torch.stack([(reply[:n] - c).abs() for c in cands]).min(0).values
         errs = [float(per_elem.max())] + [float((reply[:n] - c).abs().max()) for c in cands]
+        # the version stamp counts applies the snapshot WHOLLY contains (own two +
+        # `claimed` of the other worker's): every element must hold at least those
+        stamp = int(float(reply[n]))
+        claimed = stamp - 2
+        stamp_ok = 0 <= claimed <= 2 and float(torch.stack(
+            [(reply[:n] - c).abs() for c in cands[claimed:]]).min(0).values.max()) < 1e-4
         recvs = [(p, a, b) for k, p, a, b in tr.spans if k == "recv"]
         sends = [(p, a, b) for k, p, a, b in tr.spans if k == "send"]
         a1 = recvs[0][1]
@@ -146,6 +152,7 @@ def _scenario(uneven: bool = False):
             "w1_first_recv_end": a1.elapsed_time(w1[0][1]),
             "reply_end": a1.elapsed_time(sends[-1][2]),
             "reply_version": float(reply[n]), "version": ps.version,
+            "stamp_ok": stamp_ok, "applied": ps.applied.value(),
             "order": [p for p, _, _ in recvs],
             "dur1": a1.elapsed_time(recvs[0][2]),
             "start2": a1.elapsed_time(recvs[1][1]),
@@ -189,7 +196,10 @@ def test_ps_links_overlap_receives(queues):
     # (b) every delta applied exactly once (any order: fp32 atomics, so a
     # tolerance); (c) the reply saw at least worker 1's own applies
     assert r["master_err"] < 1e-4 and r["reply_err"] < 1e-4, r
-    assert r["version"] == 4 and r["reply_version"] == 4.0
+    # the stamp is what the snapshot wholly holds (device applied-count read on the
+    # replying stream before the copy), not the host's enqueue count
+    assert r["version"] == 4 and r["applied"] == 4 and r["stamp_ok"], r
+    assert 2.0 <= r["reply_version"] <= 4.0, r
     assert r["order"] == [1, 2, 1, 2]
     # the same peer's transfers stay ordered on its link
     assert r["w1_second_start"] >= r["w1_first_end"] - 1e-3, r
@@ -209,7 +219,11 @@ def test_ps_completion_ordered_applies():
     print(r)
     assert r["master_err"] < 1e-4, r
     assert r["reply_err_own"] < 1e-4 and r["reply_prefix"] == 0, r
-    assert r["version"] == 4 and r["links"]["recv"] == 4 and r["links"]["send"] == 1
+    # the reply holds worker 2's own two applies only, and says so (VERDICT r5 #2:
+    # it used to carry the host enqueue count, 4)
+    assert r["reply_version"] == 2.0 and r["stamp_ok"], r
+    assert r["version"] == 4 and r["applied"] == 4
+    assert r["links"]["recv"] == 4 and r["links"]["send"] == 1
     assert r["reply_end"] < r["w1_first_recv_end"], r
 
 
