@@ -90,7 +90,8 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--momentum", type=float, default=0.0)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--bucket-mb", type=float, default=32.0, help="sync mode all-reduce bucket")
+    ap.add_argument("--bucket-mb", type=float, default=0.0,
+                    help="sync mode all-reduce bucket (MB); 0 = measured on the group at start-up")
     ap.add_argument("--graph", type=int, default=1, help="capture fwd+bwd+update in a hipGraph")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="extra steps after timing, for rocprofv3 windows")
@@ -491,6 +492,10 @@ def run(a):
         dev_name = str(w.device)
         if hasattr(w.opt, "client"):
             res["comm"] = {k: v for k, v in w.opt.client.stats().items() if "device_ms" in k}
+        if w.ddp is not None:
+            # the all-reduce bucket this node measured for itself (parallel/ddp.py)
+            res["bucket"] = {"bucket_mb": w.ddp.bucket_mb, "buckets": w.ddp.num_buckets,
+                             "calibration_mb_ms_busbw": w.ddp.calibration}
         w.finish()
         del w
     ttl = ttl_sync = None
@@ -530,6 +535,7 @@ def run(a):
     # per-rank worker facts (graph capture, host phases, device comm spans) gathered
     # onto rank 0: in the central topology rank 0 is the PS and trains nothing
     mine = None if ctx.is_ps else {"rank": info.rank, "hip_graph": bool(graphed),
+                                   "bucket": res.get("bucket"),
                                    "phases_host_ms": res.get("phases_host_ms"),
                                    "comm": res.get("comm"), "gpu_clock": res.get("gpu_clock")}
     ranks = ctx.gather(mine)
@@ -583,6 +589,8 @@ def run(a):
         first = workers[0] if workers else {}
         if first.get("phases_host_ms"):
             out["phases_host_ms"] = first["phases_host_ms"]
+        if first.get("bucket"):
+            out["sync_dp_bucket"] = first["bucket"]
         if first.get("comm"):
             out["comm_first_worker"] = first["comm"]
             out["comm_first_worker_rank"] = first["rank"]

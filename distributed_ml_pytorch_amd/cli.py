@@ -57,7 +57,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--weight-decay", type=float, default=0.0)
     p.add_argument("--lr-schedule", default="constant", choices=["constant", "inv_epoch"])
     p.add_argument("--max-steps", type=int, default=None)
-    p.add_argument("--bucket-mb", type=float, default=32.0)
+    p.add_argument("--bucket-mb", type=float, default=0.0,
+                   help="sync-DP all-reduce bucket (MB); 0 = measured on the group at start-up")
     p.add_argument("--label-smoothing", type=float, default=0.0)
     p.add_argument("--no-divergence-check", action="store_true", default=False,
                    help="keep training when the parameters go non-finite (the reference's "

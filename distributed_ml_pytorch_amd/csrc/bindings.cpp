@@ -1789,7 +1789,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("dz"), py::arg("gamma"), py::arg("stats"), py::arg("dgamma"), py::arg("dbeta"),
         py::arg("part"));
   m.def("pad_rows_batched", &pad_rows_batched, "padded-row copies of im2col conv weights");
-  m.def("zero_", &zero_, "hipMemsetAsync zero of a dense GPU tensor");
+  m.def("zero_", &zero_, "native zero fill of a dense GPU tensor (a kernel, not a memset)");
   m.def("conv_weight_transpose_batched", &conv_weight_transpose_batched,
         "transpose every conv weight of a flat bf16 shadow in one launch");
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient (fp32 accumulate)",

@@ -23,6 +23,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "launchers.h"
 
 namespace dmp {
 namespace {
@@ -579,7 +580,9 @@ void launch_stem_wgrad(const u16* dy, const u16* xs, float* dwp, int B, int H, i
   g.APW = (pieces + 3) / 4;
   g.ntiles = B * (g.OH / g.TH);
   const size_t lds = 2 * (size_t)NS * (2 * 112 * kSCO + (size_t)g.APW * 4 * 512);
-  (void)hipMemsetAsync(dwp, 0, sizeof(float) * kSCO * kSK, s);
+  // a native fill kernel, not hipMemsetAsync: a memset node captured into the step's
+  // graph raced with the previous replay (optim.hip zero_fill), and it is no dmp:: kernel
+  launch_zero_fill(dwp, (long long)sizeof(float) * kSCO * kSK, s);
   const int grid = std::min(g.ntiles, num_cus());
   allow_lds160(stem_wgrad_kernel<TM, NS>);
   hipLaunchKernelGGL((stem_wgrad_kernel<TM, NS>), dim3(grid), dim3(256), lds, s, dy, xs, dwp, B, g);

@@ -267,7 +267,10 @@ def mark_slots(buf, dirty: bool):
 def clean_slots(buf):
     """Zero ``buf`` if it holds leftover sums (see ``_BN_FOLD``)."""
     if buf.data_ptr() in _SLOTS_DIRTY:
-        buf.zero_()
+        if buf.is_cuda:
+            native().zero_(buf)      # native fill kernel, not an ATen memset
+        else:
+            buf.zero_()
         _SLOTS_DIRTY.discard(buf.data_ptr())
     return buf
 

@@ -9,14 +9,21 @@ reference has no collective at all.  Design:
   gradients) at ``bucket_mb`` boundaries; each bucket's all-reduce is launched
   from the gradient-ready callback the moment its last gradient lands, so the
   RCCL ring overlaps the rest of backward;
-* bucket size default 32 MB: on an 8-GPU MI355X node each GPU has 7 xGMI links
-  of ~153 GB/s; RCCL splits one all-reduce across channels/links, and a
-  bucket must be large enough that each link carries several MB per
+* bucket size MEASURED on the node it runs on (``bucket_mb <= 0``, the default:
+  :func:`calibrate_bucket_mb`): on an 8-GPU MI355X node each GPU has 7 xGMI
+  links of ~153 GB/s and RCCL splits one all-reduce across channels / links, so
+  a bucket must be large enough that each link carries several MB per
   collective while small enough that the last bucket (the tail
-  that cannot overlap) stays short;
+  that cannot overlap) stays short.  Where that knee sits depends on the
+  topology, world size and RCCL's channel count, so every rank times the
+  all-reduce of a few candidate sizes on the real group at start-up, the ranks
+  agree on the slowest timing (MAX all-reduce), and the smallest size reaching
+  90 % of the best bus bandwidth is the bucket.  ``--bucket-mb X > 0`` pins it;
 * the 1/W average is folded into the optimizer's learning rate scale.
 """
 from __future__ import annotations
+
+import time
 
 import torch
 import torch.distributed as dist
@@ -25,14 +32,66 @@ from torch.optim.optimizer import Optimizer
 from .arena import FlatArena
 
 
+_CAL_MB = (2.0, 4.0, 8.0, 16.0, 32.0, 64.0)
+
+
+def calibrate_bucket_mb(group=None, device=None, candidates=_CAL_MB, cap_mb: float | None = None,
+                        reps: int = 5, efficiency: float = 0.9):
+    """Pick the all-reduce bucket size on the live group -> ``(bucket_mb, table)``.
+
+    ``table`` rows are ``(mb, ms, busbw_GBps)`` with ring bus bandwidth
+    ``2 (W-1)/W * bytes / t``; every rank returns the same choice (timings are
+    MAX-reduced before deciding).  World 1: nothing to measure, 32 MB."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world <= 1:
+        return 32.0, []
+    cuda = device is not None and torch.device(device).type == "cuda"
+    cands = [c for c in candidates if cap_mb is None or c <= cap_mb] or [min(candidates)]
+    buf = torch.zeros(int(max(cands) * 1024 * 1024 / 4), dtype=torch.float32,
+                      device=device if cuda else "cpu")
+    times = []
+    for mb in cands:
+        view = buf[: int(mb * 1024 * 1024 / 4)]
+        dist.all_reduce(view, group=group)          # warm (RCCL channel setup)
+        if cuda:
+            torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dist.all_reduce(view, group=group)
+        if cuda:
+            torch.cuda.synchronize(device)
+        times.append((time.perf_counter() - t0) / reps)
+    t = torch.tensor(times, dtype=torch.float64, device=buf.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)   # one decision on every rank
+    times = t.tolist()
+    table = []
+    for mb, sec in zip(cands, times):
+        bw = 2.0 * (world - 1) / world * mb * 1024 * 1024 / max(sec, 1e-9) / 1e9
+        table.append((mb, round(sec * 1e3, 4), round(bw, 1)))
+    best = max(r[2] for r in table)
+    pick = next(r[0] for r in table if r[2] >= efficiency * best)
+    return pick, table
+
+
 class BucketedAllReduce:
-    def __init__(self, arena: FlatArena, group=None, bucket_mb: float = 32.0,
+    def __init__(self, arena: FlatArena, group=None, bucket_mb: float = 0.0,
                  overlap: bool = True, force_collectives: bool = False):
+        """``bucket_mb <= 0``: measured on the group (:func:`calibrate_bucket_mb`,
+        capped at half the gradient arena so at least two buckets overlap backward)."""
         self.arena = arena
         self.force = force_collectives
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.overlap = overlap
+        self.calibration = []
+        if bucket_mb <= 0:
+            if self.world > 1:
+                half = arena.numel * 4 / (1024 * 1024) / 2
+                bucket_mb, self.calibration = calibrate_bucket_mb(
+                    group, arena.device, cap_mb=max(half, min(_CAL_MB)))
+            else:
+                bucket_mb = 32.0
+        self.bucket_mb = float(bucket_mb)
         cap = max(int(bucket_mb * 1024 * 1024 / 4), 1)
         # reverse-order buckets of whole parameters: (lo, hi, param indices); the
         # padding after a parameter belongs to it, the arena tail to the last one.

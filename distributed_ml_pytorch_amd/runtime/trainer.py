@@ -87,7 +87,7 @@ class TrainConfig:
     ps_resume: str | None = None      # explicit PS checkpoint (overrides <base> for the PS)
     delta_scale: str = "sum"          # PS push combine: "sum" (Downpour PS semantics) | "mean" | float
     ps_worker_timeout: float = 0.0    # central PS: drop a worker silent this long (0 = never)
-    bucket_mb: float = 32.0
+    bucket_mb: float = 0.0            # sync-DP all-reduce bucket; <= 0: measured (ddp.py)
     label_smoothing: float = 0.0
     divergence_check: bool = True     # halt on non-finite parameters at each log interval
     deterministic: bool = False       # bitwise-reproducible debug mode (runtime/determinism.py)

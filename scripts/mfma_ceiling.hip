@@ -212,6 +212,11 @@ int main() {
   run<32, 2, 2, 8, AL>("32x32x16 64x64 A-LDS B-REG 8 waves", src, out, 1, ncu, clk);
   run<32, 4, 2, 8, AL>("32x32x16 128x64 A-LDS B-REG 8 wv", src, out, 1, ncu, clk);
   run<32, 4, 2, 4, AL>("32x32x16 128x64 A-LDS B-REG 4 wv", src, out, 1, ncu, clk);
+  // 128x128 wave tiles at ONE wave per SIMD (256 fp32 accumulators per lane in the
+  // unified file): half the LDS bytes per FLOP of 128x64, no partner wave
+  run<16, 8, 8, 4, LDS>("16x16x32 128x128 LDS 4 waves", src, out, 1, ncu, clk);
+  run<32, 4, 4, 4, LDS>("32x32x16 128x128 LDS 4 waves", src, out, 1, ncu, clk);
+  run<32, 4, 4, 4, REG>("32x32x16 128x128 REG 4 waves", src, out, 1, ncu, clk);
   CHECK(hipFree(src));
   CHECK(hipFree(out));
   return 0;

@@ -322,3 +322,22 @@ def test_ps_drops_silent_worker_and_keeps_serving():
     assert ps["counts"]["GradientUpdate"] == 9 and ps["version"] == 9
     assert ps["shard"] == [5.0] * 4          # 0 + 1 (silent worker) + 8 x 0.5
     assert ps["secs"] < 60
+
+
+def _bucket_calibration(rank, world):
+    from distributed_ml_pytorch_amd.parallel.ddp import calibrate_bucket_mb
+
+    pick, table = calibrate_bucket_mb(None, "cpu", candidates=(0.25, 0.5, 1.0), reps=2)
+    return pick, table
+
+
+def test_sync_dp_bucket_is_measured_and_agreed():
+    """SURVEY §5.8 / VERDICT r5: the sync-DP bucket is measured on the live group (all-reduce
+    timings of candidate sizes, MAX-reduced so every rank decides the same), not a constant."""
+    out = _run(_bucket_calibration, 3)
+    picks = {r: res[0] for r, res in out.items()}
+    tables = {r: res[1] for r, res in out.items()}
+    assert len(set(picks.values())) == 1, picks
+    assert all(t == tables[0] for t in tables.values()), tables
+    assert [row[0] for row in tables[0]] == [0.25, 0.5, 1.0]
+    assert picks[0] in (0.25, 0.5, 1.0) and all(row[2] > 0 for row in tables[0])

@@ -13,8 +13,10 @@ import torch
 
 pytestmark = [pytest.mark.gpu, pytest.mark.strict_native]
 
+# (vit_tiny's head dim 16 is outside the fused attention kernel: on the GPU it runs
+# only in the oracle mode, which test_op_outside_native_coverage_raises covers)
 MODELS = [("resnet18", 16), ("resnet50", 4), ("vit_b16", 2), ("alexnet", 16), ("lenet", 16),
-          ("mlp", 16), ("vit_tiny", 8)]
+          ("mlp", 16)]
 
 
 def _is_copy(name: str) -> bool:
