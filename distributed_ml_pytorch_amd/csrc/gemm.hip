@@ -225,27 +225,10 @@ __device__ __forceinline__ bf16x8 frag(const u16* img, int r, int ks, int lane) 
 //     every wave's vmcnt count stays uniform.
 // OCC > 0: at least OCC waves per SIMD (the register budget that lets two 8-wave
 // blocks share a CU, so one block's prologue / epilogue overlaps the other's MFMAs)
-//
-// RP = true (round 6): register-pipelined k-loop for ONE wave per SIMD with big
-// wave tiles (4 waves of 128 x 128 on a 256 x 256 tile: 256 fp32 accumulators per
-// lane, half the LDS bytes per FLOP of the 8-wave 128 x 64 tiles; the bare loop's
-// ceiling is 70 % of peak against 64 %, profiles/mfma_loop_ceiling_r6.txt).  With
-// no partner wave on the SIMD, nothing hides a fragment read behind another wave's
-// MFMAs, so the wave hides its OWN: k-tile t's MFMAs run from one register set
-// while k-tile t+1's fragments stream into the other, the reads pinned between the
-// MFMAs (sched_group_barrier).  BK = 32, an NS-deep LDS-DMA ring (NS = 3 or 4),
-// NS-1 k-tiles in flight; one raw barrier per k-tile, in the middle of its MFMAs
-// (the first half runs on registers alone and covers the barrier skew):
-//   [stage t+NS-1 | MFMA half 1 of t | vmcnt: t+1 landed; lgkmcnt(0); s_barrier |
-//    MFMA half 2 of t interleaved with the reads of t+1]
-//   * RAW: k-tile t+1 is read only after every wave waited for its own DMAs of it
-//     and passed the barrier;
-//   * WAR: stage t+NS-1 overwrites slot (t-1) % NS, whose fragments every wave
-//     read before the barrier of iteration t-1 (lgkmcnt(0) ahead of it);
-//   * past the last k-tile the DMAs read zeros into slots nobody reads, so every
-//     wave's vmcnt count stays uniform.
+// (Round 6 also built a register-pipelined one-wave-per-SIMD 128x128 k-loop here; it measured
+// slower than the ping-pong tiles and was removed: profiles/gemm_rp_tiles_r6.txt.)
 template <int BM, int BN, int BK, int WM, int WN, int NS, bool AT, bool BT, int EPI, int KG = 1,
-          bool PP = false, int OCC = 0, bool RP = false>
+          bool PP = false, int OCC = 0>
 __global__ void __launch_bounds__(64 * WM * WN * KG)
 __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) {
   constexpr int NWG = WM * WN, NW = NWG * KG;
@@ -569,68 +552,7 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
 
   // bias (fwd) into the accumulators before any DMA is in flight
   tile_init(m0, n0);
-  if constexpr (RP) {
-    static_assert(KG == 1 && (NS == 3 || NS == 4) && BK == 32 && !PP,
-                  "register-pipelined tiles: BK 32, 3 or 4 slots");
-    static_assert(SA::INS % NW == 0 && SB::INS % NW == 0, "uniform DMA count per wave");
-    static_assert(TM % 2 == 0, "two MFMA halves");
-    constexpr int PWK = SA::PW_MIN + SB::PW_MIN;   // DMAs per wave per k-tile
-    constexpr int NRD = (AT ? 2 : 1) * TM + (BT ? 2 : 1) * TN;   // LDS reads per k-tile
-    bf16x8 a0[TM], b0[TN], a1[TM], b1[TN];
-    auto rd = [&](bf16x8 (&af)[TM], bf16x8 (&bf)[TN], int kt) {
-      const u16* As = lds + (kt % NS) * STAGE;
-      const u16* Bs = As + SA::EL;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag<BM, AT, BK>(As, ra + i * 16, 0, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = frag<BN, BT, BK>(Bs, rb + j * 16, 0, lane);
-    };
-    auto mf = [&](const bf16x8 (&af)[TM], const bf16x8 (&bf)[TN], int i0, int i1) {
-#pragma unroll
-      for (int i = i0; i < i1; ++i) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = TRANS_OUT ? mfma_bf16(bf[j], af[i], acc[i][j])
-                                : mfma_bf16(af[i], bf[j], acc[i][j]);
-        if (EPI == EPI_ACC32 && do_bias) accb[i] = mfma_bf16(af[i], ones, accb[i]);
-      }
-    };
-    // one k-tile: MFMAs from (ac, bc); k-tile kt + 1's fragments into (an, bn)
-    auto body = [&](bf16x8 (&ac)[TM], bf16x8 (&bc)[TN], bf16x8 (&an)[TM], bf16x8 (&bn)[TN],
-                    int kt) {
-      stage((kt + NS - 1) % NS, kt + NS - 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mf(ac, bc, 0, TM / 2);
-      __builtin_amdgcn_sched_barrier(0);
-      gwait_vm<(NS - 2) * PWK>();                   // k-tile kt+1 landed (this wave)
-      __builtin_amdgcn_s_barrier();                 // ... and for every wave
-      __builtin_amdgcn_sched_barrier(0);
-      rd(an, bn, kt + 1);
-      mf(ac, bc, TM / 2, TM);
-      // pin the reads between the second half's MFMAs: one read per MFMA pair
-#pragma unroll
-      for (int r = 0; r < NRD; ++r) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, TM * TN / 2 - 2 * NRD > 0
-                                                      ? TM * TN / 2 - 2 * NRD : 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    };
-#pragma unroll
-    for (int s0 = 0; s0 < NS - 1; ++s0) stage(s0, s0);   // k-tiles past KT load zeros
-    gwait_vm<(NS - 2) * PWK>();                     // k-tile 0 landed (this wave)
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    rd(a0, b0, 0);
-    int kt = 0;
-    for (; kt + 1 < KT; kt += 2) {
-      body(a0, b0, a1, b1, kt);
-      body(a1, b1, a0, b0, kt + 1);
-    }
-    if (kt < KT) body(a0, b0, a1, b1, kt);
-    gwait_vm<0>();     // the zero-read DMAs past KT land before the epilogue reuses the LDS
-  } else if constexpr (PP) {
+  if constexpr (PP) {
     static_assert(WM == 2 && KG == 1 && NS == 4 && BK == 32, "ping-pong tiles: 2 wave rows, BK 32, 4 slots");
     static_assert(SA::INS % NW == 0 && SB::INS % NW == 0, "uniform DMA count per wave");
     constexpr int PWK = SA::PW_MIN + SB::PW_MIN;   // DMAs per wave per k-tile
@@ -907,7 +829,7 @@ void launch_small(const GemmArgs& g, int splits, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ configs
-struct Cfg { int bm, bn, bk, wm, wn, ns, kg = 1, pp = 0, occ = 0, rp = 0; };
+struct Cfg { int bm, bn, bk, wm, wn, ns, kg = 1, pp = 0, occ = 0; };
 // LDS = ns * (bm + bn) * bk * 2 B.  Tile heights 160 / 192 exist for tile
 // counts: M = 12608 tokens x N = 768 is 150 tiles of 256x256 (59 % of 256 CUs)
 // but 237 of 160x256.  A k-strided (transposed) operand needs a tile side that
@@ -930,9 +852,6 @@ constexpr Cfg kCfgs[] = {
     {128, 256, 32, 2, 4, 2, 1, 0, 4},   // 13: 48 KiB, 8 waves of 64x64
     {128, 256, 32, 2, 4, 3, 1, 0, 4},   // 14: 72 KiB, 8 waves of 64x64
     {256, 128, 32, 4, 2, 2, 1, 0, 4},   // 15: 48 KiB, 8 waves of 64x64
-    // register-pipelined, one wave per SIMD (round 6): 16-17
-    {256, 256, 32, 2, 2, 4, 1, 0, 0, 1},   // 16: 128 KiB, 4 waves of 128x128
-    {128, 256, 32, 1, 2, 3, 1, 0, 0, 1},   // 17: 72 KiB, 2 waves of 128x128, two blocks / CU
 };
 // (4 waves of 128x128 per 256x256 / 192x256 tile, accumulators in AGPRs: 20-40 %
 // slower than the 8-wave tiles on every ViT shape -- profiles/gemm_vs_hipblaslt_r2.txt)
@@ -946,7 +865,7 @@ constexpr bool cfg_ok(const Cfg& c, bool at, bool bt) {
 constexpr int cfg_blocks_per_cu(const Cfg& c) {
   const int lds = c.ns * (c.bm + c.bn) * c.bk * 2;
   const int by_lds = (160 * 1024) / (lds > 0 ? lds : 1);
-  const int by_regs = c.rp ? 4 / (c.wm * c.wn) : (c.occ > 0 || c.wm * c.wn * c.kg <= 4) ? 2 : 1;
+  const int by_regs = (c.occ > 0 || c.wm * c.wn * c.kg <= 4) ? 2 : 1;
   return by_lds < by_regs ? (by_lds < 1 ? 1 : by_lds) : by_regs;
 }
 
@@ -1008,7 +927,7 @@ void launch_cfg(const GemmArgs& a, int splits, hipStream_t s) {
     }
     if constexpr (c.kg == 1 || EPI == EPI_ACC32)
       hipLaunchKernelGGL((gemm_kernel<c.bm, c.bn, c.bk, c.wm, c.wn, c.ns, AT, BT, EPI, c.kg,
-                                      c.pp != 0, c.occ, c.rp != 0>),
+                                      c.pp != 0, c.occ>),
                          dim3((unsigned)grid_x, (unsigned)grid_y), dim3(64 * c.wm * c.wn * c.kg), 0,
                          s, g);
     else
@@ -1035,9 +954,7 @@ void launch_mode(int cfg, const GemmArgs& a, int splits, hipStream_t s) {
     case 12: launch_cfg<12, AT, BT, EPI>(a, splits, s); break;
     case 13: launch_cfg<13, AT, BT, EPI>(a, splits, s); break;
     case 14: launch_cfg<14, AT, BT, EPI>(a, splits, s); break;
-    case 15: launch_cfg<15, AT, BT, EPI>(a, splits, s); break;
-    case 16: launch_cfg<16, AT, BT, EPI>(a, splits, s); break;
-    default: launch_cfg<17, AT, BT, EPI>(a, splits, s); break;
+    default: launch_cfg<15, AT, BT, EPI>(a, splits, s); break;
   }
 }
 
