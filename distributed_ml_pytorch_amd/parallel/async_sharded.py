@@ -388,8 +388,14 @@ class AsyncShardedPSClient(PSClient):
         sn = self.shard_n
         free = self._pull_free.popleft() if len(self._pull_free) > self.staleness else None
         if free is None:
-            bufs = {o: torch.empty(sn + (0 if o == self.rank else 1), dtype=torch.float32,
-                                   device=self.device) for o in range(self.world)}
+            # allocated on the side stream that receives into them (deterministic mode
+            # NaN-fills torch.empty on the allocating stream); the own shard's snapshot
+            # stream orders behind that too
+            with (torch.cuda.stream(self.side) if self.cuda else _Null()):
+                bufs = {o: torch.empty(sn + (0 if o == self.rank else 1), dtype=torch.float32,
+                                       device=self.device) for o in range(self.world)}
+            if self.cuda:
+                self.server.stream.wait_stream(self.side)
             free_ev = None
         else:
             bufs, free_ev = free

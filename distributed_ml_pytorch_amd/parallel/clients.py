@@ -256,11 +256,17 @@ class LocalPSClient(PSClient):
     forward on a side HIP stream"), and reports its ``push`` / ``pull`` device
     spans (``comm_times``)."""
 
+    # DMP_LOCAL_PS_SIDE=0: the round-5 placement (apply and snapshot on the compute
+    # stream), kept for the same-box A/B (profiles/local_ps_side_stream_r6.txt)
+    SIDE = os.environ.get("DMP_LOCAL_PS_SIDE", "1") != "0"
+
     def init(self):
         self.master = self.arena.p32.detach().clone()
         self.ps_version = 0
         self.side = torch.cuda.Stream(self.device) if self.cuda else None
         self._pull_bufs: deque = deque()       # (snapshot buffer, land-done event)
+        if self.cuda and not self.SIDE:
+            self.side = torch.cuda.current_stream(self.device)
         if self.side is not None:
             warm_stream(self.side)     # bind its queue now, not mid-step
             # the master copy above was made on the compute stream
@@ -292,9 +298,12 @@ class LocalPSClient(PSClient):
             self.pending.append(_Pending(step, snap, version=self.ps_version))
             self.bytes_recv += snap.numel() * snap.element_size()
             return
-        buf, free_ev = self._pull_bufs.popleft() if len(self._pull_bufs) > self.staleness else \
-            (torch.empty(self.master.numel(), dtype=self.wire_dtype, device=self.device), None)
         with torch.cuda.stream(self.side):
+            # allocated ON the side stream: anything the allocator does to a new block
+            # (deterministic mode NaN-fills torch.empty) is ordered before the copy
+            buf, free_ev = self._pull_bufs.popleft() if len(self._pull_bufs) > self.staleness \
+                else (torch.empty(self.master.numel(), dtype=self.wire_dtype,
+                                  device=self.device), None)
             if free_ev is not None:
                 self.side.wait_event(free_ev)   # the land kernel that last read buf is done
             with self._timed("pull"):
@@ -664,8 +673,16 @@ class ShardedPSClient(PSClient):
     def request_pull(self, step: int):
         n = self.arena.numel
         wdt = torch.bfloat16 if self.bf16_wire else torch.float32
-        buf, free_ev = self._pull_bufs.popleft() if len(self._pull_bufs) > self.staleness else \
-            (torch.empty(n, dtype=wdt, device=self.device), None)
+        if self.cuda and (self.world > 1 or self.force):
+            with torch.cuda.stream(self.side):
+                # allocated on the side stream that fills it (see LocalPSClient)
+                buf, free_ev = self._pull_bufs.popleft() \
+                    if len(self._pull_bufs) > self.staleness else \
+                    (torch.empty(n, dtype=wdt, device=self.device), None)
+        else:
+            buf, free_ev = self._pull_bufs.popleft() \
+                if len(self._pull_bufs) > self.staleness else \
+                (torch.empty(n, dtype=wdt, device=self.device), None)
         self.bytes_recv += n * buf.element_size() * (self.world - 1) // max(self.world, 1)
         if self.world == 1 and not self.force:
             buf.copy_(self.master)
