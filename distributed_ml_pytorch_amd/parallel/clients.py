@@ -245,7 +245,8 @@ class PSClient:
 class LocalPSClient(PSClient):
     """In-process parameter server on the worker's device (single-GPU / tests).
 
-    The PS work runs on the side HIP stream, ordered by events exactly as the
+    With ``DMP_LOCAL_PS_SIDE=1`` the PS work runs on the side HIP stream, ordered by
+    events exactly as the
     N > 1 clients order theirs (:class:`ShardedPSClient` push / pull): the
     compute stream only hands the accumulator off (``push_handoff``); the
     master's apply and the pull snapshot run on ``side`` behind that event and
@@ -256,9 +257,11 @@ class LocalPSClient(PSClient):
     forward on a side HIP stream"), and reports its ``push`` / ``pull`` device
     spans (``comm_times``)."""
 
-    # DMP_LOCAL_PS_SIDE=0: the round-5 placement (apply and snapshot on the compute
-    # stream), kept for the same-box A/B (profiles/local_ps_side_stream_r6.txt)
-    SIDE = os.environ.get("DMP_LOCAL_PS_SIDE", "1") != "0"
+    # Measured slower on the 1-GPU bench (same box, alternating runs: 3.68-3.69 vs
+    # 3.615-3.617 ms per ResNet-18 step, profiles/local_ps_side_stream_r6.txt), so the
+    # default keeps the apply and the snapshot on the compute stream; DMP_LOCAL_PS_SIDE=1
+    # selects the side-stream placement described above (the N > 1 structure).
+    SIDE = os.environ.get("DMP_LOCAL_PS_SIDE", "0") == "1"
 
     def init(self):
         self.master = self.arena.p32.detach().clone()

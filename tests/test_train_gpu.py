@@ -359,3 +359,23 @@ def test_vit_native_gradients_match_fp32():
         if rel > 5e-2:
             bad[n] = rel
     assert not bad, bad
+
+
+def test_local_ps_side_stream_matches_compute_stream(monkeypatch):
+    """LocalPSClient with the PS apply / pull snapshot on the side stream (event-ordered,
+    DMP_LOCAL_PS_SIDE=1) trains bitwise like the compute-stream placement: in the
+    deterministic mode both runs must agree exactly (push / pull cadence 2 / 3 steps)."""
+    from distributed_ml_pytorch_amd.parallel.clients import LocalPSClient
+
+    runs = {}
+    try:
+        for side in (False, True):
+            monkeypatch.setattr(LocalPSClient, "SIDE", side)
+            runs[side] = _det_run("resnet18", steps=7)
+    finally:
+        torch.use_deterministic_algorithms(False)
+        torch.backends.cudnn.deterministic = False
+    (l0, p0, _), (l1, p1, _) = runs[False], runs[True]
+    assert all(v == v for v in l0), l0
+    assert l0 == l1, (l0, l1)
+    assert torch.equal(p0, p1)
