@@ -90,6 +90,23 @@ struct GemmArgs {
   int xcd_k;
 };
 
+// Diagnostic build only (-DDMP_GEMM_STAMPS, scripts/gemm_stamps.cpp): per-block
+// s_memrealtime stamps (100 MHz, one clock for every XCD) at kernel entry, after
+// the prologue's first k-tile landed, after the k-loop and after the epilogue.  No
+// stamp instruction exists in the extension build.
+#ifdef DMP_GEMM_STAMPS
+__device__ unsigned long long g_gemm_stamps[1 << 16][4];
+#define DMP_STAMP(i)                                                                  \
+  do {                                                                                \
+    if (threadIdx.x == 0) {                                                           \
+      const unsigned b = blockIdx.x + blockIdx.y * gridDim.x;                         \
+      if (b < (1u << 16)) g_gemm_stamps[b][i] = __builtin_amdgcn_s_memrealtime();     \
+    }                                                                                 \
+  } while (0)
+#else
+#define DMP_STAMP(i) do {} while (0)
+#endif
+
 __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
@@ -550,6 +567,7 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
     }
   };
 
+  DMP_STAMP(0);
   // bias (fwd) into the accumulators before any DMA is in flight
   tile_init(m0, n0);
   if constexpr (PP) {
@@ -561,6 +579,7 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
     for (int s = 0; s < 3; ++s) stage(s, s);        // k-tiles past KT load zeros
     gwait_vm<2 * PWK>();                            // k-tile 0 landed (this wave)
     __builtin_amdgcn_s_barrier();
+    DMP_STAMP(1);
     if (late) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     for (int kt = 0; kt < KT; ++kt) {
@@ -604,11 +623,13 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
     else gwait_vm<0>();
     // ... and for every wave; everyone is done reading slot (kt-1) % NS
     __builtin_amdgcn_s_barrier();
+    if (kt == 0) DMP_STAMP(1);
     asm volatile("" ::: "memory");
     if (kt + NS - 1 < KT) stage((kt + NS - 1) % NS, kt + NS - 1);
     compute(kt % NS);
   }
   }
+  DMP_STAMP(2);
   if constexpr (KG == 2) {
     // group 1 parks its partial sums in the drained ring, group 0 adds them
     gwait_vm<0>();
@@ -679,6 +700,7 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
     }
   }
   epilogue(m0, n0);
+  DMP_STAMP(3);
 }
 
 // ------------------------------------------------------- any-shape fallback
