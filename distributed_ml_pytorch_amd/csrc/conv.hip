@@ -32,6 +32,18 @@
 #include <cstdlib>
 
 #include "common.h"
+
+// cache policy (buffer aux bits) of the conv output stores: 0 default, 2 = nt
+// (streaming); compile-time A/B knobs (scripts/conv_ab.py build-defines).  Measured
+// per kernel family (profiles/conv_store_policy_r6.txt): the halo tiles' epilogues
+// (fwd / dgrad, row-staged or not) -2.7..-4.3 % with nt on the 16x16 / 8x8 layers;
+// the persistent 64-channel kernel +8 % slower with nt (dgrad): kept at the default
+#ifndef DMP_CONV_STORE_AUX
+#define DMP_CONV_STORE_AUX 0
+#endif
+#ifndef DMP_HALO_STORE_AUX
+#define DMP_HALO_STORE_AUX 2
+#endif
 #include "launchers.h"
 
 // Roofline ablations (scripts/conv_roofline.py builds a separate library with
@@ -487,7 +499,7 @@ __global__ void __launch_bounds__(64 * WM * WN) conv_igemm_kernel(ConvArgs a) {
         v[r] = bf2f(h[r]);   // statistics of the stored (rounded) values
       }
       const u32x2_t packed = {(u32)h[0] | ((u32)h[1] << 16), (u32)h[2] | ((u32)h[3] << 16)};
-      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, DMP_CONV_STORE_AUX);
       if (STATS) {
         const float keep = ok ? 1.f : 0.f;
 #pragma unroll
@@ -679,7 +691,7 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
         v[r] = bf2f(hv[r]);
       }
       const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
-      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, DMP_HALO_STORE_AUX);
       if (STATS) {
         const float keep = ok ? 1.f : 0.f;
 #pragma unroll
@@ -822,7 +834,7 @@ __device__ __forceinline__ void halo_epilogue_rows(const ConvArgs& a, f32x4 (&ac
         v.v[e] = f2bf(t);
       }
     }
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rsY, off[q], 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rsY, off[q], 0, DMP_HALO_STORE_AUX);
     if (STATS && off[q] != kOOB) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -1551,7 +1563,7 @@ __global__ void __launch_bounds__(64 * NW) conv_halo64p_kernel(ConvArgs a, HaloP
       }
     }
     const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
-    __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, DMP_CONV_STORE_AUX);
   };
   // addend rows of the tile being stored have landed (they were issued BEFORE
   // the next stage's DMA: wait until only those dma_pw pieces may be in flight)

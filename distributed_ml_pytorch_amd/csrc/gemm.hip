@@ -94,6 +94,13 @@ struct GemmArgs {
 // s_memrealtime stamps (100 MHz, one clock for every XCD) at kernel entry, after
 // the prologue's first k-tile landed, after the k-loop and after the epilogue.  No
 // stamp instruction exists in the extension build.
+// cache policy of the bf16 output stores (buffer instruction aux bits): 2 = nt
+// (streaming).  Measured with the stamped diagnostic build: -2 % on the QKV forward,
+// -5.5 % on a 4096^2 K = 1024 forward, -1..2 % at K = 3072; sc1 (16) is slower
+// (profiles/gemm_store_policy_r6.txt)
+#ifndef DMP_GEMM_STORE_AUX
+#define DMP_GEMM_STORE_AUX 2
+#endif
 #ifdef DMP_GEMM_STAMPS
 __device__ unsigned long long g_gemm_stamps[1 << 16][4];
 #define DMP_STAMP(i)                                                                  \
@@ -528,10 +535,10 @@ __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) gemm_kernel(GemmArgs g) 
         }
         if (!narrow) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, out), rsC, o[q], 0,
-                                                 0);
+                                                 DMP_GEMM_STORE_AUX);
           if constexpr (EPI == EPI_GELU)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, out2), rsC2, o[q],
-                                                   0, 0);
+                                                   0, DMP_GEMM_STORE_AUX);
         } else if (o[q] != kOOBg) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
