@@ -30,6 +30,33 @@ __device__ __forceinline__ void store8(u16* p, const float v[8]) {
   *reinterpret_cast<bf16x8*>(p) = r;
 }
 
+// Streaming loads / stores with an optional non-temporal hint (NT bit 1: loads,
+// bit 2: stores; DMP_BN_NT, measured per shape in profiles/bn_nt_policy_r6.txt)
+typedef unsigned bn_u32x4 __attribute__((ext_vector_type(4)));
+template <int NT>
+__device__ __forceinline__ bf16x8 bn_ldv(const u16* p) {
+  if constexpr ((NT & 1) != 0) {
+    return __builtin_bit_cast(bf16x8, __builtin_nontemporal_load(reinterpret_cast<const bn_u32x4*>(p)));
+  } else {
+    return *reinterpret_cast<const bf16x8*>(p);
+  }
+}
+template <int NT>
+__device__ __forceinline__ void bn_stv(u16* p, const bf16x8& r) {
+  if constexpr ((NT & 2) != 0) {
+    __builtin_nontemporal_store(__builtin_bit_cast(bn_u32x4, r), reinterpret_cast<bn_u32x4*>(p));
+  } else {
+    *reinterpret_cast<bf16x8*>(p) = r;
+  }
+}
+template <int NT>
+__device__ __forceinline__ void bn_st8(u16* p, const float v[8]) {
+  bf16x8 r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r.v[k] = f2bf(v[k]);
+  bn_stv<NT>(p, r);
+}
+
 // Pre-activation of the forward apply, shared by the forward and the backward's
 // ReLU-mask recomputation so both round identically (explicit fma).
 __device__ __forceinline__ float bn_pre(float x, float sc, float sh) { return __fmaf_rn(x, sc, sh); }
@@ -57,7 +84,7 @@ __device__ __forceinline__ void relu_mask_from_x(const float xv[8], const float*
 // -------- per-block channel partial sums --------------------------------
 // MODE 0: s += x, q += x*x                       (forward statistics)
 // MODE 1: s += dz, q += dz*(x-mean)*invstd        (backward reduction)
-template <int MODE, int RELU>
+template <int MODE, int RELU, int NT = 0>
 __global__ void __launch_bounds__(256) bn_partial_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
     const uint8_t* __restrict__ mask, const float* __restrict__ stats, float* __restrict__ part,
@@ -99,9 +126,9 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long long off = (row + u * rpi) * C + cg * 8;
-        xr[u] = *reinterpret_cast<const bf16x8*>(x + off);
-        if (MODE == 1) dr[u] = *reinterpret_cast<const bf16x8*>(dy + off);
-        if (MODE == 1 && RELU == 1) yr[u] = *reinterpret_cast<const bf16x8*>(y + off);
+        xr[u] = bn_ldv<NT>(x + off);
+        if (MODE == 1) dr[u] = bn_ldv<NT>(dy + off);
+        if (MODE == 1 && RELU == 1) yr[u] = bn_ldv<NT>(y + off);
         if (MODE == 1 && RELU == 3) mb[u] = mask[off >> 3];
       }
 #pragma unroll
@@ -506,7 +533,7 @@ __device__ __forceinline__ void fold_fwd_coefs(const float* __restrict__ part,
   __syncthreads();
 }
 
-template <int CS, bool RELU, bool RES, bool MASK>
+template <int CS, bool RELU, bool RES, bool MASK, int NT = 0>
 __global__ void __launch_bounds__(256) bn_apply_fold_kernel(
     const u16* __restrict__ x, const u16* __restrict__ res, const float* __restrict__ part,
     float* __restrict__ zero_buf, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -542,10 +569,10 @@ __global__ void __launch_bounds__(256) bn_apply_fold_kernel(
         r.v[k] = f2bf(o[k]);
         bits |= (r.v[k] != 0 ? 1u : 0u) << k;
       }
-      *reinterpret_cast<bf16x8*>(y + off) = r;
+      bn_stv<NT>(y + off, r);
       mask[off >> 3] = (uint8_t)bits;
     } else {
-      store8(y + off, o);
+      bn_st8<NT>(y + off, o);
     }
   };
   constexpr int U = 4;
@@ -556,8 +583,8 @@ __global__ void __launch_bounds__(256) bn_apply_fold_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long off = (row + u * RPI) * C + cofs;
-      xr[u] = *reinterpret_cast<const bf16x8*>(x + off);
-      if (RES) rr[u] = *reinterpret_cast<const bf16x8*>(res + off);
+      xr[u] = bn_ldv<NT>(x + off);
+      if (RES) rr[u] = bn_ldv<NT>(res + off);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) one(xr[u], rr[u], (row + u * RPI) * C + cofs);
@@ -602,7 +629,7 @@ __device__ __forceinline__ void fold_bwd_coefs(const float* __restrict__ part,
   __syncthreads();
 }
 
-template <int CS, int RELU, bool WRITE_DRES>
+template <int CS, int RELU, bool WRITE_DRES, int NT = 0>
 __global__ void __launch_bounds__(256) bn_bwd_apply_fold_kernel(
     const u16* __restrict__ x, const u16* __restrict__ dy, const u16* __restrict__ y,
     const uint8_t* __restrict__ mask, const float* __restrict__ part,
@@ -641,11 +668,11 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fold_kernel(
       }
     }
     if (RELU == 3) relu_mask_bits(mb, g);
-    if (WRITE_DRES) store8(dres + off, g);
+    if (WRITE_DRES) bn_st8<NT>(dres + off, g);
     float o[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = ka[k] * g[k] + kc[k] * xv[k] + kb[k];
-    store8(dx + off, o);
+    bn_st8<NT>(dx + off, o);
   };
   constexpr int U = 4;
   long long row = start + r0;
@@ -655,9 +682,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_fold_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long off = (row + u * RPI) * C + cofs;
-      xr[u] = *reinterpret_cast<const bf16x8*>(x + off);
-      dr[u] = *reinterpret_cast<const bf16x8*>(dy + off);
-      if (RELU == 1) yr[u] = *reinterpret_cast<const bf16x8*>(y + off);
+      xr[u] = bn_ldv<NT>(x + off);
+      dr[u] = bn_ldv<NT>(dy + off);
+      if (RELU == 1) yr[u] = bn_ldv<NT>(y + off);
       if (RELU == 3) mb[u] = mask[off >> 3];
     }
 #pragma unroll
@@ -910,6 +937,16 @@ static int onepass_blocks(long long M, int C) {
   return (int)std::max<long long>(1, g);
 }
 
+// cache policy of the streaming BN passes (CS = 64 slices): bit 1 non-temporal
+// loads, bit 2 non-temporal stores (DMP_BN_NT, default 0)
+static int bn_nt_policy() {
+  static const int v = [] {
+    const char* e = std::getenv("DMP_BN_NT");
+    return e ? (std::atoi(e) & 3) : 0;
+  }();
+  return v;
+}
+
 static int fold_cs(int C) { return C % 64 == 0 ? 64 : C % 32 == 0 ? 32 : C % 16 == 0 ? 16 : 8; }
 
 // row blocks per slice: >= 4 vectors per thread (DMP_BN_FOLD_VPT), at most 1024
@@ -947,25 +984,31 @@ void launch_bn_fwd_fold(const u16* x, const u16* res, u16* y, const float* gamma
   }
   const int cs = fold_cs(C);
   const dim3 grid = fold_grid(M, C, cs);
-#define DMP_FOLD_F(CS, R, S, K)                                                              \
-  hipLaunchKernelGGL((bn_apply_fold_kernel<CS, R, S, K>), grid, dim3(256), 0, s, x, res, part, \
-                     zero_buf, gamma, beta, running_mean, running_var, momentum, eps, stats, y, \
+#define DMP_FOLD_F(CS, R, S, K, NT)                                                              \
+  hipLaunchKernelGGL((bn_apply_fold_kernel<CS, R, S, K, NT>), grid, dim3(256), 0, s, x, res, part, \
+                     zero_buf, gamma, beta, running_mean, running_var, momentum, eps, stats, y,     \
                      mask, M, C)
-#define DMP_FOLD_FV(CS)                                       \
+#define DMP_FOLD_FV(CS, NT)                                   \
   if (relu && mask) {                                          \
-    if (res) DMP_FOLD_F(CS, true, true, true);                 \
-    else DMP_FOLD_F(CS, true, false, true);                    \
+    if (res) DMP_FOLD_F(CS, true, true, true, NT);             \
+    else DMP_FOLD_F(CS, true, false, true, NT);                \
   } else if (relu) {                                           \
-    if (res) DMP_FOLD_F(CS, true, true, false);                \
-    else DMP_FOLD_F(CS, true, false, false);                   \
+    if (res) DMP_FOLD_F(CS, true, true, false, NT);            \
+    else DMP_FOLD_F(CS, true, false, false, NT);               \
   } else {                                                     \
-    if (res) DMP_FOLD_F(CS, false, true, false);               \
-    else DMP_FOLD_F(CS, false, false, false);                  \
+    if (res) DMP_FOLD_F(CS, false, true, false, NT);           \
+    else DMP_FOLD_F(CS, false, false, false, NT);              \
   }
-  if (cs == 64) { DMP_FOLD_FV(64) }
-  else if (cs == 32) { DMP_FOLD_FV(32) }
-  else if (cs == 16) { DMP_FOLD_FV(16) }
-  else { DMP_FOLD_FV(8) }
+  const int nt = bn_nt_policy();
+  if (cs == 64) {
+    if (nt == 1) { DMP_FOLD_FV(64, 1) }
+    else if (nt == 2) { DMP_FOLD_FV(64, 2) }
+    else if (nt == 3) { DMP_FOLD_FV(64, 3) }
+    else { DMP_FOLD_FV(64, 0) }
+  }
+  else if (cs == 32) { DMP_FOLD_FV(32, 0) }
+  else if (cs == 16) { DMP_FOLD_FV(16, 0) }
+  else { DMP_FOLD_FV(8, 0) }
 #undef DMP_FOLD_FV
 #undef DMP_FOLD_F
 }
@@ -997,35 +1040,45 @@ void launch_bn_bwd_fold(const u16* x, const u16* dy, const u16* y, const float* 
 #undef DMP_BN_ONE
     return;
   }
-#define DMP_BN_PART(R)                                                                          \
-  hipLaunchKernelGGL((bn_partial_kernel<1, R>), dim3(G), dim3(256), lds, s, x, dy, y, mask, stats, \
+  const int nt = bn_nt_policy();
+#define DMP_BN_PART(R, NT)                                                                          \
+  hipLaunchKernelGGL((bn_partial_kernel<1, R, NT>), dim3(G), dim3(256), lds, s, x, dy, y, mask, stats, \
                      part, M, C)
-  if (mode == 0) DMP_BN_PART(0);
-  else if (mode == 1) DMP_BN_PART(1);
-  else if (mode == 2) DMP_BN_PART(2);
-  else DMP_BN_PART(3);
+#define DMP_BN_PARTV(R)                         \
+  if ((nt & 1) != 0) DMP_BN_PART(R, 1);         \
+  else DMP_BN_PART(R, 0);
+  if (mode == 0) { DMP_BN_PARTV(0) }
+  else if (mode == 1) { DMP_BN_PARTV(1) }
+  else if (mode == 2) { DMP_BN_PARTV(2) }
+  else { DMP_BN_PARTV(3) }
+#undef DMP_BN_PARTV
 #undef DMP_BN_PART
   const int cs = fold_cs(C);
   const dim3 grid = fold_grid(M, C, cs);
-#define DMP_FOLD_B(CS, R, D)                                                                   \
-  hipLaunchKernelGGL((bn_bwd_apply_fold_kernel<CS, R, D>), grid, dim3(256), 0, s, x, dy, y, mask, \
+#define DMP_FOLD_B(CS, R, D, NT)                                                                   \
+  hipLaunchKernelGGL((bn_bwd_apply_fold_kernel<CS, R, D, NT>), grid, dim3(256), 0, s, x, dy, y, mask, \
                      part, zero_buf, gamma, stats, dgamma, dbeta, dx, dres, M, C)
-#define DMP_FOLD_BV(CS)                                                    \
+#define DMP_FOLD_BV(CS, NT)                                                \
   if (dres) {                                                              \
-    if (mode == 0) DMP_FOLD_B(CS, 0, true);                                \
-    else if (mode == 1) DMP_FOLD_B(CS, 1, true);                           \
-    else if (mode == 2) DMP_FOLD_B(CS, 2, true);                           \
-    else DMP_FOLD_B(CS, 3, true);                                          \
+    if (mode == 0) DMP_FOLD_B(CS, 0, true, NT);                            \
+    else if (mode == 1) DMP_FOLD_B(CS, 1, true, NT);                       \
+    else if (mode == 2) DMP_FOLD_B(CS, 2, true, NT);                       \
+    else DMP_FOLD_B(CS, 3, true, NT);                                      \
   } else {                                                                 \
-    if (mode == 0) DMP_FOLD_B(CS, 0, false);                               \
-    else if (mode == 1) DMP_FOLD_B(CS, 1, false);                          \
-    else if (mode == 2) DMP_FOLD_B(CS, 2, false);                          \
-    else DMP_FOLD_B(CS, 3, false);                                         \
+    if (mode == 0) DMP_FOLD_B(CS, 0, false, NT);                           \
+    else if (mode == 1) DMP_FOLD_B(CS, 1, false, NT);                      \
+    else if (mode == 2) DMP_FOLD_B(CS, 2, false, NT);                      \
+    else DMP_FOLD_B(CS, 3, false, NT);                                     \
   }
-  if (cs == 64) { DMP_FOLD_BV(64) }
-  else if (cs == 32) { DMP_FOLD_BV(32) }
-  else if (cs == 16) { DMP_FOLD_BV(16) }
-  else { DMP_FOLD_BV(8) }
+  if (cs == 64) {
+    if (nt == 1) { DMP_FOLD_BV(64, 1) }
+    else if (nt == 2) { DMP_FOLD_BV(64, 2) }
+    else if (nt == 3) { DMP_FOLD_BV(64, 3) }
+    else { DMP_FOLD_BV(64, 0) }
+  }
+  else if (cs == 32) { DMP_FOLD_BV(32, 0) }
+  else if (cs == 16) { DMP_FOLD_BV(16, 0) }
+  else { DMP_FOLD_BV(8, 0) }
 #undef DMP_FOLD_BV
 #undef DMP_FOLD_B
 }

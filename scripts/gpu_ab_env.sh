@@ -14,4 +14,4 @@ while IFS= read -r line; do
   grep '^{' gpurun_out/ab_one.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["config"]["model"], d["value"], d["ms_per_step"], (d.get("gpu_clock_timed_window") or {}).get("sclk_mhz_mean"), d.get("comm_first_worker"))' >> $out
   [[ $rc == 0 ]] || { tail -20 gpurun_out/ab_one.log >> $out; exit $rc; }
 done < "$1"
-cat $out
+[[ "$(readlink -f /dev/stdout)" == "$(readlink -f $out)" ]] || cat $out
