@@ -691,7 +691,10 @@ __device__ __forceinline__ void halo_epilogue(const ConvArgs& a, f32x4 (&acc)[TM
         v[r] = bf2f(hv[r]);
       }
       const u32x2_t packed = {(u32)hv[0] | ((u32)hv[1] << 16), (u32)hv[2] | ((u32)hv[3] << 16)};
-      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0, DMP_HALO_STORE_AUX);
+      // (the stride-2 data gradient scatters every other pixel: default policy, its
+      // half-line writes merge in L2)
+      __builtin_amdgcn_raw_buffer_store_b64(packed, rsY, ok ? rowoff + 2u * n : kOOB, 0,
+                                            S2 ? 0 : DMP_HALO_STORE_AUX);
       if (STATS) {
         const float keep = ok ? 1.f : 0.f;
 #pragma unroll
