@@ -122,7 +122,7 @@ def _wgrad_candidates(K: int, CO: int | None = None):
                     continue
                 for bp32 in (0, 1):
                     for ns3 in (0, 1):
-                        for chunk in (2, 4, 8):          # x512 rows of P per block
+                        for chunk in (1, 2, 4, 8):       # x512 rows of P per block
                             cands.append(sel | (bp32 << 2) | (ns3 << 3) | (chunk << 4) | (bm << 8)
                                          | (xcd << 9))
     return cands
