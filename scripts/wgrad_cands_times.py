@@ -1,6 +1,6 @@
-"""Every weight-gradient candidate (gather cfgs incl. the deep-ring ones, halo cfgs) on the
-ResNet-18 wgrad shapes of one batch size, min of 3 x 10 calls each: the committed pick, the
-best overall and the best deep-ring (4096+) cfg per shape.
+"""Every weight-gradient candidate (gather cfgs, halo cfgs) on the wgrad shapes of one batch
+size in the committed tune cache, min of 3 x 10 calls each: the committed pick, the best
+overall and the best gather cfg with 512-row pixel chunks per shape.
     python scripts/wgrad_cands_times.py --batch 64"""
 import argparse
 import json
@@ -50,13 +50,13 @@ def main():
         res = {c: t_us(lambda: nat.conv_wgrad(dy, x, dw, st, pd, c)) for c in cands}
         pick = cache[json.dumps(k)]
         best = min(res.items(), key=lambda kv: kv[1])
-        deep = min(((c, u) for c, u in res.items() if (c >> 4) & 15 == 1 and c < 1000), key=lambda kv: kv[1],
+        c512 = min(((c, u) for c, u in res.items() if (c >> 4) & 15 == 1 and c < 1000), key=lambda kv: kv[1],
                    default=(None, float("nan")))
         pt = res.get(pick, float("nan"))
         tot_pick += pt if pt == pt else 0.0
         tot_best += best[1]
         print(f"{str(k[1:]):44s} pick {pick}:{pt:6.1f}  best {best[0]}:{best[1]:6.1f}  "
-              f"chunk512 {deep[0]}:{deep[1]:6.1f}", flush=True)
+              f"chunk512 {c512[0]}:{c512[1]:6.1f}", flush=True)
     print(f"sum over shapes (one call each): picks {tot_pick:.1f} us, best {tot_best:.1f} us")
 
 
