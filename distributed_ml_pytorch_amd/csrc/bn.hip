@@ -954,7 +954,10 @@ static int fold_cs(int C) { return C % 64 == 0 ? 64 : C % 32 == 0 ? 32 : C % 16 
 // floats from L2; the streaming pass needs the blocks: ResNet-18 bs512 3.77
 // ms/step unfolded, 4.15 at 32 vectors per thread, 3.66 at 8, 3.65 at 4
 // (profiles/bn_fold_stem3_r2.txt).  Cap 1024 vs 2048: ResNet-50 bs128 -0.14
-// ms/step, ResNet-18 unchanged; 512 and 4096 slower (profiles/bn_grid_knobs_r4.txt)
+// ms/step, ResNet-18 unchanged; 512 and 4096 slower (profiles/bn_grid_knobs_r4.txt).
+// Small tensors (the reference batch): a grid of fewer than DMP_BN_FOLD_SMALL blocks
+// at 4 vectors per thread goes to 1 vector per thread instead -- more blocks for a
+// latency-bound pass (profiles/bn_grid_knobs_r6.txt)
 static dim3 fold_grid(long long M, int C, int cs, long long cap_blocks = 0) {
   static const long long vpt = [] {
     const char* e = std::getenv("DMP_BN_FOLD_VPT");
@@ -964,8 +967,14 @@ static dim3 fold_grid(long long M, int C, int cs, long long cap_blocks = 0) {
     const char* e = std::getenv("DMP_BN_FOLD_CAP");
     return e ? std::max(1, std::atoi(e)) : 1024;
   }();
+  static const long long small = [] {
+    const char* e = std::getenv("DMP_BN_FOLD_SMALL");
+    return e ? std::max(0, std::atoi(e)) : 512;
+  }();
   const long long nsl = C / cs;
-  long long nrb = (M * (cs / 8) + 256 * vpt - 1) / (256 * vpt);
+  const long long vecs = M * (cs / 8);   // per slice
+  long long nrb = (vecs + 256 * vpt - 1) / (256 * vpt);
+  if (nrb * nsl < small) nrb = (vecs + 255) / 256;
   const long long cap = std::max<long long>(1, (cap_blocks > 0 ? cap_blocks : total) / nsl);
   nrb = std::max<long long>(1, std::min(nrb, std::min(cap, M)));
   return dim3((unsigned)nrb, (unsigned)nsl);
