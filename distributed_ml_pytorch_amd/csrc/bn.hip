@@ -1022,11 +1022,24 @@ void launch_bn_fwd_fold(const u16* x, const u16* res, u16* y, const float* gamma
 #undef DMP_FOLD_F
 }
 
+// backward reduce grid: bn_num_partials, or for a small tensor (fewer than
+// DMP_BN_PART_SMALL blocks at 8 vectors per thread) 2 vectors per thread
+static int bn_bwd_partials(long long M, int C) {
+  static const int small = [] {
+    const char* e = std::getenv("DMP_BN_PART_SMALL");
+    return e ? std::max(0, std::atoi(e)) : 256;
+  }();
+  const int G = bn_num_partials(M, C);
+  if (G >= small) return G;
+  const long long g = M * (C / 8) / (256 * 2);
+  return (int)std::max<long long>(G, std::min<long long>(g, std::min<long long>(2048, M)));
+}
+
 void launch_bn_bwd_fold(const u16* x, const u16* dy, const u16* y, const float* gamma,
                         const float* stats, float* dgamma, float* dbeta, float* part,
                         float* zero_buf, u16* dx, u16* dres, long long M, int C, bool relu,
                         hipStream_t s, const uint8_t* mask, float* coef) {
-  const int G = bn_num_partials(M, C);
+  const int G = bn_bwd_partials(M, C);
   const int rpi = 256 / (C / 8);
   const size_t lds = (size_t)rpi * C * 2 * sizeof(float);
   const int mode = !relu ? 0 : (mask ? 3 : (y ? 1 : 2));
