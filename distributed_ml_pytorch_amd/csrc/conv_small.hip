@@ -729,7 +729,10 @@ void launch_stem3_wgrad(const u16* dy, const u16* x, int xbytes, int sb, int sh,
   }();
   const long long steps = (a.P + 127) / 128;
   long long per = (steps + target - 1) / target;
-  if (per < 1) per = 1;
+  // >= 4 steps per block: at the reference batch (512 steps) 128 blocks beat 512 --
+  // a quarter of the per-block atomic flushes (ResNet-18 bs64 -0.75 %,
+  // profiles/stem3_wgrad_grid_r6.txt); batches >= 256 already run >= 4 per block
+  if (per < 4) per = 4;
   a.groups = (int)per;
   const long long nb = (steps + per - 1) / per;
   hipLaunchKernelGGL(stem3_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a);
