@@ -25,7 +25,10 @@ import threading
 import torch
 
 _LOG = logging.getLogger(__name__)
-_state = threading.local()
+# overrides of stock_allowed() blocks, innermost last.  Process-wide, not
+# thread-local: the autograd engine runs a CUDA backward on its own device
+# thread, and a block's setting must hold for the backward it launches too.
+_overrides: list = []
 _global_allow = False
 _seen: set = set()
 _lock = threading.Lock()
@@ -46,19 +49,20 @@ def allow_stock(on: bool = True, reason: str = "stock oracle mode"):
 
 @contextlib.contextmanager
 def stock_allowed(on: bool = True):
-    """Thread-local override for a block (tests: fp32 oracles on the GPU; the
-    strict all-native test sets ``on=False``)."""
-    prev = getattr(_state, "allow", None)
-    _state.allow = bool(on)
+    """Override for a block, including the backward passes it runs (tests: fp32
+    oracles on the GPU; the strict all-native test sets ``on=False``)."""
+    with _lock:
+        _overrides.append(bool(on))
     try:
         yield
     finally:
-        _state.allow = prev
+        with _lock:
+            _overrides.pop()
 
 
 def is_allowed() -> bool:
-    local = getattr(_state, "allow", None)
-    return _global_allow if local is None else local
+    with _lock:
+        return _overrides[-1] if _overrides else _global_allow
 
 
 def stock_log() -> list:

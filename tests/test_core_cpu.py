@@ -359,3 +359,23 @@ def test_deferred_residual_mask_helpers():
     t.add_(1.0)
     with pytest.raises(RuntimeError):
         Fn.deferred_mask(t)
+
+
+def test_stock_policy_override_nests_and_reaches_other_threads():
+    """ops._policy.stock_allowed holds for every thread while the block runs (a CUDA
+    backward executes on the autograd engine's device thread), and nests."""
+    import threading
+
+    from distributed_ml_pytorch_amd.ops._policy import is_allowed, stock_allowed
+
+    assert not is_allowed()
+    with stock_allowed(True):
+        seen = []
+        t = threading.Thread(target=lambda: seen.append(is_allowed()))
+        t.start()
+        t.join()
+        assert seen == [True]
+        with stock_allowed(False):
+            assert not is_allowed()
+        assert is_allowed()
+    assert not is_allowed()
