@@ -363,19 +363,21 @@ def test_deferred_residual_mask_helpers():
 
 def test_stock_policy_override_nests_and_reaches_other_threads():
     """ops._policy.stock_allowed holds for every thread while the block runs (a CUDA
-    backward executes on the autograd engine's device thread), and nests."""
+    backward executes on the autograd engine's device thread), and nests.  (The
+    conftest fixture already runs this test inside an allowing block.)"""
     import threading
 
     from distributed_ml_pytorch_amd.ops._policy import is_allowed, stock_allowed
 
-    assert not is_allowed()
-    with stock_allowed(True):
-        seen = []
-        t = threading.Thread(target=lambda: seen.append(is_allowed()))
-        t.start()
-        t.join()
-        assert seen == [True]
-        with stock_allowed(False):
-            assert not is_allowed()
-        assert is_allowed()
-    assert not is_allowed()
+    outer = is_allowed()
+    for on in (False, True):
+        with stock_allowed(on):
+            seen = []
+            t = threading.Thread(target=lambda: seen.append(is_allowed()))
+            t.start()
+            t.join()
+            assert seen == [on] and is_allowed() == on
+            with stock_allowed(not on):
+                assert is_allowed() == (not on)
+            assert is_allowed() == on
+    assert is_allowed() == outer
