@@ -248,7 +248,7 @@ def _timed_steps(w, pool, steps, warmup, ctx, clock=None):
     t0 = time.perf_counter()
     for _ in range(steps):
         x, y = pool.next()
-        loss, _ = w.train_step(x, y, keep=not trace)   # only the last loss is read
+        loss, _ = w.train_step(x, y, keep=trace)   # untraced: only the last loss is read
         if trace:
             seen.append(loss)
     _sync()
