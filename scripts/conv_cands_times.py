@@ -1,0 +1,88 @@
+"""Every forward / data-gradient candidate the tuner offers (ops/conv.py _fwd_cfg / _dgrad_cfg) on the
+conv shapes of one batch size in the committed tune cache, min of 3 x 10 calls each: the committed pick
+and the best candidate per key, and a candidate cache (committed picks, with every key whose best is
+more than --margin faster replaced) for an in-step A/B.
+    python scripts/conv_cands_times.py --batch 64 --out gpurun_out/cand_fwd_dgrad.json"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch
+
+from distributed_ml_pytorch_amd.ops import conv as C
+from distributed_ml_pytorch_amd.ops._ext import native
+
+CL = torch.channels_last
+
+
+def t_us(fn, it=10, rounds=3):
+    fn()
+    best = float("inf")
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(it):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e3 / it)
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--margin", type=float, default=0.05)
+    ap.add_argument("--out", default="gpurun_out/cand_fwd_dgrad.json")
+    a = ap.parse_args()
+    nat = native()
+    here = os.path.dirname(os.path.abspath(__file__))
+    path = os.path.join(here, "..", "tuning", "mi355x_tune_cache.json")
+    cache = json.load(open(path))
+    cand = dict(cache)
+    for ks, pick in cache.items():
+        k = json.loads(ks)
+        if k[0] not in ("fwd", "dgrad") or k[1] != a.batch:
+            continue
+        if k[0] == "fwd":
+            _, B, CI, H, W, CO, R, S, st, pd = k
+            OH, OW = (H + 2 * pd - R) // st + 1, (W + 2 * pd - S) // st + 1
+        else:
+            _, B, CO, OH, OW, CI, H, W, R, S, st, pd = k
+        if CI % 8 or CO % 64:
+            continue                      # the small-CI stems have their own kernels
+        x = torch.randn(B, CI, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+        w = (torch.randn(CO, CI, R, S, device="cuda") / (R * S * CI) ** 0.5).to(torch.bfloat16).contiguous(
+            memory_format=CL)
+        dy = torch.randn(B, CO, OH, OW, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+        if k[0] == "fwd":
+            cands = C._igemm_candidates(CO) + C._halo_candidates(H, W, CI, R, S, st, pd)
+            run = lambda c: nat.conv_fwd(x, w, st, pd, True, c)   # noqa: E731
+        else:
+            cands = C._igemm_candidates(CI, fwd=st == 1)
+            if (H, W) == (OH, OW):
+                cands += C._halo_candidates(H, W, CO, R, S, st, pd)
+            elif st == 2:
+                cands += list(nat.conv_dgrad_s2_configs(H, W, OH, OW, CO, CI, R, S, st, pd))
+            run = lambda c: nat.conv_dgrad(dy, w, H, W, st, pd, c)   # noqa: E731
+        res = {}
+        for c in cands:
+            try:
+                res[c] = t_us(lambda: run(c))
+            except RuntimeError:
+                pass
+        best = min(res.items(), key=lambda kv: kv[1])
+        pt = res.get(pick, float("nan"))
+        flag = ""
+        if pt == pt and best[1] < (1 - a.margin) * pt:
+            cand[ks] = best[0]
+            flag = "  <- candidate"
+        print(f"{str(k):58s} pick {pick}:{pt:6.1f}  best {best[0]}:{best[1]:6.1f}{flag}", flush=True)
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    json.dump(cand, open(a.out, "w"), indent=0, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
