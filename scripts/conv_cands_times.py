@@ -1,4 +1,5 @@
-"""Every forward / data-gradient candidate the tuner offers (ops/conv.py _fwd_cfg / _dgrad_cfg) on the
+"""Every forward / data-gradient (/ weight-gradient with --kinds) candidate the tuner offers
+(ops/conv.py _fwd_cfg / _dgrad_cfg / _wgrad_cfg) on the
 conv shapes of one batch size in the committed tune cache, min of 3 x 10 calls each: the committed pick
 and the best candidate per key, and a candidate cache (committed picks, with every key whose best is
 more than --margin faster replaced) for an in-step A/B.
@@ -36,6 +37,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--margin", type=float, default=0.05)
     ap.add_argument("--out", default="gpurun_out/cand_fwd_dgrad.json")
+    ap.add_argument("--kinds", default="fwd,dgrad", help="comma list of fwd / dgrad / wgrad")
     a = ap.parse_args()
     nat = native()
     here = os.path.dirname(os.path.abspath(__file__))
@@ -44,9 +46,12 @@ def main():
     cand = dict(cache)
     for ks, pick in cache.items():
         k = json.loads(ks)
-        if k[0] not in ("fwd", "dgrad") or k[1] != a.batch:
+        if k[0] not in a.kinds.split(",") or k[1] != a.batch:
             continue
-        if k[0] == "fwd":
+        if k[0] == "wgrad":
+            _, B, CI, H, W, CO, _ci, R, S, st, pd = k
+            OH, OW = (H + 2 * pd - R) // st + 1, (W + 2 * pd - S) // st + 1
+        elif k[0] == "fwd":
             _, B, CI, H, W, CO, R, S, st, pd = k
             OH, OW = (H + 2 * pd - R) // st + 1, (W + 2 * pd - S) // st + 1
         else:
@@ -57,7 +62,12 @@ def main():
         w = (torch.randn(CO, CI, R, S, device="cuda") / (R * S * CI) ** 0.5).to(torch.bfloat16).contiguous(
             memory_format=CL)
         dy = torch.randn(B, CO, OH, OW, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
-        if k[0] == "fwd":
+        if k[0] == "wgrad":
+            dw = torch.zeros(CO, CI, R, S, device="cuda").contiguous(memory_format=CL)
+            cands = C._wgrad_candidates(R * S * CI, CO) + list(
+                nat.conv_wgrad_halo_configs(B, H, W, CI, CO, R, S, st, pd))
+            run = lambda c: nat.conv_wgrad(dy, x, dw, st, pd, c)   # noqa: E731
+        elif k[0] == "fwd":
             cands = C._igemm_candidates(CO) + C._halo_candidates(H, W, CI, R, S, st, pd)
             run = lambda c: nat.conv_fwd(x, w, st, pd, True, c)   # noqa: E731
         else:
