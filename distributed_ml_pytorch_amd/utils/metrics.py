@@ -178,7 +178,10 @@ class ClockSampler:
             pass
         return hs[0] if len(hs) == 1 else hs[min(self.device_index, len(hs) - 1)]
 
-    def _read(self):
+    def _read(self, extra: bool = False):
+        """(sclk, socket power[, mclk, fabric clock, hotspot temperature]) -- the extra
+        three only when ``extra`` (every 4th sample: they explain box-to-box spread
+        that sclk alone does not, e.g. a lower memory clock)."""
         smi = self._smi
         clk = smi.amdsmi_get_clock_info(self._h, smi.AmdSmiClkType.SYS)["clk"]
         pw = None
@@ -190,7 +193,23 @@ class ClockSampler:
             pw = float(pw) if isinstance(pw, (int, float)) and pw > 0 else None
         except Exception:
             pass
-        return float(clk), pw
+        mclk = fclk = temp = None
+        if extra:
+            for kind, attr in ((smi.AmdSmiClkType.MEM, "m"), (smi.AmdSmiClkType.DF, "f")):
+                try:
+                    v = float(smi.amdsmi_get_clock_info(self._h, kind)["clk"])
+                    if attr == "m":
+                        mclk = v
+                    else:
+                        fclk = v
+                except Exception:
+                    pass
+            try:
+                temp = float(smi.amdsmi_get_temp_metric(self._h, smi.AmdSmiTemperatureType.HOTSPOT,
+                                                        smi.AmdSmiTemperatureMetric.CURRENT))
+            except Exception:
+                pass
+        return float(clk), pw, mclk, fclk, temp
 
     def start(self):
         if self._h is None:
@@ -201,11 +220,13 @@ class ClockSampler:
         self._stop = threading.Event()
 
         def loop():
+            k = 0
             while not self._stop.is_set():
                 try:
-                    self.samples.append(self._read())
+                    self.samples.append(self._read(extra=k % 4 == 0))
                 except Exception:
                     return
+                k += 1
                 self._stop.wait(self.period)
 
         self._thr = threading.Thread(target=loop, daemon=True)
@@ -218,8 +239,8 @@ class ClockSampler:
         self._stop.set()
         self._thr.join(timeout=1.0)
         self._thr = None
-        clks = [c for c, _ in self.samples if c and c > 0]
-        pws = [p for _, p in self.samples if p]
+        clks = [x[0] for x in self.samples if x[0] and x[0] > 0]
+        pws = [x[1] for x in self.samples if x[1]]
         if not clks:
             return None
         out = {"samples": len(clks), "sclk_mhz_mean": round(sum(clks) / len(clks), 1),
@@ -227,6 +248,10 @@ class ClockSampler:
         if pws:
             out["power_w_mean"] = round(sum(pws) / len(pws), 1)
             out["power_w_max"] = max(pws)
+        for i, name in ((2, "mclk_mhz_mean"), (3, "fclk_mhz_mean"), (4, "hotspot_c_mean")):
+            v = [x[i] for x in self.samples if len(x) > i and x[i] is not None]
+            if v:
+                out[name] = round(sum(v) / len(v), 1)
         return out
 
 
