@@ -33,6 +33,16 @@ __global__ void __launch_bounds__(256) im2col_kernel(const u16* __restrict__ x,
     int ci = k0 % CI;
     int rs = k0 / CI;
     int s = rs % S, r = rs / S;
+    if ((CI & 7) == 0) {
+      // every 8-chunk is 8 consecutive channels of ONE tap: a 16-B load (the
+      // 64+-channel ResNet convs on the im2col weight-gradient route)
+      const int ih = oh * stride - pad + r, iw = ow * stride - pad + s;
+      bf16x8 v{};
+      if (k0 < K && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+        v = *reinterpret_cast<const bf16x8*>(x + ((b * H + ih) * W + iw) * CI + ci);
+      *reinterpret_cast<bf16x8*>(cols + q * 8) = v;
+      continue;
+    }
     bf16x8 out;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {

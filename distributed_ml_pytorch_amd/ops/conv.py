@@ -196,6 +196,48 @@ def _gemm1x1_wgrad(dy, x, g):
     gemm(2, 3, _rows_nhwc(dy), _rows_nhwc(x), g.reshape(g.shape[0], g.shape[1]))
 
 
+# ------------------------------------ weight gradient as patch matrix x GEMM
+# dW[co][(r, s, ci)] += sum_p dY[p][co] cols[p][(r, s, ci)]: the native patch
+# matrix (csrc/im2col.hip, 16-B taps when CI % 8 == 0) into the wgrad GEMM
+# (mode 2, split-K over the pixels, fp32 into the arena view -- the
+# channels_last [CO][R][S][CI] gradient IS the [CO][K] GEMM output).  A tuner
+# candidate for the small-map layers (ResNet-18 layer3 / layer4 at the
+# reference batch 64: 1024-4096 pixels, 256-512 channels), bounded by the patch
+# matrix size.  Opt-in (DMP_CONV_IM2COL_WGRAD=1): graph-replayed per-candidate
+# timing put it at 2.2-6x the gather / halo picks on every ResNet-18 bs64 3x3
+# key (45-61 vs 7-22 us: the patch-matrix write plus a short-K GEMM launch,
+# profiles/im2col_wgrad_route_r6.txt), so the tuner is not offered it by default.
+_IM2COL_ROUTE = 30001
+_IM2COL_WGRAD = os.environ.get("DMP_CONV_IM2COL_WGRAD", "0") == "1"
+_IM2COL_WGRAD_MAX_BYTES = 64 << 20
+
+
+def _im2col_wgrad_ok(x, shape, stride, pad) -> bool:
+    CO, CI, R, S = shape
+    if not _IM2COL_WGRAD or (R, S) == (1, 1) or CI % 8 or CO % 8:
+        return False
+    B, _, H, W = x.shape
+    OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+    return 2 * B * OH * OW * R * S * CI <= _IM2COL_WGRAD_MAX_BYTES
+
+
+def _im2col_wgrad(dy, x, g, stride, pad):
+    """g: fp32 [CO, CI, R, S] channels_last, accumulated in place."""
+    from .linear import gemm
+
+    CO, CI, R, S = g.shape
+    K = R * S * CI
+    cols = native().im2col(x.contiguous(memory_format=torch.channels_last), R, S, stride, pad, K)
+    gemm(2, 3, _rows_nhwc(dy), cols, g.permute(0, 2, 3, 1).reshape(CO, K))
+
+
+def _gemm_route_wgrad(route, dy, x, g, stride, pad):
+    if route == _IM2COL_ROUTE:
+        _im2col_wgrad(dy, x, g, stride, pad)
+    else:
+        _gemm1x1_wgrad(dy, x, g)
+
+
 def _fwd_cfg(x, w16, stride, pad):
     key = ("fwd", *x.shape, w16.shape[0], w16.shape[2], w16.shape[3], stride, pad)
     cands = _igemm_candidates(w16.shape[0]) + _halo_candidates(
@@ -249,10 +291,12 @@ def _wgrad_cfg(dy, x, shape, stride, pad):
                                                        stride, pad))
     if _gemm1x1_ok(shape, stride, pad, shape[1], shape[0]):
         cands.append(_GEMM_ROUTE)
+    elif _im2col_wgrad_ok(x, shape, stride, pad):
+        cands.append(_IM2COL_ROUTE)
 
     def run(c):
-        if c == _GEMM_ROUTE:
-            _gemm1x1_wgrad(dy, x, scratch)
+        if c in (_GEMM_ROUTE, _IM2COL_ROUTE):
+            _gemm_route_wgrad(c, dy, x, scratch, stride, pad)
         else:
             native().conv_wgrad(dy, x, scratch, stride, pad, c)
     return TUNER.best(key, run, cands)
@@ -390,26 +434,27 @@ class _NativeConv(Function):
             wcfg = _wgrad_cfg(dy, x, tuple(master.shape), stride, pad)
             g = master.grad if getattr(master, "_dmp_arena", False) else None
             bias_in_wgrad = (bias is not None and bias.requires_grad and wcfg < _WH_BASE
-                             and wcfg != _GEMM_ROUTE and getattr(bias, "_dmp_arena", False)
+                             and getattr(bias, "_dmp_arena", False)
                              and bias.grad is not None and bias.grad.is_contiguous()
                              and bias.grad.dtype == torch.float32
                              and g is not None and g.is_contiguous(
                                  memory_format=torch.channels_last)
                              and getattr(master, "_dmp_grad_ready", None) is None)
-            if wcfg == _GEMM_ROUTE:
+            if wcfg in (_GEMM_ROUTE, _IM2COL_ROUTE):
                 gg = g if g is not None and g.is_contiguous(
                     memory_format=torch.channels_last) else None
                 if gg is None:
                     gw = torch.zeros(tuple(master.shape), dtype=torch.float32, device=x.device)
                     gw = gw.contiguous(memory_format=torch.channels_last)
-                    _gemm1x1_wgrad(dy, x, gw)
+                    _gemm_route_wgrad(wcfg, dy, x, gw, stride, pad)
                     gw = gw.to(master.dtype)
                 else:
                     cb = getattr(master, "_dmp_grad_ready", None)
                     if cb is None and _WG_STREAM_ENABLED:
-                        _side_wgrad(x.device, lambda: _gemm1x1_wgrad(dy, x, gg), dy, x)
+                        _side_wgrad(x.device,
+                                    lambda: _gemm_route_wgrad(wcfg, dy, x, gg, stride, pad), dy, x)
                     else:
-                        _gemm1x1_wgrad(dy, x, gg)
+                        _gemm_route_wgrad(wcfg, dy, x, gg, stride, pad)
                         if cb is not None:
                             cb(master)
             elif bias_in_wgrad:

@@ -19,16 +19,25 @@ CL = torch.channels_last
 
 
 def t_us(fn, it=10, rounds=3):
-    fn()
+    """Per-call device time of ``fn`` replayed from a captured graph (as in the training
+    step: a Python-side route's host cost does not count), min over ``rounds``."""
+    fn()                                   # first call: any inner GEMM pick is tuned here
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(it):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     best = float("inf")
     for _ in range(rounds):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(it):
-            fn()
+        g.replay()
         e1.record()
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1) * 1e3 / it)
+    del g
     return best
 
 
@@ -44,6 +53,9 @@ def main():
     path = os.path.join(here, "..", "tuning", "mi355x_tune_cache.json")
     cache = json.load(open(path))
     cand = dict(cache)
+    # the GEMM routes' inner GEMMs: committed picks, new keys tuned on first use
+    from distributed_ml_pytorch_amd.ops.tuner import TUNER
+    TUNER.cache.update({tuple(json.loads(ks)): v for ks, v in cache.items()})
     for ks, pick in cache.items():
         k = json.loads(ks)
         if k[0] not in a.kinds.split(",") or k[1] != a.batch:
@@ -66,7 +78,13 @@ def main():
             dw = torch.zeros(CO, CI, R, S, device="cuda").contiguous(memory_format=CL)
             cands = C._wgrad_candidates(R * S * CI, CO) + list(
                 nat.conv_wgrad_halo_configs(B, H, W, CI, CO, R, S, st, pd))
-            run = lambda c: nat.conv_wgrad(dy, x, dw, st, pd, c)   # noqa: E731
+            if C._gemm1x1_ok((CO, CI, R, S), st, pd, CI, CO):
+                cands.append(C._GEMM_ROUTE)
+            elif C._im2col_wgrad_ok(x, (CO, CI, R, S), st, pd):
+                cands.append(C._IM2COL_ROUTE)
+            run = lambda c: (C._gemm_route_wgrad(c, dy, x, dw, st, pd)   # noqa: E731
+                             if c in (C._GEMM_ROUTE, C._IM2COL_ROUTE)
+                             else nat.conv_wgrad(dy, x, dw, st, pd, c))
         elif k[0] == "fwd":
             cands = C._igemm_candidates(CO) + C._halo_candidates(H, W, CI, R, S, st, pd)
             run = lambda c: nat.conv_fwd(x, w, st, pd, True, c)   # noqa: E731
@@ -81,15 +99,23 @@ def main():
         for c in cands:
             try:
                 res[c] = t_us(lambda: run(c))
-            except RuntimeError:
-                pass
+            except RuntimeError as e:
+                if c >= C._GEMM_ROUTE:
+                    print(f"  route {c} failed: {e}", flush=True)
         best = min(res.items(), key=lambda kv: kv[1])
         pt = res.get(pick, float("nan"))
         flag = ""
         if pt == pt and best[1] < (1 - a.margin) * pt:
             cand[ks] = best[0]
             flag = "  <- candidate"
-        print(f"{str(k):58s} pick {pick}:{pt:6.1f}  best {best[0]}:{best[1]:6.1f}{flag}", flush=True)
+        route = next((f"  route {c}:{res.get(c, float('nan')):6.1f}" for c in
+                      (C._GEMM_ROUTE, C._IM2COL_ROUTE) if c in cands), "")
+        print(f"{str(k):58s} pick {pick}:{pt:6.1f}  best {best[0]}:{best[1]:6.1f}{route}{flag}",
+              flush=True)
+    for kt, v in TUNER.cache.items():          # GEMM keys first tuned here
+        ks = json.dumps(list(kt))
+        if ks not in cand and kt[0] == "gemm":
+            cand[ks] = v
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(cand, open(a.out, "w"), indent=0, sort_keys=True)
 

@@ -584,6 +584,38 @@ def test_conv1x1_gemm_route(monkeypatch):
     assert _rel(conv.weight.grad, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("B,CI,H,CO,st", [(8, 256, 8, 256, 1), (4, 128, 16, 256, 2),
+                                          (6, 64, 5, 128, 1)])
+def test_conv_im2col_wgrad_route(monkeypatch, B, CI, H, CO, st):
+    """3x3 weight gradient as patch matrix x wgrad GEMM (ops/conv.py _IM2COL_ROUTE):
+    the helper accumulating into a channels_last fp32 gradient, and a whole layer
+    with the route forced, vs fp32."""
+    from distributed_ml_pytorch_amd.ops import conv as C
+    from distributed_ml_pytorch_amd.ops import layers as L
+
+    monkeypatch.setattr(C, "_IM2COL_WGRAD", True)     # opt-in route
+    torch.manual_seed(3)
+    x = torch.randn(B, CI, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(CO, CI, 3, 3, device="cuda") / (9 * CI) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=CL)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(x.float(), wr, None, st, 1)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=CL)
+    yr.backward(dy.float())
+    assert C._im2col_wgrad_ok(x, tuple(w.shape), st, 1)
+    g = torch.zeros(CO, CI, 3, 3, device="cuda").contiguous(memory_format=CL)
+    C._im2col_wgrad(dy, x, g, st, 1)
+    assert _rel(g, wr.grad) < 1e-2
+    C._im2col_wgrad(dy, x, g, st, 1)                 # accumulates
+    assert _rel(g, 2 * wr.grad) < 1e-2
+    monkeypatch.setattr(C, "_wgrad_cfg", lambda *a: C._IM2COL_ROUTE)
+    conv = L.Conv2d(CI, CO, 3, stride=st, padding=1, bias=False).cuda()
+    with torch.no_grad():
+        conv.weight.copy_(w.float())
+    conv(x.detach().clone().requires_grad_(True)).backward(dy)
+    assert _rel(conv.weight.grad, wr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("B,H", [(2, 224), (3, 48), (1, 8)])
 def test_stem_conv_fwd_stats_wgrad(B, H):
     """ImageNet 7x7/2/3 stem (space-to-depth MFMA kernels) vs fp32 PyTorch."""

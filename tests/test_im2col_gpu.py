@@ -18,6 +18,8 @@ def _rel(a, b):
     (16, 6, 14, 16, 5, 1, 0, True, True, True),      # LeNet conv2 (input grad: col2im)
     (4, 3, 64, 64, 7, 2, 3, False, False, False),    # ResNet-50 stem geometry
     (8, 5, 9, 24, 3, 2, 1, True, False, True),       # odd everything
+    (8, 16, 12, 24, 3, 1, 1, True, False, True),     # CI % 8 == 0: 16-B tap loads
+    (4, 32, 11, 40, 3, 2, 1, False, True, True),     # 16-B taps, stride 2, odd map
 ])
 def test_im2col_conv_matches_fp32(B, CI, H, CO, k, st, pd, bias, relu, xgrad):
     from distributed_ml_pytorch_amd.ops import layers as L
