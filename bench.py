@@ -112,6 +112,11 @@ def parse(argv=None):
                          "--ttl-eval-every steps as the reference evaluates on its test set "
                          "(/root/reference/example/main.py:83-89,110-131); 0 skips")
     ap.add_argument("--ttl-eval-every", type=int, default=50)
+    ap.add_argument("--ttl-plateau-steps", type=int, default=500,
+                    help="once the training-loss target is reached, stop waiting for the held-out "
+                         "accuracy target after this many steps without a new best held-out "
+                         "accuracy (N > 1 on the shared 128-batch set plateaus below 0.7: "
+                         "0.65 at N = 2 from step ~1600 to 4000); 0 = wait up to --ttl-max-steps")
     ap.add_argument("--ttl-heldout-acc", type=float, default=0.7,
                     help="held-out accuracy target: ttl_heldout_steps = first evaluation at or above it")
     ap.add_argument("--central-check", type=int, default=-1,
@@ -298,6 +303,7 @@ def time_to_target(a, cfg, ctx, mode=None):
     steps, reached, window = 0, False, []
     t_train, train_steps = None, 0
     h_reached, h_steps, h_time, h_last = held is None, None, None, (None, None)
+    h_best, h_best_step, plateau = -1.0, 0, False
     eval_s = 0.0
     while steps < a.ttl_max_steps:
         x, y = pool.next()
@@ -330,7 +336,12 @@ def time_to_target(a, cfg, ctx, mode=None):
             if not h_reached and h_last[1] >= a.ttl_heldout_acc:
                 # training time only, like time_to_target_s (evaluations excluded)
                 h_reached, h_steps, h_time = True, steps, time.perf_counter() - t0 - eval_s
-        if reached and h_reached:
+            if h_last[1] > h_best + 1e-3:
+                h_best, h_best_step = h_last[1], steps
+            # (worker-mean values: every rank takes the same decision)
+            plateau = (reached and not h_reached and a.ttl_plateau_steps > 0
+                       and steps - h_best_step >= a.ttl_plateau_steps)
+        if reached and (h_reached or plateau):
             break
     _sync()
     t = time.perf_counter() - t0
@@ -342,6 +353,8 @@ def time_to_target(a, cfg, ctx, mode=None):
                     "ttl_heldout_acc": None if h_last[1] is None else round(h_last[1], 4),
                     "ttl_heldout_steps": h_steps, "ttl_heldout_reached": bool(h_reached),
                     "ttl_heldout_s": None if h_time is None else round(h_time, 3),
+                    "ttl_heldout_best_acc": round(h_best, 4) if h_best >= 0 else None,
+                    "ttl_heldout_plateau_stop": bool(plateau),
                     "ttl_eval_s": round(eval_s, 3)})
     return out
 
@@ -509,7 +522,8 @@ def run(a):
     # held-out fields are already worker means (identical on every worker); the
     # MAX brings them to rank 0 (the PS contributes -1 = "not a worker")
     held_keys = ("ttl_heldout_loss", "ttl_heldout_acc", "ttl_heldout_steps",
-                 "ttl_heldout_reached", "ttl_heldout_s", "ttl_eval_s")
+                 "ttl_heldout_reached", "ttl_heldout_s", "ttl_eval_s", "ttl_heldout_best_acc",
+                 "ttl_heldout_plateau_stop")
     held_vals = [-1.0 if not ttl or ttl.get(k) is None else float(ttl[k]) for k in held_keys]
     red = ctx.host_reduce([elapsed, -elapsed if elapsed else -1e30, ref_elapsed, final_loss,
                            *ttl_vals, *held_vals])
@@ -526,6 +540,9 @@ def run(a):
                 "ttl_heldout_reached": hv["ttl_heldout_reached"] > 0,
                 "ttl_heldout_s": None if hv["ttl_heldout_s"] < 0 else round(hv["ttl_heldout_s"], 3),
                 "ttl_eval_s": max(0.0, round(hv["ttl_eval_s"], 3)),
+                "ttl_heldout_best_acc": (None if hv["ttl_heldout_best_acc"] < 0
+                                         else round(hv["ttl_heldout_best_acc"], 4)),
+                "ttl_heldout_plateau_stop": hv["ttl_heldout_plateau_stop"] > 0,
                 "ttl_heldout_target_acc": a.ttl_heldout_acc})
     if ctx.is_ps:
         shape_src = ctx.host_reduce([0.0, 0.0, 0.0])      # matched by workers below

@@ -110,6 +110,19 @@ def test_bench_central_ps_with_time_to_target():
         assert out["ttl_heldout_steps"] % 50 == 0
 
 
+def test_bench_ttl_heldout_plateau_stop():
+    """Training-loss target reached, held-out target out of reach: the run stops
+    once the held-out accuracy has not improved for --ttl-plateau-steps."""
+    r, lines = _bench(["--gpus", "1", "--steps", "2", "--warmup", "1", "--model", "mlp",
+                       "--batch", "16", "--ttl-target", "5.0", "--ttl-max-steps", "3000",
+                       "--ttl-heldout-acc", "1.01", "--ttl-eval-every", "10",
+                       "--ttl-plateau-steps", "40", "--ref-batch", "0", "--ttl-compare-sync", "0"])
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads(lines[0])
+    assert out["ttl_reached"] and not out["ttl_heldout_reached"]
+    assert out["ttl_heldout_plateau_stop"] and 0.0 <= out["ttl_heldout_best_acc"] <= 1.0
+
+
 def test_bench_rejects_world_size_mismatch():
     r, _ = _bench(["--gpus", "3", "--steps", "1"],
                   env_extra={"RANK": "0", "WORLD_SIZE": "2", "LOCAL_RANK": "0"})
