@@ -17,4 +17,5 @@ python3 scripts/prof_steady.py $O/prof/r18_kernel_trace.csv --steps 15 --top 50 
 timeout -k 10 300 python bench.py --model vit_b16 --batch 64 --steps 30 --warmup 10 --ttl-target 0 --ref-batch 0 > $O/vit.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --model resnet50 --batch 128 --steps 30 --warmup 10 --ttl-target 0 --ref-batch 0 > $O/r50.log 2>&1 || exit $?
 for f in vit r50; do grep '^{' $O/$f.log | cut -c1-200; done
+bash scripts/gpu_prof_bs64.sh && cp gpurun_out/p64/steady.txt $O/steady_r18_bs64.txt
 exit 0
